@@ -1,0 +1,100 @@
+/*
+ * zseek_hip.h — GPU extensions of the MI355X-native libzseek (C ABI).
+ *
+ * Plain pointers and sizes only (no HIP or torch types): device pointers are
+ * hipMalloc'd (or torch-allocated) memory on the reader's device, and a
+ * stream is a hipStream_t passed as void* (NULL = the library's own stream).
+ *
+ * Reference interfaces these replace / extend:
+ *   zsk_lz4_decode_frames  — the per-frame LZ4F_decompress loop of
+ *                            /root/reference/src/decompress.c:752-773 (and
+ *                            :627-664 for the no-cache variant), batched over
+ *                            every frame of a request in one grid.
+ *   zsk_reader_frames      — the seek-table accessors frame_offset_c/d and
+ *                            frame_size_c/d, seek_table.c:204-226.
+ *   zsk_pread_device       — zseek_pread (decompress.c:806-824) with the
+ *                            decoded bytes left in device memory.
+ */
+#ifndef ZSEEK_HIP_H
+#define ZSEEK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "zseek.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One seek-table frame of a device batch. */
+typedef struct {
+    uint64_t c_off;   /* compressed frame start in d_comp                  */
+    uint64_t d_off;   /* decoded frame start in d_out                      */
+    uint32_t c_size;  /* compressed size (seek-table cSize)                */
+    uint32_t d_size;  /* decoded size (seek-table dSize); the frame writes */
+                      /* exactly [d_off, d_off + d_size) of d_out          */
+} zsk_frame_desc_t;
+
+/* Per-frame status codes written to d_status (low 16 bits).  Values 1..19
+ * follow liblz4's LZ4F error numbering (see zsk_status_string). */
+#define ZSK_OK 0
+#define ZSK_ERR_DST_OVERFLOW 100  /* frame decodes past its dSize        */
+#define ZSK_ERR_SHORT_FRAME 101   /* frame decodes to less than dSize    */
+#define ZSK_ERR_TRUNCATED 102     /* compressed frame ends mid-block     */
+#define ZSK_STATUS_DIRECT 0x10000 /* liblz4 would have used its direct path */
+
+/*
+ * Decode @nframes independent LZ4 frames on the GPU, asynchronously on
+ * @stream.  @d_desc, @d_comp, @d_out, @d_status are device pointers;
+ * @d_comp must stay readable up to the 4-byte boundary after the last
+ * compressed byte.  Each frame writes only its own [d_off, d_off+d_size).
+ * Returns 0 if the launch was queued, -1 otherwise.
+ */
+ZSEEK_EXPORT int zsk_lz4_decode_frames(const zsk_frame_desc_t *d_desc,
+    uint32_t nframes, const void *d_comp, void *d_out, int32_t *d_status,
+    void *stream);
+
+/* Human-readable name of a frame status (LZ4F-style "ERROR_..." names). */
+ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
+
+/* Number of frames of an open reader and its seek table as prefix sums:
+ * c_off/d_off receive n+1 entries each (either may be NULL). */
+ZSEEK_EXPORT ssize_t zsk_reader_frames(zseek_reader_t *reader,
+    uint64_t *c_off, uint64_t *d_off);
+
+/* Codec of an open reader (ZSEEK_LZ4 / ZSEEK_ZSTD), -1 for NULL. */
+ZSEEK_EXPORT int zsk_reader_type(zseek_reader_t *reader);
+
+/*
+ * zseek_pread into device memory @d_buf (on the reader's device): decoded
+ * bytes [offset, offset+count) are produced on the GPU and never cross PCIe.
+ * Same return convention as zseek_pread.  Synchronous.
+ */
+ZSEEK_EXPORT ssize_t zsk_pread_device(zseek_reader_t *reader, void *d_buf,
+    size_t count, size_t offset, void *call_data,
+    char errbuf[ZSEEK_ERRBUF_SIZE]);
+
+/* GPU-side counters of a reader. */
+typedef struct {
+    uint64_t batches;          /* decode grids launched                 */
+    uint64_t frames_decoded;   /* frames decoded on the GPU             */
+    uint64_t bytes_decoded;    /* decoded bytes produced on the GPU     */
+    uint64_t bytes_uploaded;   /* compressed bytes copied host->device  */
+    uint64_t device_memory;    /* device bytes held by the reader       */
+    int device;                /* HIP device ordinal, -1 before first use */
+} zsk_gpu_stats_t;
+
+ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader,
+    zsk_gpu_stats_t *stats);
+
+/* Largest decoded span one batch grid covers (bytes, default 256 MiB;
+ * env ZSEEK_HIP_BATCH_BYTES overrides at open). */
+ZSEEK_EXPORT bool zsk_reader_set_batch_bytes(zseek_reader_t *reader,
+    size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZSEEK_HIP_H */

@@ -1,0 +1,11 @@
+"""libzseek_amd — MI355X-native random-access decode path of libzseek.
+
+The product is the C-ABI shared library ``libzseek_amd/lib/libzseek.so``
+(include/zseek.h + include/zseek_hip.h); this package is its Python host
+mirror (``libzseek_amd.zseek``) used by tests and bench.py.
+"""
+from .zseek import (  # noqa: F401
+    ZSEEK_LZ4, ZSEEK_ZSTD, FRAME_DESC_DTYPE, LibraryNotBuilt, Reader, Writer, ZseekError,
+    decode_frames, frame_batch, lib, lz4_seekable, seek_table_of, status_string,
+    synth_buffer, tools, zstd_seekable,
+)

@@ -1,0 +1,102 @@
+// host.h — host-side building blocks of the reader (internal).
+#ifndef ZSK_HOST_H
+#define ZSK_HOST_H
+
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <list>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/zseek.h"
+#include "zsk_internal.h"
+
+namespace zsk {
+
+// Error formatting (ref src/common.c:29-54): vsnprintf into an 80-byte
+// caller buffer, no-op for NULL.
+void set_error(char *errbuf, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+void set_error_errno(char *errbuf, const char *msg, int errnum);
+
+// In-memory seek table as prefix sums (ref src/seek_table.c:36-47, 62-110).
+// SoA so a batch's descriptors are built with two subtractions per frame.
+struct SeekTable {
+    std::vector<uint64_t> c_off;   // n+1 entries, c_off[n] = total compressed
+    std::vector<uint64_t> d_off;   // n+1 entries, d_off[n] = total decoded
+    std::vector<uint32_t> checksum;   // n entries when the descriptor says so
+    bool checksum_flag = false;
+
+    size_t frames() const { return c_off.empty() ? 0 : c_off.size() - 1; }
+    uint64_t decompressed_size() const { return d_off.empty() ? 0 : d_off.back(); }
+    size_t memory_usage() const;
+    // Frame holding decompressed offset, -1 past the end (ref :187-202).
+    int64_t frame_of(uint64_t offset) const;
+    uint64_t csize(size_t i) const { return c_off[i + 1] - c_off[i]; }
+    uint64_t dsize(size_t i) const { return d_off[i + 1] - d_off[i]; }
+};
+
+// Parse the seekable-format footer/table through the user's callbacks with
+// the reference's validation (ref src/seek_table.c:112-176).  false on any
+// failure (the caller reports "read_seek_table failed").
+bool read_seek_table(const zseek_read_file_t &uf, void *call_data, SeekTable *st);
+
+// LRU of decoded frames keyed by frame index (ref src/cache.c): capacity in
+// frames, find() promotes to MRU, insert() evicts the LRU when full and takes
+// ownership of the frame bytes.
+class FrameCache {
+  public:
+    explicit FrameCache(size_t capacity) : capacity_(capacity) {}
+    ~FrameCache();
+    // nullptr when absent; on hit *len = frame size.
+    const uint8_t *find(size_t idx, size_t *len);
+    bool contains(size_t idx) const { return map_.count(idx) != 0; }
+    bool insert(size_t idx, uint8_t *data, size_t len);   // takes ownership
+    size_t entries() const { return lru_.size(); }
+    size_t memory_usage() const;
+    size_t capacity() const { return capacity_; }
+
+  private:
+    struct Entry {
+        size_t idx;
+        uint8_t *data;
+        size_t len;
+    };
+    size_t capacity_;
+    size_t bytes_ = 0;
+    std::list<Entry> lru_;   // front = LRU, back = MRU
+    std::unordered_map<size_t, std::list<Entry>::iterator> map_;
+};
+
+// Per-reader GPU context: one stream, device buffers and pinned staging
+// grown geometrically, created lazily at the first decode.
+struct DeviceCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t *d_comp = nullptr;
+    size_t d_comp_cap = 0;
+    uint8_t *d_out = nullptr;
+    size_t d_out_cap = 0;
+    FrameDesc *d_desc = nullptr;
+    size_t d_desc_cap = 0;   // frames
+    int32_t *d_status = nullptr;
+    size_t d_status_cap = 0;
+    uint8_t *h_comp = nullptr;   // pinned
+    size_t h_comp_cap = 0;
+    FrameDesc *h_desc = nullptr;   // pinned
+    size_t h_desc_cap = 0;
+    int32_t *h_status = nullptr;   // pinned
+    size_t h_status_cap = 0;
+    uint64_t batches = 0, frames_decoded = 0, bytes_decoded = 0, bytes_uploaded = 0;
+
+    ~DeviceCtx();
+    bool init(char *errbuf);
+    bool reserve(size_t comp, size_t out, size_t nframes, char *errbuf);
+    size_t device_bytes() const { return d_comp_cap + d_out_cap + d_desc_cap * 28; }
+    size_t host_bytes() const { return h_comp_cap + h_desc_cap * 28; }
+};
+
+}   // namespace zsk
+
+#endif

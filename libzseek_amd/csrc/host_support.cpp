@@ -1,0 +1,322 @@
+// host_support.cpp — error buffers, seek table, decoded-frame LRU, GPU
+// context.  Host C++ behind the C ABI of include/zseek.h.
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "host.h"
+
+namespace zsk {
+
+// ---------------------------------------------------------------------------
+// errors (ref src/common.c:29-54)
+// ---------------------------------------------------------------------------
+void set_error(char *errbuf, const char *fmt, ...)
+{
+    if (!errbuf)
+        return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(errbuf, ZSEEK_ERRBUF_SIZE, fmt, ap);
+    va_end(ap);
+}
+
+void set_error_errno(char *errbuf, const char *msg, int errnum)
+{
+    char tmp[1024];
+    const char *s = strerror_r(errnum, tmp, sizeof(tmp));   // GNU variant
+    if (!msg || !*msg)
+        set_error(errbuf, "%s", s);
+    else
+        set_error(errbuf, "%s: %s", msg, s);
+}
+
+// ---------------------------------------------------------------------------
+// seek table (ref src/seek_table.c:15-23 constants, :62-176 parse)
+// ---------------------------------------------------------------------------
+namespace {
+constexpr uint32_t kFooter = 9;
+constexpr uint32_t kSeekMagic = 0x8F92EAB1u;
+constexpr uint32_t kSkippableMagic = 0x184D2A5Eu;   // ZSTD_MAGIC_SKIPPABLE_START | 0xE
+constexpr uint32_t kSkippableHdr = 8;
+constexpr uint64_t kChunk = 1u << 20;   // entries read per callback (1 MiB)
+
+inline uint32_t le32(const uint8_t *p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+           ((uint32_t)p[3] << 24);
+}
+}   // namespace
+
+size_t SeekTable::memory_usage() const
+{
+    return sizeof(*this) + c_off.capacity() * sizeof(uint64_t) +
+           d_off.capacity() * sizeof(uint64_t) + checksum.capacity() * sizeof(uint32_t);
+}
+
+int64_t SeekTable::frame_of(uint64_t offset) const
+{
+    size_t n = frames();
+    if (n == 0 || offset >= d_off[n])
+        return -1;
+    // last frame whose start is <= offset (same answer as the reference's
+    // lo/hi bisection, including zero-size frames)
+    size_t lo = 0, hi = n;
+    while (lo + 1 < hi) {
+        size_t mid = lo + (hi - lo) / 2;
+        if (d_off[mid] <= offset)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return (int64_t)lo;
+}
+
+bool read_seek_table(const zseek_read_file_t &uf, void *call_data, SeekTable *st)
+{
+    ssize_t fsize = uf.fsize(uf.user_data, call_data);
+    if (fsize < (ssize_t)kFooter)
+        return false;
+    uint8_t footer[kFooter];
+    if (uf.pread(footer, kFooter, (size_t)fsize - kFooter, uf.user_data, call_data) !=
+        (ssize_t)kFooter)
+        return false;
+    if (le32(footer + 5) != kSeekMagic)
+        return false;
+    uint8_t desc = footer[4];
+    if (desc & 0x7c)   // reserved descriptor bits
+        return false;
+    const bool ck = (desc & 0x80) != 0;
+    const uint64_t n = le32(footer);
+    const uint64_t esize = 8 + (ck ? 4 : 0);
+    const uint64_t frame_size = kSkippableHdr + n * esize + kFooter;
+    if (frame_size > (uint64_t)fsize)
+        return false;
+    const uint64_t table_at = (uint64_t)fsize - frame_size;
+    uint8_t hdr[kSkippableHdr];
+    if (uf.pread(hdr, kSkippableHdr, table_at, uf.user_data, call_data) !=
+        (ssize_t)kSkippableHdr)
+        return false;
+    if (le32(hdr) != kSkippableMagic || le32(hdr + 4) != frame_size - kSkippableHdr)
+        return false;
+
+    st->checksum_flag = ck;
+    st->c_off.assign(n + 1, 0);
+    st->d_off.assign(n + 1, 0);
+    st->checksum.assign(ck ? n : 0, 0);
+    std::vector<uint8_t> buf;
+    uint64_t c = 0, d = 0, pos = table_at + kSkippableHdr;
+    for (uint64_t e = 0; e < n;) {
+        uint64_t m = n - e < kChunk ? n - e : kChunk;
+        buf.resize(m * esize);
+        if (uf.pread(buf.data(), buf.size(), pos, uf.user_data, call_data) !=
+            (ssize_t)buf.size())
+            return false;
+        pos += buf.size();
+        const uint8_t *p = buf.data();
+        for (uint64_t k = 0; k < m; k++, e++, p += esize) {
+            st->c_off[e] = c;
+            st->d_off[e] = d;
+            c += le32(p);
+            d += le32(p + 4);
+            if (ck)
+                st->checksum[e] = le32(p + 8);
+        }
+    }
+    st->c_off[n] = c;
+    st->d_off[n] = d;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// decoded-frame LRU (ref src/cache.c:52-176)
+// ---------------------------------------------------------------------------
+FrameCache::~FrameCache()
+{
+    for (auto &e : lru_)
+        free(e.data);
+}
+
+const uint8_t *FrameCache::find(size_t idx, size_t *len)
+{
+    auto it = map_.find(idx);
+    if (it == map_.end())
+        return nullptr;
+    lru_.splice(lru_.end(), lru_, it->second);   // promote to MRU
+    *len = it->second->len;
+    return it->second->data;
+}
+
+bool FrameCache::insert(size_t idx, uint8_t *data, size_t len)
+{
+    if (capacity_ == 0)
+        return false;
+    auto it = map_.find(idx);
+    if (it != map_.end()) {   // refresh an existing entry
+        bytes_ -= it->second->len;
+        free(it->second->data);
+        it->second->data = data;
+        it->second->len = len;
+        bytes_ += len;
+        lru_.splice(lru_.end(), lru_, it->second);
+        return true;
+    }
+    if (lru_.size() == capacity_) {
+        Entry &old = lru_.front();
+        bytes_ -= old.len;
+        free(old.data);
+        map_.erase(old.idx);
+        lru_.pop_front();
+    }
+    lru_.push_back(Entry{idx, data, len});
+    map_[idx] = std::prev(lru_.end());
+    bytes_ += len;
+    return true;
+}
+
+size_t FrameCache::memory_usage() const
+{
+    // object + one list node and one hash node per entry + frame bytes
+    return sizeof(*this) + lru_.size() * (sizeof(Entry) + 2 * sizeof(void *)) +
+           map_.size() * (sizeof(size_t) + 3 * sizeof(void *)) + bytes_;
+}
+
+// ---------------------------------------------------------------------------
+// GPU context
+// ---------------------------------------------------------------------------
+DeviceCtx::~DeviceCtx()
+{
+    if (device < 0)
+        return;
+    (void)hipSetDevice(device);
+    if (stream)
+        (void)hipStreamSynchronize(stream);
+    (void)hipFree(d_comp);
+    (void)hipFree(d_out);
+    (void)hipFree(d_desc);
+    (void)hipFree(d_status);
+    (void)hipHostFree(h_comp);
+    (void)hipHostFree(h_desc);
+    (void)hipHostFree(h_status);
+    if (stream)
+        (void)hipStreamDestroy(stream);
+}
+
+bool DeviceCtx::init(char *errbuf)
+{
+    if (device >= 0)
+        return true;
+    int dev = 0;
+    const char *env = getenv("ZSEEK_HIP_DEVICE");
+    if (env && *env) {
+        dev = atoi(env);
+    } else if (hipGetDevice(&dev) != hipSuccess) {
+        dev = 0;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error(errbuf, "no HIP device available");
+        return false;
+    }
+    if (dev < 0 || dev >= count || hipSetDevice(dev) != hipSuccess) {
+        set_error(errbuf, "invalid HIP device %d", dev);
+        return false;
+    }
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error(errbuf, "create HIP stream failed");
+        return false;
+    }
+    device = dev;
+    return true;
+}
+
+namespace {
+template <typename T>
+bool grow_dev(T **p, size_t *cap, size_t want_elems)
+{
+    if (want_elems <= *cap)
+        return true;
+    size_t n = *cap * 2 > want_elems ? *cap * 2 : want_elems;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    // +256 B: readable tail for the 4-byte-granular input window
+    if (hipMalloc((void **)p, n * sizeof(T) + 256) != hipSuccess)
+        return false;
+    *cap = n;
+    return true;
+}
+
+template <typename T>
+bool grow_host(T **p, size_t *cap, size_t want_elems)
+{
+    if (want_elems <= *cap)
+        return true;
+    size_t n = *cap * 2 > want_elems ? *cap * 2 : want_elems;
+    (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipHostMalloc((void **)p, n * sizeof(T) + 256, hipHostMallocDefault) != hipSuccess)
+        return false;
+    *cap = n;
+    return true;
+}
+}   // namespace
+
+bool DeviceCtx::reserve(size_t comp, size_t out, size_t nframes, char *errbuf)
+{
+    (void)hipSetDevice(device);
+    if (!grow_dev(&d_comp, &d_comp_cap, comp) || !grow_dev(&d_out, &d_out_cap, out) ||
+        !grow_dev(&d_desc, &d_desc_cap, nframes) ||
+        !grow_dev(&d_status, &d_status_cap, nframes)) {
+        set_error(errbuf, "allocate GPU decode buffers failed");
+        return false;
+    }
+    if (!grow_host(&h_comp, &h_comp_cap, comp) || !grow_host(&h_desc, &h_desc_cap, nframes) ||
+        !grow_host(&h_status, &h_status_cap, nframes)) {
+        set_error(errbuf, "allocate pinned staging failed");
+        return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// status names (LZ4F_getErrorName strings of liblz4 1.9.3 for 1..19)
+// ---------------------------------------------------------------------------
+const char *status_name(int32_t st)
+{
+    static const char *const names[] = {
+        "OK_NoError", "ERROR_GENERIC", "ERROR_maxBlockSize_invalid",
+        "ERROR_blockMode_invalid", "ERROR_contentChecksumFlag_invalid",
+        "ERROR_compressionLevel_invalid", "ERROR_headerVersion_wrong",
+        "ERROR_blockChecksum_invalid", "ERROR_reservedFlag_set",
+        "ERROR_allocation_failed", "ERROR_srcSize_tooLarge",
+        "ERROR_dstMaxSize_tooSmall", "ERROR_frameHeader_incomplete",
+        "ERROR_frameType_unknown", "ERROR_frameSize_wrong", "ERROR_srcPtr_wrong",
+        "ERROR_decompressionFailed", "ERROR_headerChecksum_invalid",
+        "ERROR_contentChecksum_invalid", "ERROR_frameDecoding_alreadyStarted",
+    };
+    int32_t code = st & 0xFFFF;
+    if (code >= 0 && code < (int32_t)(sizeof(names) / sizeof(names[0])))
+        return names[code];
+    switch (code) {
+    case ST_DST_OVERFLOW:
+        return "decoded data exceeds frame size";
+    case ST_SHORT_FRAME:
+        return "decoded data shorter than frame size";
+    case ST_TRUNCATED:
+        return "truncated frame";
+    case ST_UNSUPPORTED:
+        return "unsupported frame";
+    case ST_NOT_RUN:
+        return "decoder did not run";
+    default:
+        return "Unspecified error code";
+    }
+}
+
+}   // namespace zsk

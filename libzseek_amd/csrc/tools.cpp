@@ -1,0 +1,202 @@
+// tools.cpp — bench/test input tooling (libzseek_tools.so), not the hot path.
+//
+//   zsk_tool_synth          the SURVEY.md §8d synthetic buffer(N): 64 MiB
+//                           chunks gen(64 MiB, seed = 1 + chunk), generated in
+//                           parallel (chunks are independent).
+//   zsk_tool_lz4_seekable   a seekable LZ4 file image of a buffer, frames
+//                           compressed in parallel with liblz4 exactly as the
+//                           reference writer's direct path does when every
+//                           zseek_write is frame_size bytes
+//                           (/root/reference/src/compress.c:737-786: prefs
+//                           {level, autoFlush=1, max64KB}, no content size;
+//                           a final short frame goes through the buffered path
+//                           and carries its content size, :463-518).
+//   zsk_tool_zstd_seekable  same for zstd (ZSTD_compress2, level/strategy as
+//                           compress.c:58-91, single worker).
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <thread>
+#include <vector>
+
+#include <lz4frame.h>
+#include <zstd.h>
+
+#define ZSK_TOOL extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr size_t kSynthChunk = 64u << 20;
+
+void gen(uint8_t *out, size_t n, uint64_t seed)
+{
+    uint64_t s = seed;
+    auto next = [&s]() {
+        s += 0x9E3779B97F4A7C15ULL;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        return z ^ (z >> 31);
+    };
+    size_t i = 0;
+    while (i < n) {
+        uint64_t r = next();
+        if (i >= 65536 && r % 100 < 52) {
+            size_t len = 4 + (size_t)((r >> 8) % 69);
+            size_t off = 1 + (size_t)((r >> 24) % 8192);
+            if (off > i)
+                off = i;
+            for (size_t k = 0; k < len && i < n; k++, i++)
+                out[i] = out[i - off];
+        } else {
+            size_t len = 1 + (size_t)((r >> 8) % 48);
+            for (size_t k = 0; k < len && i < n; k++, i++)
+                out[i] = (uint8_t)(0x20 + next() % 64);
+        }
+    }
+}
+
+template <typename F>
+void parallel_for(size_t n, int threads, F fn)
+{
+    if (threads < 1)
+        threads = 1;
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; t++)
+        pool.emplace_back([&]() {
+            for (size_t i; (i = next.fetch_add(1)) < n;)
+                fn(i);
+        });
+    for (auto &th : pool)
+        th.join();
+}
+
+void put32(uint8_t *p, uint32_t v)
+{
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p[2] = (uint8_t)(v >> 16);
+    p[3] = (uint8_t)(v >> 24);
+}
+
+// frames compressed into per-frame slots, then packed + seek table appended
+template <typename Compress>
+int seekable(const uint8_t *in, size_t n, size_t frame_size, int threads, size_t slot,
+             uint8_t *out, size_t out_cap, size_t *out_len, Compress compress)
+{
+    if (frame_size == 0)
+        return -1;
+    size_t nf = (n + frame_size - 1) / frame_size;
+    std::vector<uint8_t> tmp(nf * slot);
+    std::vector<size_t> csize(nf, 0);
+    std::atomic<int> bad{0};
+    parallel_for(nf, threads, [&](size_t i) {
+        size_t a = i * frame_size, len = n - a < frame_size ? n - a : frame_size;
+        size_t c = compress(tmp.data() + i * slot, slot, in + a, len, len < frame_size);
+        if (c == 0)
+            bad = 1;
+        csize[i] = c;
+    });
+    if (bad)
+        return -1;
+    size_t total = 0;
+    for (size_t c : csize)
+        total += c;
+    size_t table = 8 + 8 * nf + 9;
+    if (total + table > out_cap)
+        return -1;
+    size_t at = 0;
+    for (size_t i = 0; i < nf; i++) {
+        memcpy(out + at, tmp.data() + i * slot, csize[i]);
+        at += csize[i];
+    }
+    uint8_t *t = out + at;
+    put32(t, 0x184D2A5Eu);
+    put32(t + 4, (uint32_t)(table - 8));
+    for (size_t i = 0; i < nf; i++) {
+        size_t a = i * frame_size, len = n - a < frame_size ? n - a : frame_size;
+        put32(t + 8 + 8 * i, (uint32_t)csize[i]);
+        put32(t + 12 + 8 * i, (uint32_t)len);
+    }
+    put32(t + 8 + 8 * nf, (uint32_t)nf);
+    t[12 + 8 * nf] = 0;
+    put32(t + 13 + 8 * nf, 0x8F92EAB1u);
+    *out_len = at + table;
+    return 0;
+}
+
+LZ4F_preferences_t lz4_prefs(int level, size_t content)
+{
+    LZ4F_preferences_t p;
+    memset(&p, 0, sizeof(p));
+    p.compressionLevel = level;
+    p.autoFlush = 1;
+    p.frameInfo.blockSizeID = LZ4F_max64KB;
+    p.frameInfo.contentSize = content;
+    return p;
+}
+
+}   // namespace
+
+ZSK_TOOL void zsk_tool_synth(uint8_t *out, size_t n, int threads)
+{
+    size_t chunks = (n + kSynthChunk - 1) / kSynthChunk;
+    parallel_for(chunks, threads, [&](size_t c) {
+        size_t a = c * kSynthChunk;
+        gen(out + a, n - a < kSynthChunk ? n - a : kSynthChunk, 1 + c);
+    });
+}
+
+ZSK_TOOL void zsk_tool_gen(uint8_t *out, size_t n, uint64_t seed)
+{
+    gen(out, n, seed);
+}
+
+ZSK_TOOL size_t zsk_tool_lz4_seekable_bound(size_t n, size_t frame_size)
+{
+    LZ4F_preferences_t p = lz4_prefs(0, frame_size);
+    size_t nf = frame_size ? (n + frame_size - 1) / frame_size : 0;
+    return nf * LZ4F_compressFrameBound(frame_size, &p) + 8 + 8 * nf + 9;
+}
+
+ZSK_TOOL int zsk_tool_lz4_seekable(const uint8_t *in, size_t n, size_t frame_size, int level,
+                                   int threads, uint8_t *out, size_t out_cap, size_t *out_len)
+{
+    LZ4F_preferences_t pb = lz4_prefs(level, frame_size);
+    size_t slot = LZ4F_compressFrameBound(frame_size, &pb);
+    return seekable(in, n, frame_size, threads, slot, out, out_cap, out_len,
+                    [level](uint8_t *dst, size_t cap, const uint8_t *src, size_t len,
+                            bool last_short) -> size_t {
+                        LZ4F_preferences_t p = lz4_prefs(level, last_short ? len : 0);
+                        size_t c = LZ4F_compressFrame(dst, cap, src, len, &p);
+                        return LZ4F_isError(c) ? 0 : c;
+                    });
+}
+
+ZSK_TOOL size_t zsk_tool_zstd_seekable_bound(size_t n, size_t frame_size)
+{
+    size_t nf = frame_size ? (n + frame_size - 1) / frame_size : 0;
+    return nf * ZSTD_compressBound(frame_size) + 8 + 8 * nf + 9;
+}
+
+ZSK_TOOL int zsk_tool_zstd_seekable(const uint8_t *in, size_t n, size_t frame_size, int level,
+                                    int strategy, int threads, uint8_t *out, size_t out_cap,
+                                    size_t *out_len)
+{
+    size_t slot = ZSTD_compressBound(frame_size);
+    return seekable(in, n, frame_size, threads, slot, out, out_cap, out_len,
+                    [level, strategy](uint8_t *dst, size_t cap, const uint8_t *src, size_t len,
+                                      bool) -> size_t {
+                        thread_local ZSTD_CCtx *cctx = nullptr;
+                        if (!cctx)
+                            cctx = ZSTD_createCCtx();
+                        ZSTD_CCtx_reset(cctx, ZSTD_reset_session_and_parameters);
+                        ZSTD_CCtx_setParameter(cctx, ZSTD_c_compressionLevel, level);
+                        ZSTD_CCtx_setParameter(cctx, ZSTD_c_strategy, strategy);
+                        size_t c = ZSTD_compress2(cctx, dst, cap, src, len);
+                        return ZSTD_isError(c) ? 0 : c;
+                    });
+}

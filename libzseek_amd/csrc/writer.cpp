@@ -1,0 +1,356 @@
+// writer.cpp — zseek_writer_* (sequential writer of seekable LZ4 / zstd files).
+//
+// Out of the GPU hot path: kept so the library stays a
+// drop-in for the reference's full C API and so tests/bench can produce
+// inputs.  Frames are compressed on the host with the same liblz4 / libzstd
+// calls and parameters as the reference (/root/reference/src/compress.c), so
+// the files are byte-identical to the reference writer's for the same write
+// sequence.  One reference defect is not reproduced: a short buffered write
+// followed by a write >= min_frame_size (compress.c:791-795 checks frame_cm,
+// which LZ4 never sets) logs a frame with a stale dSize and corrupts the file;
+// here buffered bytes always end their frame first.
+#include <errno.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include <lz4frame.h>
+#include <zstd.h>
+
+#include "../../include/zseek.h"
+#include "host.h"
+
+using namespace zsk;
+
+namespace {
+constexpr uint32_t kMaxFrames = 0x8000000u;   // ZSTD_SEEKABLE_MAXFRAMES (ref seek_table.c:17)
+
+struct FrameLogEntry {
+    uint32_t c_size, d_size;
+};
+}   // namespace
+
+struct zseek_writer {
+    zseek_write_file_t user_file;
+    zseek_compression_type_t type;
+    ZSTD_CCtx *cctx = nullptr;
+    bool mt = false;
+    LZ4F_preferences_t prefs;
+    size_t frame_uc = 0;   // current frame, uncompressed bytes
+    size_t frame_cm = 0;   // current frame, compressed bytes already written
+    size_t min_frame_size = 0;
+    size_t total_cm = 0;
+    std::vector<FrameLogEntry> log;
+    std::vector<uint8_t> ubuf, cbuf;
+};
+
+static bool default_write(const void *data, size_t size, void *user_data, void *call_data)
+{
+    (void)call_data;
+    return fwrite(data, 1, size, (FILE *)user_data) == size;
+}
+
+static bool log_frame(zseek_writer *w, char *errbuf)
+{
+    if (w->log.size() == kMaxFrames) {
+        set_error(errbuf, "log frame: Frame index is too large");
+        return false;
+    }
+    w->log.push_back(FrameLogEntry{(uint32_t)w->frame_cm, (uint32_t)w->frame_uc});
+    w->total_cm += w->frame_cm;
+    w->frame_uc = 0;
+    w->frame_cm = 0;
+    return true;
+}
+
+static bool emit(zseek_writer *w, const void *p, size_t n, void *call_data, char *errbuf)
+{
+    if (!w->user_file.write(p, n, w->user_file.user_data, call_data)) {
+        set_error(errbuf, "write to file failed");
+        return false;
+    }
+    return true;
+}
+
+// One LZ4 frame of src (ref compress.c:463-518 buffered, :737-786 direct).
+// content_size = 0 omits the content-size field, as the reference's direct
+// path does.
+static bool lz4_frame(zseek_writer *w, const void *src, size_t n, size_t content_size,
+                      void *call_data, char *errbuf)
+{
+    w->prefs.frameInfo.contentSize = content_size;
+    size_t bound = LZ4F_compressFrameBound(n, &w->prefs);
+    w->cbuf.resize(bound);
+    size_t c = LZ4F_compressFrame(w->cbuf.data(), bound, src, n, &w->prefs);
+    if (LZ4F_isError(c)) {
+        set_error(errbuf, "%s: %s", "compress frame", LZ4F_getErrorName(c));
+        return false;
+    }
+    w->frame_uc += n;
+    w->frame_cm += c;
+    return emit(w, w->cbuf.data(), c, call_data, errbuf) && log_frame(w, errbuf);
+}
+
+static bool zstd_frame(zseek_writer *w, const void *src, size_t n, void *call_data,
+                       char *errbuf)
+{
+    size_t bound = ZSTD_compressBound(n);
+    w->cbuf.resize(bound);
+    size_t c = ZSTD_compress2(w->cctx, w->cbuf.data(), bound, src, n);
+    if (ZSTD_isError(c)) {
+        set_error(errbuf, "%s: %s", "compress frame", ZSTD_getErrorName(c));
+        return false;
+    }
+    w->frame_uc += n;
+    w->frame_cm += c;
+    return emit(w, w->cbuf.data(), c, call_data, errbuf) && log_frame(w, errbuf);
+}
+
+// End the buffered frame (ref end_frame_lz4 :463-518, end_frame_zstd :338-394,
+// end_frame_zstd_mt :281-333).
+static bool end_frame(zseek_writer *w, void *call_data, char *errbuf)
+{
+    if (w->type == ZSEEK_LZ4) {
+        size_t n = w->ubuf.size();
+        w->frame_uc = 0;
+        bool ok = lz4_frame(w, w->ubuf.data(), n, n, call_data, errbuf);
+        w->ubuf.clear();
+        return ok;
+    }
+    if (!w->mt) {
+        size_t n = w->ubuf.size();
+        w->frame_uc = 0;
+        bool ok = zstd_frame(w, w->ubuf.data(), n, call_data, errbuf);
+        w->ubuf.clear();
+        return ok;
+    }
+    size_t out_len = ZSTD_CStreamOutSize();
+    w->cbuf.resize(out_len);
+    ZSTD_inBuffer in = {nullptr, 0, 0};
+    size_t rem;
+    do {
+        ZSTD_outBuffer out = {w->cbuf.data(), out_len, 0};
+        rem = ZSTD_compressStream2(w->cctx, &out, &in, ZSTD_e_end);
+        if (ZSTD_isError(rem)) {
+            set_error(errbuf, "%s: %s", "compress", ZSTD_getErrorName(rem));
+            return false;
+        }
+        w->frame_cm += out.pos;
+        if (!emit(w, w->cbuf.data(), out.pos, call_data, errbuf))
+            return false;
+    } while (rem > 0);
+    return log_frame(w, errbuf);
+}
+
+extern "C" ZSEEK_EXPORT zseek_writer_t *zseek_writer_open_full(zseek_write_file_t user_file,
+                                                               zseek_compression_param_t *zsp,
+                                                               size_t min_frame_size,
+                                                               void *call_data, char *errbuf)
+{
+    (void)call_data;
+    zseek_compression_type_t type = zsp ? zsp->type : ZSEEK_ZSTD;   // ref :252-255
+    if (type != ZSEEK_ZSTD && type != ZSEEK_LZ4) {
+        set_error(errbuf, "wrong compression type (%d)", (int)type);
+        return nullptr;
+    }
+    zseek_writer *w = new (std::nothrow) zseek_writer();
+    if (!w) {
+        set_error_errno(errbuf, "allocate writer", ENOMEM);
+        return nullptr;
+    }
+    w->user_file = user_file;
+    w->type = type;
+    w->min_frame_size = min_frame_size;
+    memset(&w->prefs, 0, sizeof(w->prefs));
+    if (type == ZSEEK_LZ4) {
+        // ref compress.c:203-207
+        w->prefs.compressionLevel = zsp ? zsp->params.lz4_params.compression_level : 0;
+        w->prefs.autoFlush = 1;
+        w->prefs.frameInfo.blockSizeID = LZ4F_max64KB;
+        w->ubuf.reserve(min_frame_size);
+        return w;
+    }
+    int level = zsp ? zsp->params.zstd_params.compression_level : ZSTD_CLEVEL_DEFAULT;
+    int strategy = zsp ? zsp->params.zstd_params.strategy : (int)ZSTD_fast;
+    w->cctx = ZSTD_createCCtx();
+    if (!w->cctx) {
+        set_error(errbuf, "context creation failed");
+        delete w;
+        return nullptr;
+    }
+    size_t r = ZSTD_CCtx_setParameter(w->cctx, ZSTD_c_compressionLevel, level);
+    if (ZSTD_isError(r)) {
+        set_error(errbuf, "%s: %s", "set compression level", ZSTD_getErrorName(r));
+        goto fail;
+    }
+    r = ZSTD_CCtx_setParameter(w->cctx, ZSTD_c_strategy, strategy);
+    if (ZSTD_isError(r)) {
+        set_error(errbuf, "%s: %s", "set strategy", ZSTD_getErrorName(r));
+        goto fail;
+    }
+    if (zsp && zsp->params.zstd_params.nb_workers > 1) {
+        r = ZSTD_CCtx_setParameter(w->cctx, ZSTD_c_nbWorkers, zsp->params.zstd_params.nb_workers);
+        if (ZSTD_isError(r)) {
+            set_error(errbuf, "%s: %s", "set nb of workers", ZSTD_getErrorName(r));
+            goto fail;
+        }
+        if (zsp->params.zstd_params.cpuset) {
+            // create the worker pool while pinned to the caller's cpuset
+            // (ref compress.c:105-139)
+            pthread_t self = pthread_self();
+            cpu_set_t prev;
+            int pr = pthread_getaffinity_np(self, sizeof(prev), &prev);
+            if (pr) {
+                set_error_errno(errbuf, "get thread affinity", pr);
+                goto fail;
+            }
+            pthread_setaffinity_np(self, zsp->params.zstd_params.cpusetsize,
+                                   zsp->params.zstd_params.cpuset);
+            ZSTD_inBuffer in = {nullptr, 0, 0};
+            ZSTD_outBuffer out = {nullptr, 0, 0};
+            r = ZSTD_compressStream2(w->cctx, &out, &in, ZSTD_e_continue);
+            pthread_setaffinity_np(self, sizeof(prev), &prev);
+            if (ZSTD_isError(r)) {
+                set_error(errbuf, "%s: %s", "create threads", ZSTD_getErrorName(r));
+                goto fail;
+            }
+        }
+        w->mt = true;
+    }
+    w->ubuf.reserve(min_frame_size);
+    return w;
+fail:
+    ZSTD_freeCCtx(w->cctx);
+    delete w;
+    return nullptr;
+}
+
+extern "C" ZSEEK_EXPORT zseek_writer_t *zseek_writer_open(FILE *cfile,
+                                                          zseek_compression_param_t *zsp,
+                                                          size_t min_frame_size, void *call_data,
+                                                          char *errbuf)
+{
+    zseek_write_file_t uf = {cfile, default_write};
+    return zseek_writer_open_full(uf, zsp, min_frame_size, call_data, errbuf);
+}
+
+static bool write_mt(zseek_writer *w, const void *buf, size_t len, void *call_data,
+                     char *errbuf)
+{
+    // ref compress.c:599-648: end the previous frame lazily, then stream
+    if (w->frame_uc >= w->min_frame_size && !end_frame(w, call_data, errbuf)) {
+        set_error(errbuf, "end_frame_zstd failed");
+        return false;
+    }
+    size_t out_len = ZSTD_compressBound(len);
+    w->cbuf.resize(out_len);
+    ZSTD_inBuffer in = {buf, len, 0};
+    do {
+        ZSTD_outBuffer out = {w->cbuf.data(), out_len, 0};
+        size_t rem = ZSTD_compressStream2(w->cctx, &out, &in, ZSTD_e_continue);
+        if (ZSTD_isError(rem)) {
+            set_error(errbuf, "%s: %s", "compress", ZSTD_getErrorName(rem));
+            return false;
+        }
+        w->frame_cm += out.pos;
+        if (!emit(w, w->cbuf.data(), out.pos, call_data, errbuf))
+            return false;
+    } while (in.pos < in.size);
+    w->frame_uc += len;
+    return true;
+}
+
+extern "C" ZSEEK_EXPORT bool zseek_write(zseek_writer_t *w, const void *buf, size_t len,
+                                         void *call_data, char *errbuf)
+{
+    if (!w) {
+        set_error(errbuf, "invalid writer");
+        return false;
+    }
+    if (w->type == ZSEEK_ZSTD && w->mt)
+        return write_mt(w, buf, len, call_data, errbuf);
+    if (w->ubuf.empty() && len >= w->min_frame_size) {
+        // compress straight from the caller's buffer (ref :710-714, :791-795)
+        return w->type == ZSEEK_LZ4 ? lz4_frame(w, buf, len, 0, call_data, errbuf)
+                                    : zstd_frame(w, buf, len, call_data, errbuf);
+    }
+    if (len)
+        w->ubuf.insert(w->ubuf.end(), (const uint8_t *)buf, (const uint8_t *)buf + len);
+    w->frame_uc += len;
+    if (w->frame_uc >= w->min_frame_size && !end_frame(w, call_data, errbuf)) {
+        set_error(errbuf, w->type == ZSEEK_LZ4 ? "end_frame_lz4 failed" : "end_frame_zstd failed");
+        return false;
+    }
+    return true;
+}
+
+static size_t seek_table_size(size_t frames)
+{
+    return 8 + 8 * frames + 9;
+}
+
+extern "C" ZSEEK_EXPORT bool zseek_writer_close(zseek_writer_t *w, void *call_data, char *errbuf)
+{
+    if (!w)
+        return true;
+    bool ok = true;
+    if (w->frame_uc > 0 && !end_frame(w, call_data, errbuf)) {
+        set_error(errbuf, w->type == ZSEEK_LZ4 ? "end_frame_lz4 failed" : "end_frame_zstd failed");
+        ok = false;
+    }
+    // seekable-format seek table (ref seek_table.c:365-419): skippable
+    // header, n x {cSize, dSize}, n, descriptor 0 (no checksums), magic
+    std::vector<uint8_t> t(seek_table_size(w->log.size()));
+    auto put32 = [&](size_t at, uint32_t v) {
+        t[at] = (uint8_t)v;
+        t[at + 1] = (uint8_t)(v >> 8);
+        t[at + 2] = (uint8_t)(v >> 16);
+        t[at + 3] = (uint8_t)(v >> 24);
+    };
+    put32(0, 0x184D2A5Eu);
+    put32(4, (uint32_t)(t.size() - 8));
+    size_t at = 8;
+    for (const FrameLogEntry &e : w->log) {
+        put32(at, e.c_size);
+        put32(at + 4, e.d_size);
+        at += 8;
+    }
+    put32(at, (uint32_t)w->log.size());
+    t[at + 4] = 0;
+    put32(at + 5, 0x8F92EAB1u);
+    if (!w->user_file.write(t.data(), t.size(), w->user_file.user_data, call_data) && ok) {
+        set_error(errbuf, "write to file failed");
+        ok = false;
+    }
+    ZSTD_freeCCtx(w->cctx);
+    delete w;
+    return ok;
+}
+
+extern "C" ZSEEK_EXPORT bool zseek_writer_stats(zseek_writer_t *w, zseek_writer_stats_t *stats,
+                                                char *errbuf)
+{
+    if (!w) {
+        set_error(errbuf, "invalid writer");
+        return false;
+    }
+    if (!stats) {
+        set_error(errbuf, "invalid stats pointer");
+        return false;
+    }
+    // ref compress.c:835-881
+    size_t frames = w->log.size() + (w->frame_uc > 0 ? 1 : 0);
+    stats->seek_table_size = seek_table_size(w->log.size()) + (w->frame_uc > 0 ? 8 : 0);
+    stats->seek_table_memory = sizeof(w->log) + w->log.capacity() * sizeof(FrameLogEntry);
+    stats->frames = frames;
+    stats->compressed_size = w->total_cm + w->frame_cm + stats->seek_table_size;
+    size_t buffered = w->ubuf.capacity() + w->cbuf.capacity();
+    if (w->type == ZSEEK_ZSTD)
+        buffered += ZSTD_sizeof_CCtx(w->cctx);
+    stats->buffer_size = buffered;
+    return true;
+}

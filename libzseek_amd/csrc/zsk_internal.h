@@ -1,0 +1,58 @@
+// zsk_internal.h — shared between the host reader and the HIP kernels.
+// Not installed; the public C ABI lives in include/zseek.h and
+// include/zseek_hip.h.
+#ifndef ZSK_INTERNAL_H
+#define ZSK_INTERNAL_H
+
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+namespace zsk {
+
+// One seek-table frame of a batch (layout shared with zsk_frame_desc_t in
+// include/zseek_hip.h).
+struct FrameDesc {
+    uint64_t c_off;    // compressed frame offset in the batch's input span
+    uint64_t d_off;    // decoded frame offset in the batch's output span
+    uint32_t c_size;   // seek-table cSize
+    uint32_t d_size;   // seek-table dSize
+};
+static_assert(sizeof(FrameDesc) == 24, "FrameDesc is part of the C ABI");
+
+// Per-frame status.  Low 16 bits: liblz4 LZ4F error code numbering
+// (lz4frame.h LZ4F_LIST_ERRORS, 0 = OK) or one of the zseek-specific codes
+// >= 100.  Bit 16: the failing block would have been decoded by liblz4
+// straight into the destination (its "direct" path, which reports
+// ERROR_GENERIC) — used to reproduce the reference's error strings.
+enum : int32_t {
+    ST_OK = 0,
+    ST_GENERIC = 1,
+    ST_MAXBLOCK = 2,
+    ST_VERSION = 6,
+    ST_BLOCK_CHECKSUM = 7,
+    ST_RESERVED = 8,
+    ST_HDR_INCOMPLETE = 12,
+    ST_FRAME_TYPE = 13,
+    ST_FRAME_SIZE = 14,
+    ST_DECOMPRESS_FAILED = 16,
+    ST_HDR_CHECKSUM = 17,
+    ST_CONTENT_CHECKSUM = 18,
+    ST_DST_OVERFLOW = 100,   // frame decodes to more than its seek-table dSize
+    ST_SHORT_FRAME = 101,    // frame decodes to less than its seek-table dSize
+    ST_TRUNCATED = 102,      // compressed frame ends mid-block
+    ST_UNSUPPORTED = 103,
+    ST_NOT_RUN = 0x7fff,     // status slot never written (launch failed)
+    ST_BLOCK_ERR = 200,      // internal: block-level parse failure
+    ST_DIRECT_FLAG = 0x10000,
+};
+
+// Launch the LZ4 frame decoder over nframes frames (asynchronous on stream).
+int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                      uint8_t *d_out, int32_t *d_status, hipStream_t stream);
+
+const char *status_name(int32_t st);
+
+}   // namespace zsk
+
+#endif
