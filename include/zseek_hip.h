@@ -43,6 +43,8 @@ typedef struct {
 #define ZSK_ERR_SHORT_FRAME 101   /* frame decodes to less than dSize    */
 #define ZSK_ERR_TRUNCATED 102     /* compressed frame ends mid-block     */
 #define ZSK_STATUS_DIRECT 0x10000 /* liblz4 would have used its direct path */
+#define ZSK_STATUS_BLOCK 0x20000  /* the failure is inside an LZ4 block   */
+/* bits 24-25: LZ4 block size id - 4 of a frame that failed in a block */
 
 /*
  * Decode @nframes independent LZ4 frames on the GPU, asynchronously on

@@ -88,6 +88,10 @@ struct DeviceCtx {
     size_t h_desc_cap = 0;
     int32_t *h_status = nullptr;   // pinned
     size_t h_status_cap = 0;
+    uint32_t *d_fail = nullptr;    // per-frame output offset of a failure
+    size_t d_fail_cap = 0;
+    uint32_t *h_fail = nullptr;
+    size_t h_fail_cap = 0;
     uint64_t batches = 0, frames_decoded = 0, bytes_decoded = 0, bytes_uploaded = 0;
 
     ~DeviceCtx();

@@ -199,6 +199,8 @@ DeviceCtx::~DeviceCtx()
     (void)hipFree(d_out);
     (void)hipFree(d_desc);
     (void)hipFree(d_status);
+    (void)hipFree(d_fail);
+    (void)hipHostFree(h_fail);
     (void)hipHostFree(h_comp);
     (void)hipHostFree(h_desc);
     (void)hipHostFree(h_status);
@@ -272,12 +274,12 @@ bool DeviceCtx::reserve(size_t comp, size_t out, size_t nframes, char *errbuf)
     (void)hipSetDevice(device);
     if (!grow_dev(&d_comp, &d_comp_cap, comp) || !grow_dev(&d_out, &d_out_cap, out) ||
         !grow_dev(&d_desc, &d_desc_cap, nframes) ||
-        !grow_dev(&d_status, &d_status_cap, nframes)) {
+        !grow_dev(&d_status, &d_status_cap, nframes) || !grow_dev(&d_fail, &d_fail_cap, nframes)) {
         set_error(errbuf, "allocate GPU decode buffers failed");
         return false;
     }
     if (!grow_host(&h_comp, &h_comp_cap, comp) || !grow_host(&h_desc, &h_desc_cap, nframes) ||
-        !grow_host(&h_status, &h_status_cap, nframes)) {
+        !grow_host(&h_status, &h_status_cap, nframes) || !grow_host(&h_fail, &h_fail_cap, nframes)) {
         set_error(errbuf, "allocate pinned staging failed");
         return false;
     }

@@ -59,6 +59,7 @@ struct Wave {
     uint32_t w0, w1, w2, w3;      // window dwords: [wq, wq+1024)
     uint8_t *ring;                // this wave's LDS ring
     uint32_t flushed;             // output bytes flushed to HBM
+    uint32_t fail_op;             // output offset of the block that failed
     uint32_t lane;
 
     __device__ __forceinline__ uint32_t load_dw(uint32_t coord) const
@@ -315,6 +316,7 @@ struct Wave {
         uint32_t op = 0;
         flushed = 0;
         for (;;) {
+            fail_op = op;
             if (clen - ip < 4)
                 return ST_TRUNCATED;
             ensure(ip + s0);
@@ -347,9 +349,14 @@ struct Wave {
                     if (st == ST_BLOCK_ERR) {
                         // liblz4 reports GENERIC when it decodes straight
                         // into dst (room >= max block), else
-                        // decompressionFailed (via its tmp buffer)
+                        // decompressionFailed (via its tmp buffer).  Room
+                        // here = the rest of the frame (the reference's
+                        // cached path); the host re-derives it for no-cache
+                        // reads from fail_op and the block size id.
                         bool direct = (dlen - op) >= max_block;
-                        return direct ? (ST_GENERIC | ST_DIRECT_FLAG) : ST_DECOMPRESS_FAILED;
+                        int32_t bits = (int32_t)((bsid - 4) << ST_BSID_SHIFT);
+                        return (direct ? (ST_GENERIC | ST_DIRECT_FLAG) : ST_DECOMPRESS_FAILED) |
+                               ST_BLOCK_FAIL_FLAG | bits;
                     }
                     return st;
                 }
@@ -358,6 +365,7 @@ struct Wave {
             ip += need;
         }
         flush_tail(op);
+        fail_op = op;
         if (csize_flag && content_size != op)
             return ST_FRAME_SIZE;
         if (content_ck) {
@@ -450,7 +458,8 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc 
                                                                 uint32_t nframes,
                                                                 const uint8_t *__restrict__ comp,
                                                                 uint8_t *__restrict__ out,
-                                                                int32_t *__restrict__ status)
+                                                                int32_t *__restrict__ status,
+                                                                uint32_t *__restrict__ fail_at)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * RING];
     const uint32_t wave = uni(threadIdx.x >> 6);
@@ -472,16 +481,20 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc 
     w.out_aligned = (reinterpret_cast<uintptr_t>(obase) & 3) == 0;
     w.ring = lds + wave * RING;
     w.flushed = 0;
+    w.fail_op = 0;
     int32_t st = w.frame();
-    if (w.lane == 0)
+    if (w.lane == 0) {
         status[f] = st;
+        if (fail_at)
+            fail_at[f] = w.fail_op;
+    }
 }
 
 }   // namespace
 
 // Launch configuration chosen per frame size class.
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                      uint8_t *d_out, int32_t *d_status, hipStream_t stream)
+                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
@@ -489,7 +502,7 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
     constexpr int kRing = 4096;
     dim3 grid((nframes + kWaves - 1) / kWaves);
     hipLaunchKernelGGL((lz4_frames_kernel<kRing, kWaves>), grid, dim3(64 * kWaves), 0, stream,
-                       d_desc, nframes, d_comp, d_out, d_status);
+                       d_desc, nframes, d_comp, d_out, d_status, d_fail_at);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -188,6 +188,7 @@ namespace {
 struct BatchResult {
     size_t first_bad;   // == f1 when every frame decoded
     int32_t status;
+    uint32_t fail_at;   // output offset (within the frame) of the failure
 };
 
 bool read_span(zseek_reader *r, void *dst, size_t len, uint64_t off, void *call_data,
@@ -233,10 +234,14 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
     if (e == hipSuccess)
         e = hipMemsetD32Async((hipDeviceptr_t)g.d_status, ST_NOT_RUN, n, g.stream);
     if (e == hipSuccess &&
-        launch_lz4_frames(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.stream) != 0)
+        launch_lz4_frames(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
+                          g.stream) != 0)
         e = hipErrorLaunchFailure;
     if (e == hipSuccess)
         e = hipMemcpyAsync(g.h_status, g.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           g.stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(g.h_fail, g.d_fail, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                            g.stream);
     if (e == hipSuccess)
         e = hipStreamSynchronize(g.stream);
@@ -250,30 +255,50 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
     g.bytes_uploaded += csz;
     res->first_bad = f1;
     res->status = ST_OK;
+    res->fail_at = 0;
     for (size_t i = 0; i < n; i++) {
         if (g.h_status[i] != ST_OK) {
             res->first_bad = f0 + i;
             res->status = g.h_status[i];
+            res->fail_at = g.h_fail[i];
             break;
         }
     }
     return true;
 }
 
-// Error text for a failed frame, as the reference words it for the same
-// failure (decompress.c:766-768 cached, :635-660 no-cache).
-void frame_error(zseek_reader *r, int32_t st, size_t offset_in_frame, char *errbuf)
+// Error text for a failed frame, worded as the reference words the same
+// failure.  Cached reads decode the whole frame ("decompress frame: ...",
+// decompress.c:766-768); no-cache reads first decode-and-discard the
+// offset_in_frame prefix, then decode into the caller's buffer
+// (:635-660).  For a failure inside an LZ4 block liblz4 says ERROR_GENERIC
+// when the block was decoded straight into the destination (room >= max
+// block size) and ERROR_decompressionFailed when it went through its
+// temporary buffer; the room depends on which buffer the block landed in.
+void frame_error(zseek_reader *r, const BatchResult &br, size_t frame, size_t offset_in_frame,
+                 size_t count, char *errbuf)
 {
-    int32_t code = st & 0xFFFF;
-    const char *name = status_name(st);
+    const int32_t st = br.status;
+    const uint64_t dsize = r->st.dsize(frame);
+    const uint64_t at = br.fail_at;
+    const char *prefix;
+    uint64_t room;
     if (r->cache) {
-        set_error(errbuf, "%s: %s", "decompress frame", name);
-        return;
+        prefix = "decompress frame";
+        room = dsize - at;
+    } else if (at < offset_in_frame) {
+        prefix = "decompress discard data";
+        room = offset_in_frame - at;
+    } else {
+        prefix = "decompress user data";
+        uint64_t want = count < dsize - offset_in_frame ? count : dsize - offset_in_frame;
+        uint64_t used = at - offset_in_frame;
+        room = want > used ? want - used : 0;
     }
-    if (code == ST_GENERIC && (st & ST_DIRECT_FLAG))
-        name = status_name(ST_DECOMPRESS_FAILED);   // no-cache decodes via tmp
-    set_error(errbuf, "%s: %s",
-              offset_in_frame > 0 ? "decompress discard data" : "decompress user data", name);
+    const char *name = status_name(st);
+    if (st & ST_BLOCK_FAIL_FLAG)
+        name = status_name(room >= status_max_block(st) ? ST_GENERIC : ST_DECOMPRESS_FAILED);
+    set_error(errbuf, "%s: %s", prefix, name);
 }
 
 bool copy_out(DeviceCtx &g, void *dst, uint64_t src_off, size_t len, bool device_dst,
@@ -341,7 +366,7 @@ ssize_t pread_lz4(zseek_reader *r, void *buf, size_t count, size_t offset, void 
             if (!gpu_decode(r, f_first, f_first + 1, call_data, errbuf, &br))
                 return -1;
             if (br.first_bad != f_first + 1) {
-                frame_error(r, br.status, offset - st.d_off[f_first], errbuf);
+                frame_error(r, br, f_first, offset - st.d_off[f_first], count, errbuf);
                 return -1;
             }
             if (!cache_frames(r, f_first, f_first, f_first + 1, errbuf))
@@ -387,7 +412,7 @@ ssize_t pread_lz4(zseek_reader *r, void *buf, size_t count, size_t offset, void 
         if (br.first_bad < g_end) {
             if (done)
                 return (ssize_t)done;   // short read up to the corrupt frame
-            frame_error(r, br.status, offset - st.d_off[br.first_bad], errbuf);
+            frame_error(r, br, br.first_bad, offset - st.d_off[br.first_bad], count, errbuf);
             return -1;
         }
         if (r->cache && g_end > f_last) {
@@ -548,7 +573,7 @@ extern "C" ZSEEK_EXPORT int zsk_lz4_decode_frames(const zsk_frame_desc_t *d_desc
     static_assert(sizeof(zsk_frame_desc_t) == sizeof(FrameDesc), "descriptor ABI");
     return launch_lz4_frames(reinterpret_cast<const FrameDesc *>(d_desc), nframes,
                              static_cast<const uint8_t *>(d_comp), static_cast<uint8_t *>(d_out),
-                             d_status, static_cast<hipStream_t>(stream));
+                             d_status, nullptr, static_cast<hipStream_t>(stream));
 }
 
 extern "C" ZSEEK_EXPORT const char *zsk_status_string(int32_t status)

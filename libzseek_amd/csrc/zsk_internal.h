@@ -45,11 +45,21 @@ enum : int32_t {
     ST_NOT_RUN = 0x7fff,     // status slot never written (launch failed)
     ST_BLOCK_ERR = 200,      // internal: block-level parse failure
     ST_DIRECT_FLAG = 0x10000,
+    ST_BLOCK_FAIL_FLAG = 0x20000,   // failure inside an LZ4 block (fail_at valid)
+    ST_BSID_SHIFT = 24,             // bits 24-25: block size id - 4 of the frame
 };
 
+inline uint32_t status_max_block(int32_t st)
+{
+    return 1u << (8 + 2 * (((st >> ST_BSID_SHIFT) & 3) + 4));
+}
+
 // Launch the LZ4 frame decoder over nframes frames (asynchronous on stream).
+// d_fail_at (optional) receives, per frame, the output offset of the block
+// whose decode failed.
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                      uint8_t *d_out, int32_t *d_status, hipStream_t stream);
+                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
+                      hipStream_t stream);
 
 const char *status_name(int32_t st);
 

@@ -125,14 +125,15 @@ static long decode_block(const uint8_t *src, size_t src_len, uint8_t *out,
 
 int orc_lz4f_decode(const uint8_t *src, size_t src_len, uint8_t *dst,
                     size_t dst_cap, size_t *dst_len, size_t *src_used,
-                    int *failed_block_direct)
+                    size_t *fail_at, int *block_fail, size_t *max_block_out)
 {
     size_t ip = 0;
     size_t op = 0;
     *dst_len = 0;
     *src_used = 0;
-    if (failed_block_direct)
-        *failed_block_direct = 0;
+    *fail_at = 0;
+    *block_fail = 0;
+    *max_block_out = 0;
 
     /* --- frame header (LZ4F_decodeHeader order) --- */
     if (src_len < 7)
@@ -166,16 +167,18 @@ int orc_lz4f_decode(const uint8_t *src, size_t src_len, uint8_t *dst,
         return ORC_ERROR_reservedFlag_set;
     if (((orc_xxh32(src + 4, hdr - 5, 0) >> 8) & 0xFF) != src[hdr - 1])
         return ORC_ERROR_headerChecksum_invalid;
-    if (dictid_flag)
-        return ORC_ERROR_GENERIC;   /* no dictionary is ever supplied */
+    /* a dictID field is only recorded by LZ4F (no dictionary is supplied,
+     * so a match reaching before the frame start fails as usual) */
     size_t max_block = (size_t)1 << (8 + 2 * bsid);   /* 64K/256K/1M/4M */
+    *max_block_out = max_block;
     uint64_t content_size = csize_flag ? rd64(src + 6) : 0;
     ip = hdr;
 
     /* --- blocks --- */
     for (;;) {
+        *fail_at = op;
         if (src_len - ip < 4)
-            return ORC_ERROR_frameHeader_incomplete;   /* truncated */
+            return ORC_ERROR_truncated;
         uint32_t bh = rd32(src + ip);
         ip += 4;
         if (bh == 0)
@@ -185,7 +188,7 @@ int orc_lz4f_decode(const uint8_t *src, size_t src_len, uint8_t *dst,
             return ORC_ERROR_maxBlockSize_invalid;
         size_t need = bsize + (block_cksum ? 4 : 0);
         if (src_len - ip < need)
-            return ORC_ERROR_frameHeader_incomplete;   /* truncated */
+            return ORC_ERROR_truncated;
         if (bh & 0x80000000U) {
             if (op + bsize > dst_cap)
                 return ORC_ERROR_dst_overflow;
@@ -206,21 +209,21 @@ int orc_lz4f_decode(const uint8_t *src, size_t src_len, uint8_t *dst,
         if (d == -2)
             return ORC_ERROR_dst_overflow;
         if (d < 0) {
-            int direct = (dst_cap - op) >= max_block;
-            if (failed_block_direct)
-                *failed_block_direct = direct;
-            return direct ? ORC_ERROR_GENERIC : ORC_ERROR_decompressionFailed;
+            *block_fail = 1;
+            return (dst_cap - op) >= max_block ? ORC_ERROR_GENERIC
+                                               : ORC_ERROR_decompressionFailed;
         }
         op += (size_t)d;
         ip += need;
     }
 
     /* --- suffix --- */
+    *fail_at = op;
     if (csize_flag && content_size != op)
         return ORC_ERROR_frameSize_wrong;
     if (content_cksum) {
         if (src_len - ip < 4)
-            return ORC_ERROR_frameHeader_incomplete;
+            return ORC_ERROR_truncated;
         if (orc_xxh32(dst, op, 0) != rd32(src + ip))
             return ORC_ERROR_contentChecksum_invalid;
         ip += 4;

@@ -40,6 +40,7 @@ LZ4F_ERROR_NAMES = [
 ]
 ORC_ERROR_DST_OVERFLOW = 100
 ORC_ERROR_SHORT_FRAME = 101
+ORC_ERROR_TRUNCATED = 102
 
 SYNTH_CHUNK = 64 << 20
 
@@ -62,7 +63,8 @@ class Oracle:
         L.orc_lz4f_decode.restype = C.c_int
         L.orc_lz4f_decode.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                       C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
-                                      C.POINTER(C.c_int)]
+                                      C.POINTER(C.c_size_t), C.POINTER(C.c_int),
+                                      C.POINTER(C.c_size_t)]
         L.orc_seek_table_parse.restype = C.c_int64
         L.orc_seek_table_parse.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
@@ -94,13 +96,17 @@ class Oracle:
 
     # -- frames -----------------------------------------------------------
     def decode_frame(self, src: bytes, dst_cap: int):
-        """-> (status, decoded bytes, src_used, failed_block_direct)."""
+        """-> (status, decoded bytes, src_used, info) with info = dict(fail_at,
+        block_fail, max_block) describing where a failure happened."""
         s = np.frombuffer(src, np.uint8)
         d = np.empty(max(dst_cap, 1), np.uint8)
-        dl, su, direct = C.c_size_t(0), C.c_size_t(0), C.c_int(0)
+        dl, su, fa, mb = C.c_size_t(0), C.c_size_t(0), C.c_size_t(0), C.c_size_t(0)
+        bf = C.c_int(0)
         st = self.lib.orc_lz4f_decode(s.ctypes.data, s.size, d.ctypes.data, dst_cap,
-                                      C.byref(dl), C.byref(su), C.byref(direct))
-        return st, d[: dl.value].tobytes(), su.value, direct.value
+                                      C.byref(dl), C.byref(su), C.byref(fa), C.byref(bf),
+                                      C.byref(mb))
+        info = {"fail_at": fa.value, "block_fail": bool(bf.value), "max_block": mb.value}
+        return st, d[: dl.value].tobytes(), su.value, info
 
     def seek_table(self, file: bytes):
         """-> dict(c_off, d_off, checksum, checksum_flag) or None."""
@@ -138,8 +144,9 @@ class Oracle:
     def error_name(code: int) -> str:
         if 0 <= code < len(LZ4F_ERROR_NAMES):
             return LZ4F_ERROR_NAMES[code]
-        return {ORC_ERROR_DST_OVERFLOW: "decoded size exceeds frame size",
-                ORC_ERROR_SHORT_FRAME: "decoded size below frame size"}.get(code, "?")
+        return {ORC_ERROR_DST_OVERFLOW: "decoded data exceeds frame size",
+                ORC_ERROR_SHORT_FRAME: "decoded data shorter than frame size",
+                ORC_ERROR_TRUNCATED: "truncated frame"}.get(code, "?")
 
     def pread_model(self, file: bytes, count: int, offset: int):
         """Reference zseek_pread result for a valid file: bytes of ONE frame."""
