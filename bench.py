@@ -154,7 +154,7 @@ def main():
     alg_bytes = comp_bytes + dsum           # sum(cSize + dSize)
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9
-    value = dsum * world / t_max / 1e9
+    value = dsum * world * args.steps / t_max / 1e9
     line = {
         "metric": METRIC,
         "value": round(value, 2),

@@ -492,18 +492,41 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc 
 
 }   // namespace
 
-// Launch configuration chosen per frame size class.
+template <int RING, int WAVES>
+static int launch_variant(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                          uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
+                          hipStream_t stream)
+{
+    dim3 grid((nframes + WAVES - 1) / WAVES);
+    hipLaunchKernelGGL((lz4_frames_kernel<RING, WAVES>), grid, dim3(64 * WAVES), 0, stream,
+                       d_desc, nframes, d_comp, d_out, d_status, d_fail_at);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Launch configuration.
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
-    constexpr int kWaves = 4;
-    constexpr int kRing = 4096;
-    dim3 grid((nframes + kWaves - 1) / kWaves);
-    hipLaunchKernelGGL((lz4_frames_kernel<kRing, kWaves>), grid, dim3(64 * kWaves), 0, stream,
-                       d_desc, nframes, d_comp, d_out, d_status, d_fail_at);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return launch_variant<4096, 4>(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
+}
+
+// Tuning hook: explicit (ring, waves) variants for scripts/kbench.py.
+int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
+                              const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                              hipStream_t stream)
+{
+    switch (variant) {
+    case 0: return launch_variant<4096, 4>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 1: return launch_variant<8192, 2>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 2: return launch_variant<8192, 4>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 3: return launch_variant<16384, 1>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 4: return launch_variant<16384, 2>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 5: return launch_variant<4096, 1>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 6: return launch_variant<2048, 4>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    default: return -1;
+    }
 }
 
 }   // namespace zsk

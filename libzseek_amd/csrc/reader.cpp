@@ -576,6 +576,19 @@ extern "C" ZSEEK_EXPORT int zsk_lz4_decode_frames(const zsk_frame_desc_t *d_desc
                              d_status, nullptr, static_cast<hipStream_t>(stream));
 }
 
+// Kernel tuning hook (not part of the stable ABI): decode with an explicit
+// launch variant, see launch_lz4_frames_variant.
+extern "C" ZSEEK_EXPORT int zsk_dev_lz4_decode_variant(int variant, const zsk_frame_desc_t *d_desc,
+                                                       uint32_t nframes, const void *d_comp,
+                                                       void *d_out, int32_t *d_status,
+                                                       void *stream)
+{
+    return launch_lz4_frames_variant(variant, reinterpret_cast<const FrameDesc *>(d_desc),
+                                     nframes, static_cast<const uint8_t *>(d_comp),
+                                     static_cast<uint8_t *>(d_out), d_status,
+                                     static_cast<hipStream_t>(stream));
+}
+
 extern "C" ZSEEK_EXPORT const char *zsk_status_string(int32_t status)
 {
     return status_name(status);

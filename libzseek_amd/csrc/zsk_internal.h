@@ -61,6 +61,10 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                       hipStream_t stream);
 
+int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
+                              const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                              hipStream_t stream);
+
 const char *status_name(int32_t st);
 
 }   // namespace zsk
