@@ -4,26 +4,28 @@
 // (/root/reference/src/decompress.c:752-773, LZ4F_decompress in a loop) with
 // ONE grid over every frame a zseek_pread range covers.
 //
-// Mapping (see DESIGN.md §3):
-//   * one wave64 decodes one seek-table frame; WAVES independent waves per
-//     workgroup, frames dealt one per wave in grid order;
-//   * the compressed frame streams through a 1 KiB register window per wave
-//     (4 VGPRs x 64 lanes x 4 B, coalesced 256-B buffer loads, 2 windows of
-//     prefetch); the token parse runs wave-uniform on the scalar unit, bytes
-//     picked out of the window with v_readlane;
-//   * literal runs move window -> LDS with ds_bpermute (lane i takes byte i);
-//   * decoded bytes land in a per-wave LDS ring (RING bytes); matches whose
-//     source is still in the ring are copied LDS -> LDS, older ones are
+// Mapping (DESIGN.md §3):
+//   * a wave64 decodes G = 64/L frames at once: lane group g (L lanes) owns
+//     one seek-table frame.  All parse state (ip, op, block bounds, ...) is
+//     group-uniform but lives in VGPRs, so the token parse of G frames costs
+//     ONE stream of vector instructions spread over the CU's four SIMDs —
+//     a one-frame-per-wave scalar parse saturates the CU's single scalar
+//     unit instead (measured: 125 SALU per sequence, 0.94 SALU/cycle/CU);
+//   * the compressed frame streams through a per-frame LDS input window
+//     (2 x CHUNK bytes, CHUNK = 16 B x L): each lane prefetches its 16 B of
+//     the next chunk into registers (one coalesced global_load_dwordx4 per
+//     lane) a whole chunk ahead of use; tokens / offsets are read from the
+//     window with ds_read2_b32 + v_alignbyte;
+//   * decoded bytes land in a per-frame LDS ring (RING bytes); matches whose
+//     source is still in the ring are copied LDS -> LDS, older sources are
 //     re-read from the frame's already-flushed output in HBM;
-//   * completed 256-B ring chunks are flushed with one coalesced dword store
-//     per lane.
-//   * every global access goes through a per-frame buffer resource whose
-//     num_records is the frame's seek-table size: hardware range checking
-//     keeps a corrupt frame from touching any byte outside its own slot.
+//   * completed CHUNK-byte ring slices are flushed with one 16-B store per
+//     lane (global_store_dwordx4).
 //
 // Validation follows liblz4 1.9.3 (the library the reference links) so that
 // success/failure matches the reference; oracle/lz4_oracle.c restates the same
-// rules on the CPU.
+// rules on the CPU.  Every global access is bounded by the frame's seek-table
+// sizes (reads clamp into the frame, writes never pass dSize).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -33,427 +35,214 @@ namespace zsk {
 
 namespace {
 
-constexpr uint32_t kRsrcDw3 = 0x00020000u;   // gfx9-family raw buffer, 32-bit data
 constexpr uint32_t kLz4Magic = 0x184D2204u;
 constexpr uint32_t kMinMatch = 4;
 constexpr uint32_t kMfLimit = 12;
 constexpr uint32_t kLastLiterals = 5;
-constexpr uint32_t kFlush = 256;   // bytes per flush chunk (64 lanes x 4 B)
 
-__device__ __forceinline__ uint32_t uni(uint32_t v)
+enum : uint32_t { M_DONE = 0, M_BLKHDR = 1, M_SEQ = 2 };
+
+__device__ __forceinline__ uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t sh)
 {
-    return __builtin_amdgcn_readfirstlane(v);
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-template <int RING>
-struct Wave {
-    static_assert((RING & (RING - 1)) == 0 && RING >= 1024, "RING: power of 2 >= 1 KiB");
-    static constexpr uint32_t kMask = RING - 1;
+// Per-group decode context.  Every member is uniform across the L lanes of
+// a group but differs between groups: the compiler keeps it in VGPRs.
+template <int L, int RING, int CM = 1, int DIAG = 0>
+struct Group {
+    static constexpr uint32_t CHUNK = 16 * L * CM;   // input refill / output flush size
+    static constexpr uint32_t IWIN = 2 * CHUNK;   // input window (LDS)
+    static constexpr uint32_t RMASK = RING - 1;
+    static_assert((RING & (RING - 1)) == 0, "RING must be a power of two");
+    static_assert(RING >= 64 * L, "RING too small for the flush slice");
+    // match sources at distance <= NEAR are still in the ring
+    static constexpr uint32_t NEAR = RING - 16 * L - 2 * L;
 
-    __amdgpu_buffer_rsrc_t in;    // [frame start aligned down to 4, +roundup(s0+clen,4))
-    __amdgpu_buffer_rsrc_t outr;  // [frame output, +dlen)
-    uint32_t s0;                  // frame start misalignment (coords = offset + s0)
-    uint32_t clen, dlen;
-    bool out_aligned;             // frame output base 4-byte aligned
-    uint32_t wq;                  // window base coord (multiple of 4)
-    uint32_t w0, w1, w2, w3;      // window dwords: [wq, wq+1024)
-    uint8_t *ring;                // this wave's LDS ring
-    uint32_t flushed;             // output bytes flushed to HBM
-    uint32_t fail_op;             // output offset of the block that failed
-    uint32_t lane;
+    uint32_t gl;                 // lane within group
+    const uint8_t *cab;          // compressed frame base, aligned down to 16
+    uint32_t s0;                 // misalignment: coord = offset + s0
+    uint32_t clen, climit;       // compressed size; coord limit (16-aligned)
+    uint8_t *obase;              // decoded frame base in HBM
+    uint32_t dlen;
+    bool oal;                    // obase 16-byte aligned
+    uint32_t filled;             // window holds coords [filled - IWIN, filled)
+    uint4 pf[CM];                // prefetched 16*CM B of chunk [filled, +CHUNK)
+    uint8_t *ring;               // LDS: RING bytes
+    uint8_t *iwin;               // LDS: IWIN + 16 (guard) bytes
+    uint32_t flushed;            // decoded bytes stored to HBM
 
-    __device__ __forceinline__ uint32_t load_dw(uint32_t coord) const
+    __device__ __forceinline__ void load_chunk(uint32_t coord)
     {
-        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(in, coord + 4 * lane, 0, 0);
-    }
-
-    __device__ __forceinline__ void window_at(uint32_t x)
-    {
-        wq = x & ~3u;
-        w0 = load_dw(wq);
-        w1 = load_dw(wq + 256);
-        w2 = load_dw(wq + 512);
-        w3 = load_dw(wq + 768);
-    }
-
-    // Make the window start within 256 B below coord x (so [x, x+256) is held
-    // by w0/w1).  Usually one shift; long literal runs may jump further.
-    __device__ __forceinline__ void ensure(uint32_t x)
-    {
-        if (x - wq < 256)
-            return;
-        if (x - wq >= 768) {
-            window_at(x);
-            return;
-        }
-        do {
-            w0 = w1;
-            w1 = w2;
-            w2 = w3;
-            wq += 256;
-            w3 = load_dw(wq + 768);
-        } while (x - wq >= 256);
-    }
-
-    // dword k (0..127) of the w0|w1 pair, uniform
-    __device__ __forceinline__ uint32_t wdword(uint32_t k) const
-    {
-        uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)w0, (int)(k & 63));
-        uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)w1, (int)(k & 63));
-        return k < 64 ? a : b;
-    }
-
-    // 4 bytes at frame offset p (requires p+s0-wq < 504)
-    __device__ __forceinline__ uint32_t peek32(uint32_t p) const
-    {
-        uint32_t x = p + s0 - wq;
-        uint32_t k = x >> 2;
-        uint64_t v = ((uint64_t)wdword(k + 1) << 32) | wdword(k);
-        return (uint32_t)(v >> ((x & 3) * 8));
-    }
-
-    __device__ __forceinline__ uint32_t byte_at(uint32_t p)
-    {
-        ensure(p + s0);
-        return peek32(p) & 0xFF;
-    }
-
-    // ---- output side -----------------------------------------------------
-    __device__ __forceinline__ void flush_chunk()
-    {
-        uint32_t base = flushed;
-        uint32_t v = *reinterpret_cast<const uint32_t *>(ring + ((base + 4 * lane) & kMask));
-        if (out_aligned) {
-            __builtin_amdgcn_raw_buffer_store_b32(v, outr, base + 4 * lane, 0, 0);
-        } else {
 #pragma unroll
-            for (int b = 0; b < 4; b++)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> (8 * b)), outr,
-                                                     base + 4 * lane + b, 0, 0);
+        for (int k = 0; k < CM; k++) {
+            uint32_t c = coord + 16 * (gl + L * k);
+            c = c < climit ? c : 0;   // clamp inside the frame (bytes past
+                                      // the frame are never parsed)
+            pf[k] = *reinterpret_cast<const uint4 *>(cab + c);
         }
-        flushed = base + kFlush;
+    }
+
+    __device__ __forceinline__ void refill()
+    {
+#pragma unroll
+        for (int k = 0; k < CM; k++) {
+            uint32_t at = (filled & (IWIN - 1)) + 16 * (gl + L * k);
+            *reinterpret_cast<uint4 *>(iwin + at) = pf[k];
+            if (at == 0)   // mirror the window head past its end (2-dword reads)
+                *reinterpret_cast<uint4 *>(iwin + IWIN) = pf[k];
+        }
+        filled += CHUNK;
+        load_chunk(filled);
+    }
+
+    __device__ __forceinline__ void window_reset(uint32_t x)
+    {
+        filled = x & ~(CHUNK - 1);
+        load_chunk(filled);
+        refill();
+        refill();
+    }
+
+    // make coords [x, x+need) readable (need <= CHUNK)
+    __device__ __forceinline__ void ensure(uint32_t x, uint32_t need)
+    {
+        if (x + need > filled + CHUNK || x < filled - IWIN)
+            window_reset(x);
+        while (x + need > filled)
+            refill();
+    }
+
+    // 4 bytes at coord x (window must hold [x, x+8))
+    __device__ __forceinline__ uint32_t peek32(uint32_t x) const
+    {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(iwin);
+        uint32_t k = (x & (IWIN - 1)) >> 2;
+        return align_bytes(w[k + 1], w[k], x & 3);
+    }
+
+    __device__ __forceinline__ uint32_t fetch32(uint32_t p)
+    {
+        ensure(p + s0, 8);
+        return peek32(p + s0);
+    }
+
+    // ---- output side -------------------------------------------------------
+    static constexpr uint32_t FSLICE = 16 * L;   // output flush slice
+
+    __device__ __forceinline__ void flush_slice()
+    {
+        if (DIAG & 2) {   // diagnostic build: no output stores
+            flushed += FSLICE;
+            return;
+        }
+        uint32_t at = flushed + 16 * gl;
+        uint4 v = *reinterpret_cast<const uint4 *>(ring + (at & RMASK));
+        if (oal) {
+            *reinterpret_cast<uint4 *>(obase + at) = v;
+        } else {
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int b = 0; b < 16; b++)
+                obase[at + b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+        }
+        flushed += FSLICE;
     }
 
     __device__ __forceinline__ void flush_upto(uint32_t op)
     {
-        while (op - flushed >= kFlush)
-            flush_chunk();
+        while (op - flushed >= FSLICE)
+            flush_slice();
     }
 
     __device__ __forceinline__ void flush_tail(uint32_t op)
     {
         flush_upto(op);
-        for (uint32_t p = flushed + lane; p < op; p += 64)
-            __builtin_amdgcn_raw_buffer_store_b8(ring[p & kMask], outr, p, 0, 0);
+        for (uint32_t p = flushed + gl; p < op; p += L)
+            obase[p] = ring[p & RMASK];
         flushed = op;
     }
 
-    // Copy n literal bytes from frame offset ip to output offset op.
+    // n literal bytes from frame offset ip to output offset op
     __device__ __forceinline__ void copy_literals(uint32_t ip, uint32_t op, uint32_t n)
     {
-        for (uint32_t c = 0; c < n; c += 64) {
+        for (uint32_t c = 0; c < n; c += L) {
             uint32_t x = ip + c + s0;
-            ensure(x);
-            uint32_t rel = x - wq + lane;           // < 320
-            uint32_t k = rel >> 2;
-            int addr = (int)((k & 63) << 2);
-            uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)w0);
-            uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)w1);
-            uint32_t dw = k < 64 ? a : b;
-            uint8_t byte = (uint8_t)(dw >> ((rel & 3) * 8));
-            if (c + lane < n)
-                ring[(op + c + lane) & kMask] = byte;
-            flush_upto(op + (n - c < 64 ? n : c + 64));
+            ensure(x, L);
+            uint8_t b = iwin[(x + gl) & (IWIN - 1)];
+            if (c + gl < n)
+                ring[(op + c + gl) & RMASK] = b;
+            flush_upto(op + (n - c < L ? n : c + L));
         }
     }
 
-    // Copy an n-byte match at distance off to output offset op.
+    // n-byte match at distance off, written at output offset op
     __device__ __forceinline__ void copy_match(uint32_t op, uint32_t off, uint32_t n)
     {
         uint32_t c = 0;
         uint32_t eff = off;
-        if (off < 64) {
-            // first chunk: period-off pattern; then widen the distance to a
-            // multiple of off >= 64 so later chunks never overlap themselves
-            float r = __builtin_amdgcn_rcpf((float)off);
-            uint32_t q = (uint32_t)(((float)lane + 0.5f) * r);
-            uint32_t m = lane - q * off;
-            uint8_t byte = ring[(op - off + m) & kMask];
-            if (lane < n)
-                ring[(op + lane) & kMask] = byte;
-            flush_upto(op + (n < 64 ? n : 64));
-            c = 64;
-            eff = off * ((64 + off - 1) / off);
+        if (off < L) {
+            // period-off pattern for the first L bytes, then a distance that
+            // is a multiple of off and >= L (never overlaps within a step)
+            uint32_t m = gl % off;
+            uint8_t b = ring[(op - off + m) & RMASK];
+            if (gl < n)
+                ring[(op + gl) & RMASK] = b;
+            flush_upto(op + (n < L ? n : L));
+            c = L;
+            eff = off * ((L + off - 1) / off);
         }
-        const bool in_ring = eff <= (uint32_t)RING - 64;
-        for (; c < n; c += 64) {
-            uint32_t src = op + c - eff + lane;
-            uint8_t byte;
-            if (in_ring)
-                byte = ring[src & kMask];
-            else
-                byte = __builtin_amdgcn_raw_buffer_load_b8(outr, src, 0, 0);
-            if (c + lane < n)
-                ring[(op + c + lane) & kMask] = byte;
-            flush_upto(op + (n - c < 64 ? n : c + 64));
+        const bool near = (DIAG & 1) ? true : eff <= NEAR;   // DIAG 1: ring only
+        for (; c < n; c += L) {
+            uint32_t src = op + c - eff + gl;
+            uint8_t b = near ? ring[src & RMASK] : obase[src];
+            if (c + gl < n)
+                ring[(op + c + gl) & RMASK] = b;
+            flush_upto(op + (n - c < L ? n : c + L));
         }
-    }
-
-    // Decode one LZ4 block [ip, ip+bsize) into output starting at op.
-    // Returns status; *op_out = output end.
-    __device__ __forceinline__ int32_t block(uint32_t ip, uint32_t bsize, uint32_t op, uint32_t cap,
-                             uint32_t floor_, uint32_t *op_out)
-    {
-        const uint32_t iend = ip + bsize;
-        const uint32_t oend = op + cap;
-        if (bsize == 0)
-            return ST_BLOCK_ERR;
-        for (;;) {
-            if (ip >= iend)
-                return ST_BLOCK_ERR;
-            ensure(ip + s0);
-            uint32_t t4 = peek32(ip);
-            uint32_t tok = t4 & 0xFF;
-            uint32_t lit = tok >> 4;
-            uint32_t p = ip + 1;
-            if (lit == 15) {
-                if (iend - p <= 15)
-                    return ST_BLOCK_ERR;
-                uint32_t s;
-                do {
-                    if (p >= iend)
-                        return ST_BLOCK_ERR;
-                    s = byte_at(p++);
-                    lit += s;
-                } while (s == 255);
-            }
-            if (op + lit > oend - kMfLimit || iend - p < lit + 2 + 1 + kLastLiterals) {
-                // must be the last sequence: literals only, exactly to iend
-                if (iend - p != lit || op + lit > oend)
-                    return ST_BLOCK_ERR;
-                if (op + lit > dlen)
-                    return ST_DST_OVERFLOW;
-                copy_literals(p, op, lit);
-                *op_out = op + lit;
-                return ST_OK;
-            }
-            if (op + lit > dlen)
-                return ST_DST_OVERFLOW;
-            if (lit)
-                copy_literals(p, op, lit);
-            p += lit;
-            op += lit;
-            ensure(p + s0);
-            uint32_t o4 = peek32(p);
-            uint32_t off = o4 & 0xFFFF;
-            p += 2;
-            uint32_t ml = tok & 15;
-            if (ml == 15) {
-                uint32_t s;
-                do {
-                    if (p >= iend)
-                        return ST_BLOCK_ERR;
-                    s = byte_at(p++);
-                    ml += s;
-                    if (p >= iend - (kLastLiterals - 1))
-                        return ST_BLOCK_ERR;
-                } while (s == 255);
-            }
-            ml += kMinMatch;
-            if (off == 0 || off > op - floor_)
-                return ST_BLOCK_ERR;
-            if (op + ml > oend - kLastLiterals)
-                return ST_BLOCK_ERR;
-            if (op + ml > dlen)
-                return ST_DST_OVERFLOW;
-            copy_match(op, off, ml);
-            op += ml;
-            ip = p;
-        }
-    }
-
-    // Decode the whole LZ4 frame; returns status (code | direct flag).
-    __device__ __forceinline__ int32_t frame()
-    {
-        if (clen < 7)
-            return ST_HDR_INCOMPLETE;
-        window_at(s0);
-        uint32_t magic = peek32(0);
-        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u)
-            return ST_SHORT_FRAME;
-        if (magic != kLz4Magic)
-            return ST_FRAME_TYPE;
-        uint32_t desc = peek32(4);
-        uint32_t flg = desc & 0xFF, bd = (desc >> 8) & 0xFF;
-        uint32_t block_ck = (flg >> 4) & 1, indep = (flg >> 5) & 1;
-        uint32_t csize_flag = (flg >> 3) & 1, content_ck = (flg >> 2) & 1;
-        uint32_t dictid = flg & 1;
-        if ((flg >> 1) & 1)
-            return ST_RESERVED;
-        if (((flg >> 6) & 3) != 1)
-            return ST_VERSION;
-        uint32_t hdr = 7 + (csize_flag ? 8 : 0) + (dictid ? 4 : 0);
-        if (clen < hdr)
-            return ST_HDR_INCOMPLETE;
-        uint32_t bsid = (bd >> 4) & 7;
-        if ((bd >> 7) & 1)
-            return ST_RESERVED;
-        if (bsid < 4)
-            return ST_MAXBLOCK;
-        if (bd & 15)
-            return ST_RESERVED;
-        // header checksum: (XXH32(descriptor, 0) >> 8) & 0xFF
-        {
-            uint32_t hc = xxh32_small(4, hdr - 5);
-            if (((hc >> 8) & 0xFF) != byte_at(hdr - 1))
-                return ST_HDR_CHECKSUM;
-        }
-        uint64_t content_size = 0;
-        if (csize_flag)
-            content_size = (uint64_t)peek32(6) | ((uint64_t)peek32(10) << 32);
-        const uint32_t max_block = 1u << (8 + 2 * bsid);
-        uint32_t ip = hdr;
-        uint32_t op = 0;
-        flushed = 0;
-        for (;;) {
-            fail_op = op;
-            if (clen - ip < 4)
-                return ST_TRUNCATED;
-            ensure(ip + s0);
-            uint32_t bh = peek32(ip);
-            ip += 4;
-            if (bh == 0)
-                break;
-            uint32_t bsize = bh & 0x7FFFFFFFu;
-            if (bsize > max_block)
-                return ST_MAXBLOCK;
-            uint32_t need = bsize + (block_ck ? 4 : 0);
-            if (clen - ip < need)
-                return ST_TRUNCATED;
-            if (block_ck) {
-                uint32_t h = xxh32_in(ip, bsize);
-                ensure(ip + bsize + s0);
-                if (h != peek32(ip + bsize))
-                    return ST_BLOCK_CHECKSUM;
-            }
-            if (bh & 0x80000000u) {
-                if (op + bsize > dlen)
-                    return ST_DST_OVERFLOW;
-                copy_literals(ip, op, bsize);
-                op += bsize;
-            } else {
-                uint32_t floor_ = indep ? op : 0;   // offsets <= 65535 anyway
-                uint32_t nop = op;
-                int32_t st = block(ip, bsize, op, max_block, floor_, &nop);
-                if (st != ST_OK) {
-                    if (st == ST_BLOCK_ERR) {
-                        // liblz4 reports GENERIC when it decodes straight
-                        // into dst (room >= max block), else
-                        // decompressionFailed (via its tmp buffer).  Room
-                        // here = the rest of the frame (the reference's
-                        // cached path); the host re-derives it for no-cache
-                        // reads from fail_op and the block size id.
-                        bool direct = (dlen - op) >= max_block;
-                        int32_t bits = (int32_t)((bsid - 4) << ST_BSID_SHIFT);
-                        return (direct ? (ST_GENERIC | ST_DIRECT_FLAG) : ST_DECOMPRESS_FAILED) |
-                               ST_BLOCK_FAIL_FLAG | bits;
-                    }
-                    return st;
-                }
-                op = nop;
-            }
-            ip += need;
-        }
-        flush_tail(op);
-        fail_op = op;
-        if (csize_flag && content_size != op)
-            return ST_FRAME_SIZE;
-        if (content_ck) {
-            if (clen - ip < 4)
-                return ST_TRUNCATED;
-            uint32_t h = xxh32_out(op);
-            ensure(ip + s0);
-            if (h != peek32(ip))
-                return ST_CONTENT_CHECKSUM;
-        }
-        if (op != dlen)
-            return ST_SHORT_FRAME;
-        return ST_OK;
-    }
-
-    // ---- XXH32 helpers (rare paths: header / block / content checksums) ----
-    static __device__ __forceinline__ uint32_t rotl(uint32_t x, int r)
-    {
-        return (x << r) | (x >> (32 - r));
-    }
-
-    __device__ __forceinline__ uint32_t xxh32_finish(uint32_t acc, uint32_t len, uint32_t tail_p, bool from_out,
-                                     uint32_t tail_len)
-    {
-        acc += len;
-        uint32_t i = 0;
-        for (; i + 4 <= tail_len; i += 4) {
-            uint32_t w = 0;
-            for (int b = 0; b < 4; b++)
-                w |= get(tail_p + i + b, from_out) << (8 * b);
-            acc += w * 0xC2B2AE3Du;
-            acc = rotl(acc, 17) * 0x27D4EB2Fu;
-        }
-        for (; i < tail_len; i++) {
-            acc += get(tail_p + i, from_out) * 0x165667B1u;
-            acc = rotl(acc, 11) * 0x9E3779B1u;
-        }
-        acc ^= acc >> 15;
-        acc *= 0x85EBCA77u;
-        acc ^= acc >> 13;
-        acc *= 0xC2B2AE3Du;
-        acc ^= acc >> 16;
-        return acc;
-    }
-
-    __device__ __forceinline__ uint32_t get(uint32_t p, bool from_out)
-    {
-        if (from_out)
-            return uni(__builtin_amdgcn_raw_buffer_load_b8(outr, p, 0, 0));
-        return byte_at(p);
-    }
-
-    // XXH32 (seed 0) over n bytes at frame offset / output offset p: simple
-    // scalar stripes, used only for checksummed frames.
-    __device__ __forceinline__ uint32_t xxh32_any(uint32_t p, uint32_t n, bool from_out)
-    {
-        uint32_t acc;
-        uint32_t i = 0;
-        if (n >= 16) {
-            uint32_t a[4] = {0x9E3779B1u + 0x85EBCA77u, 0x85EBCA77u, 0u, 0u - 0x9E3779B1u};
-            for (; i + 16 <= n; i += 16) {
-                for (int l = 0; l < 4; l++) {
-                    uint32_t w = 0;
-                    for (int b = 0; b < 4; b++)
-                        w |= get(p + i + 4 * l + b, from_out) << (8 * b);
-                    a[l] += w * 0x85EBCA77u;
-                    a[l] = rotl(a[l], 13) * 0x9E3779B1u;
-                }
-            }
-            acc = rotl(a[0], 1) + rotl(a[1], 7) + rotl(a[2], 12) + rotl(a[3], 18);
-        } else {
-            acc = 0x165667B1u;
-        }
-        return xxh32_finish(acc, n, p + i, from_out, n - i);
-    }
-
-    __device__ __forceinline__ uint32_t xxh32_small(uint32_t p, uint32_t n) { return xxh32_any(p, n, false); }
-    __device__ __forceinline__ uint32_t xxh32_in(uint32_t p, uint32_t n) { return xxh32_any(p, n, false); }
-    __device__ __forceinline__ uint32_t xxh32_out(uint32_t n)
-    {
-        // the output was flushed by flush_tail; make the stores visible to
-        // this wave's own loads before re-reading them
-        __builtin_amdgcn_s_waitcnt(0);
-        return xxh32_any(0, n, true);
     }
 };
 
-template <int RING, int WAVES>
+// XXH32 constants (rare checksum paths)
+constexpr uint32_t P1 = 0x9E3779B1u, P2 = 0x85EBCA77u, P3 = 0xC2B2AE3Du, P4 = 0x27D4EB2Fu,
+                   P5 = 0x165667B1u;
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r)
+{
+    return (x << r) | (x >> (32 - r));
+}
+
+// XXH32 (seed 0) over n bytes; get(i) returns the 4 bytes at i (LE).
+template <typename Get>
+__device__ uint32_t xxh32(uint32_t n, Get get)
+{
+    uint32_t acc, i = 0;
+    if (n >= 16) {
+        uint32_t a0 = P1 + P2, a1 = P2, a2 = 0, a3 = 0u - P1;
+        for (; i + 16 <= n; i += 16) {
+            a0 = rotl(a0 + get(i) * P2, 13) * P1;
+            a1 = rotl(a1 + get(i + 4) * P2, 13) * P1;
+            a2 = rotl(a2 + get(i + 8) * P2, 13) * P1;
+            a3 = rotl(a3 + get(i + 12) * P2, 13) * P1;
+        }
+        acc = rotl(a0, 1) + rotl(a1, 7) + rotl(a2, 12) + rotl(a3, 18);
+    } else {
+        acc = P5;
+    }
+    acc += n;
+    for (; i + 4 <= n; i += 4)
+        acc = rotl(acc + get(i) * P3, 17) * P4;
+    for (; i < n; i++)
+        acc = rotl(acc + (get(i) & 0xFF) * P5, 11) * P1;
+    acc ^= acc >> 15;
+    acc *= P2;
+    acc ^= acc >> 13;
+    acc *= P3;
+    acc ^= acc >> 16;
+    return acc;
+}
+
+template <int L, int RING, int WAVES, int CM, int DIAG>
 __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc *__restrict__ desc,
                                                                 uint32_t nframes,
                                                                 const uint8_t *__restrict__ comp,
@@ -461,72 +250,321 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc 
                                                                 int32_t *__restrict__ status,
                                                                 uint32_t *__restrict__ fail_at)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * RING];
-    const uint32_t wave = uni(threadIdx.x >> 6);
-    const uint32_t f = uni(blockIdx.x * WAVES + wave);
-    if (f >= nframes)
-        return;
-    const FrameDesc d = desc[f];
-    Wave<RING> w;
-    w.lane = threadIdx.x & 63;
+    using G = Group<L, RING, CM, DIAG>;
+    constexpr int GPW = 64 / L;                     // frames per wave
+    constexpr uint32_t PER = RING + G::IWIN + 16;   // LDS bytes per frame
+    __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * GPW * PER];
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t grp = lane / L;
+    const uint32_t f = (blockIdx.x * WAVES + wave) * GPW + grp;
+    const bool live = f < nframes;
+
+    G g;
+    g.gl = lane % L;
+    FrameDesc d = live ? desc[f] : FrameDesc{0, 0, 0, 0};
     const uint8_t *cbase = comp + d.c_off;
-    uintptr_t ca = reinterpret_cast<uintptr_t>(cbase);
-    w.s0 = uni((uint32_t)(ca & 3));
-    w.clen = uni(d.c_size);
-    w.dlen = uni(d.d_size);
-    w.in = __builtin_amdgcn_make_buffer_rsrc((void *)(ca & ~(uintptr_t)3), 0,
-                                             (int)((w.s0 + w.clen + 3) & ~3u), kRsrcDw3);
-    uint8_t *obase = out + d.d_off;
-    w.outr = __builtin_amdgcn_make_buffer_rsrc(obase, 0, (int)w.dlen, kRsrcDw3);
-    w.out_aligned = (reinterpret_cast<uintptr_t>(obase) & 3) == 0;
-    w.ring = lds + wave * RING;
-    w.flushed = 0;
-    w.fail_op = 0;
-    int32_t st = w.frame();
-    if (w.lane == 0) {
-        status[f] = st;
-        if (fail_at)
-            fail_at[f] = w.fail_op;
+    g.s0 = (uint32_t)(reinterpret_cast<uintptr_t>(cbase) & 15);
+    g.cab = cbase - g.s0;
+    g.clen = d.c_size;
+    g.climit = (g.s0 + g.clen + 15) & ~15u;
+    g.obase = out + d.d_off;
+    g.dlen = d.d_size;
+    g.oal = (reinterpret_cast<uintptr_t>(g.obase) & 15) == 0;
+    uint8_t *base = lds + (wave * GPW + grp) * PER;
+    g.ring = base;
+    g.iwin = base + RING;
+    g.flushed = 0;
+
+    // ---- frame header (LZ4F_decodeHeader order, liblz4 1.9.3) ----------
+    int32_t st = ST_OK;
+    uint32_t mode = live ? M_BLKHDR : M_DONE;
+    uint32_t ip = 0, op = 0, fail_op = 0;
+    uint32_t block_ck = 0, indep = 1, content_ck = 0, csize_flag = 0, bsid = 4;
+    uint32_t max_block = 65536;
+    uint64_t content_size = 0;
+    uint32_t iend = 0, oend = 0, floor_ = 0, bstart = 0;
+    if (live) {
+        g.window_reset(g.s0);
+        if (g.clen < 7) {
+            st = ST_HDR_INCOMPLETE;
+        } else {
+            uint32_t magic = g.fetch32(0);
+            uint32_t dsc = g.fetch32(4);
+            uint32_t flg = dsc & 0xFF, bd = (dsc >> 8) & 0xFF;
+            block_ck = (flg >> 4) & 1;
+            indep = (flg >> 5) & 1;
+            csize_flag = (flg >> 3) & 1;
+            content_ck = (flg >> 2) & 1;
+            uint32_t dictid = flg & 1;
+            uint32_t hdr = 7 + (csize_flag ? 8 : 0) + (dictid ? 4 : 0);
+            bsid = (bd >> 4) & 7;
+            if ((magic & 0xFFFFFFF0u) == 0x184D2A50u)
+                st = ST_SHORT_FRAME;
+            else if (magic != kLz4Magic)
+                st = ST_FRAME_TYPE;
+            else if ((flg >> 1) & 1)
+                st = ST_RESERVED;
+            else if (((flg >> 6) & 3) != 1)
+                st = ST_VERSION;
+            else if (g.clen < hdr)
+                st = ST_HDR_INCOMPLETE;
+            else if ((bd >> 7) & 1)
+                st = ST_RESERVED;
+            else if (bsid < 4)
+                st = ST_MAXBLOCK;
+            else if (bd & 15)
+                st = ST_RESERVED;
+            else {
+                uint32_t hc = xxh32(hdr - 5, [&](uint32_t i) { return g.fetch32(4 + i); });
+                if (((hc >> 8) & 0xFF) != (g.fetch32(hdr - 1) & 0xFF))
+                    st = ST_HDR_CHECKSUM;
+            }
+            if (st == ST_OK) {
+                if (csize_flag)
+                    content_size = (uint64_t)g.fetch32(6) | ((uint64_t)g.fetch32(10) << 32);
+                max_block = 1u << (8 + 2 * bsid);
+                ip = hdr;
+            }
+        }
+        if (st != ST_OK)
+            mode = M_DONE;
+    }
+
+    // ---- blocks and sequences, all groups in lockstep ---------------------
+    while (__builtin_amdgcn_ballot_w64(mode != M_DONE) != 0) {
+        if (mode == M_BLKHDR) {
+            fail_op = op;
+            if (g.clen - ip < 4) {
+                st = ST_TRUNCATED;
+                mode = M_DONE;
+            } else {
+                uint32_t bh = g.fetch32(ip);
+                ip += 4;
+                uint32_t bsize = bh & 0x7FFFFFFFu;
+                uint32_t need = bsize + (block_ck ? 4 : 0);
+                if (bh == 0) {
+                    mode = M_DONE;   // EndMark; suffix below
+                } else if (bsize > max_block) {
+                    st = ST_MAXBLOCK;
+                    mode = M_DONE;
+                } else if (g.clen - ip < need) {
+                    st = ST_TRUNCATED;
+                    mode = M_DONE;
+                } else {
+                    if (block_ck) {
+                        uint32_t h = xxh32(bsize, [&](uint32_t i) { return g.fetch32(ip + i); });
+                        if (h != g.fetch32(ip + bsize)) {
+                            st = ST_BLOCK_CHECKSUM;
+                            mode = M_DONE;
+                        }
+                    }
+                    if (st == ST_OK && (bh & 0x80000000u)) {
+                        if (op + bsize > g.dlen) {
+                            st = ST_DST_OVERFLOW;
+                            mode = M_DONE;
+                        } else {
+                            g.copy_literals(ip, op, bsize);
+                            op += bsize;
+                            ip += need;
+                        }
+                    } else if (st == ST_OK) {
+                        iend = ip + bsize;
+                        bstart = op;
+                        oend = op + max_block;
+                        floor_ = indep ? op : 0;
+                        mode = M_SEQ;
+                    }
+                }
+            }
+        }
+        if (mode == M_SEQ) {
+            // one LZ4 sequence (LZ4_decompress_safe semantics, 1.9.3)
+            int32_t e = ST_OK;
+            bool last = false;
+            if (ip >= iend) {
+                e = ST_BLOCK_ERR;
+            } else {
+                uint32_t t = g.fetch32(ip);
+                uint32_t tok = t & 0xFF;
+                uint32_t lit = tok >> 4;
+                uint32_t p = ip + 1;
+                if (lit == 15) {
+                    if (iend - p <= 15) {
+                        e = ST_BLOCK_ERR;
+                    } else {
+                        uint32_t s;
+                        do {
+                            if (p >= iend) {
+                                e = ST_BLOCK_ERR;
+                                break;
+                            }
+                            s = g.fetch32(p++) & 0xFF;
+                            lit += s;
+                        } while (s == 255);
+                    }
+                }
+                if (e == ST_OK) {
+                    if (op + lit > oend - kMfLimit || iend - p < lit + 2 + 1 + kLastLiterals) {
+                        // last sequence: literals only, exactly to the block end
+                        if (iend - p != lit || op + lit > oend)
+                            e = ST_BLOCK_ERR;
+                        else if (op + lit > g.dlen)
+                            e = ST_DST_OVERFLOW;
+                        else {
+                            g.copy_literals(p, op, lit);
+                            op += lit;
+                            ip = iend;
+                            last = true;
+                        }
+                    } else if (op + lit > g.dlen) {
+                        e = ST_DST_OVERFLOW;
+                    } else {
+                        if (lit)
+                            g.copy_literals(p, op, lit);
+                        p += lit;
+                        op += lit;
+                        uint32_t o = g.fetch32(p);
+                        uint32_t off = o & 0xFFFF;
+                        p += 2;
+                        uint32_t ml = tok & 15;
+                        if (ml == 15) {
+                            uint32_t s;
+                            do {
+                                if (p >= iend) {
+                                    e = ST_BLOCK_ERR;
+                                    break;
+                                }
+                                s = g.fetch32(p++) & 0xFF;
+                                ml += s;
+                                if (p >= iend - (kLastLiterals - 1)) {
+                                    e = ST_BLOCK_ERR;
+                                    break;
+                                }
+                            } while (s == 255);
+                        }
+                        ml += kMinMatch;
+                        if (e == ST_OK) {
+                            if (off == 0 || off > op - floor_ || op + ml > oend - kLastLiterals)
+                                e = ST_BLOCK_ERR;
+                            else if (op + ml > g.dlen)
+                                e = ST_DST_OVERFLOW;
+                            else {
+                                g.copy_match(op, off, ml);
+                                op += ml;
+                                ip = p;
+                            }
+                        }
+                    }
+                }
+            }
+            if (e != ST_OK) {
+                if (e == ST_BLOCK_ERR) {
+                    // liblz4: ERROR_GENERIC when it decodes the block straight
+                    // into dst (room >= max block), else decompressionFailed
+                    // via its tmp buffer.  Room = rest of the frame (the
+                    // reference's cached path); the host re-derives it for
+                    // no-cache reads from fail_at + the block size id.
+                    bool direct = (g.dlen - bstart) >= max_block;
+                    e = (direct ? (ST_GENERIC | ST_DIRECT_FLAG) : ST_DECOMPRESS_FAILED) |
+                        ST_BLOCK_FAIL_FLAG | (int32_t)((bsid - 4) << ST_BSID_SHIFT);
+                    fail_op = bstart;
+                } else {
+                    fail_op = op;
+                }
+                st = e;
+                mode = M_DONE;
+            } else if (last) {
+                ip = iend + (block_ck ? 4 : 0);
+                mode = M_BLKHDR;
+            }
+        }
+    }
+
+    // ---- suffix: flush, content size / checksum, dSize match --------------
+    if (live) {
+        if (st == ST_OK) {
+            g.flush_tail(op);
+            fail_op = op;
+            if (csize_flag && content_size != op)
+                st = ST_FRAME_SIZE;
+            else if (content_ck) {
+                if (g.clen - ip < 4) {
+                    st = ST_TRUNCATED;
+                } else {
+                    __builtin_amdgcn_s_waitcnt(0);
+                    const uint8_t *ob = g.obase;
+                    const uint32_t n = op;
+                    uint32_t h = xxh32(n, [&](uint32_t i) {
+                        uint32_t v = 0;
+                        for (int b = 0; b < 4; b++)
+                            v |= (i + b < n ? (uint32_t)ob[i + b] : 0u) << (8 * b);
+                        return v;
+                    });
+                    if (h != g.fetch32(ip))
+                        st = ST_CONTENT_CHECKSUM;
+                }
+            }
+            if (st == ST_OK && op != g.dlen)
+                st = ST_SHORT_FRAME;
+        }
+        if (g.gl == 0) {
+            status[f] = st;
+            if (fail_at)
+                fail_at[f] = fail_op;
+        }
     }
 }
 
-}   // namespace
-
-template <int RING, int WAVES>
-static int launch_variant(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                          uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
-                          hipStream_t stream)
+template <int L, int RING, int WAVES, int CM = 1, int DIAG = 0>
+int launch_variant(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                   uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
 {
-    dim3 grid((nframes + WAVES - 1) / WAVES);
-    hipLaunchKernelGGL((lz4_frames_kernel<RING, WAVES>), grid, dim3(64 * WAVES), 0, stream,
+    constexpr uint32_t per_block = WAVES * (64 / L);
+    dim3 grid((nframes + per_block - 1) / per_block);
+    hipLaunchKernelGGL((lz4_frames_kernel<L, RING, WAVES, CM, DIAG>), grid, dim3(64 * WAVES), 0, stream,
                        d_desc, nframes, d_comp, d_out, d_status, d_fail_at);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Launch configuration.
+}   // namespace
+
+// Default launch configuration (see DESIGN.md §3 for the sweep).
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
-    return launch_variant<4096, 4>(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
+    return launch_variant<16, 4096, 2>(d_desc, nframes, d_comp, d_out, d_status, d_fail_at,
+                                       stream);
 }
 
-// Tuning hook: explicit (ring, waves) variants for scripts/kbench.py.
+// Tuning hook: explicit (lanes per frame, ring, waves) variants for
+// scripts/kbench.py.
 int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
                               const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
                               hipStream_t stream)
 {
+    if (nframes == 0)
+        return 0;
+#define ZSK_V(L, R, W, CM, D) \
+    launch_variant<L, R, W, CM, D>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream)
     switch (variant) {
-    case 0: return launch_variant<4096, 4>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
-    case 1: return launch_variant<8192, 2>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
-    case 2: return launch_variant<8192, 4>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
-    case 3: return launch_variant<16384, 1>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
-    case 4: return launch_variant<16384, 2>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
-    case 5: return launch_variant<4096, 1>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
-    case 6: return launch_variant<2048, 4>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 0: return ZSK_V(16, 4096, 2, 1, 0);
+    case 3: return ZSK_V(16, 2048, 2, 1, 0);
+    case 7: return ZSK_V(64, 4096, 4, 1, 0);
+    // diagnostic builds (wrong output, timing only): 1 = all matches from
+    // the ring, 2 = no output stores, 3 = both
+    case 10: return ZSK_V(16, 2048, 2, 1, 1);
+    case 11: return ZSK_V(16, 2048, 2, 1, 2);
+    case 12: return ZSK_V(16, 2048, 2, 1, 3);
+    case 13: return ZSK_V(64, 4096, 4, 1, 1);
+    case 14: return ZSK_V(64, 4096, 4, 1, 2);
+    case 15: return ZSK_V(64, 4096, 4, 1, 3);
     default: return -1;
     }
+#undef ZSK_V
 }
 
 }   // namespace zsk
