@@ -191,32 +191,24 @@ def main():
 
 
 def reassemble(dist, torch, out, world, rank, dev):
-    """all-gatherv of the decoded shards: every rank ends with the full
-    N x 4 GiB range (grouped broadcasts, one per source rank).  Timed apart
-    from the decode; run on a 512 MiB slice per rank to bound memory."""
+    """all-gatherv of the decoded shards (libzseek_amd.shard: one RCCL
+    broadcast per source rank, grouped): every rank ends with all N slabs.
+    Timed apart from the decode, on a 512 MiB slice per rank to bound memory."""
+    from libzseek_amd import shard
     n = min(out.numel(), 512 << 20)
+    counts = [n] * world
     full = torch.empty(n * world, dtype=torch.uint8, device=dev)
-    full[rank * n:(rank + 1) * n].copy_(out[:n])
-    torch.cuda.synchronize()
-
-    def gather():
-        reqs = []
-        for src in range(world):
-            reqs.append(dist.broadcast(full[src * n:(src + 1) * n], src=src, async_op=True))
-        for r in reqs:
-            r.wait()
-
-    gather()
+    shard.all_gatherv(dist, out[:n], counts, out=full)
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    gather()
+    shard.all_gatherv(dist, out[:n], counts, out=full)
     torch.cuda.synchronize()
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ok = bool(torch.equal(full[rank * n:(rank + 1) * n], out[:n]))
-    return {"bytes_per_rank": n, "seconds": float(t[0]),
-            "gathered_GBps_per_rank": round(n * (world - 1) / float(t[0]) / 1e9, 2),
+    return {"bytes_per_rank": n, "seconds": round(float(t[0]), 6),
+            "received_GBps_per_rank": round(n * (world - 1) / float(t[0]) / 1e9, 2),
             "method": "RCCL grouped broadcast (all-gatherv)", "own_slab_intact": ok}
 
 

@@ -163,6 +163,40 @@ struct Group {
         flushed = op;
     }
 
+    // ---- fast path: 4 bytes per lane, one 4L-byte step ------------------
+    // Write the `n` (< 4 once past the end) valid bytes of v to ring offsets
+    // dop..dop+3; lanes' surplus bytes go to a per-frame dummy slot.
+    __device__ __forceinline__ void ring_put4(uint32_t dop, uint32_t v, int32_t n)
+    {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            uint32_t at = b < n ? ((dop + b) & RMASK) : RING + IWIN + 16;
+            ring[at] = (uint8_t)(v >> (8 * b));
+        }
+    }
+
+    // literal step: bytes [c, c+4L) of the run at frame offset lsrc -> op
+    __device__ __forceinline__ void lit_step(uint32_t lsrc, uint32_t op, uint32_t n, uint32_t c)
+    {
+        uint32_t j = c + 4 * gl;
+        uint32_t x = lsrc + s0 + j;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(iwin);
+        uint32_t k = (x & (IWIN - 1)) >> 2;
+        uint32_t v = align_bytes(w[k + 1], w[k], x & 3);
+        ring_put4(op + j, v, (int32_t)n - (int32_t)j);
+    }
+
+    // match step: bytes [c, c+4L) of a match at distance off (>= 4L) -> op
+    __device__ __forceinline__ void match_step(uint32_t op, uint32_t off, uint32_t n, uint32_t c)
+    {
+        uint32_t j = c + 4 * gl;
+        uint32_t src = op - off + j;
+        const uint32_t *r = reinterpret_cast<const uint32_t *>(ring);
+        uint32_t k = (src & RMASK) >> 2;
+        uint32_t v = align_bytes(r[(k + 1) & (RMASK >> 2)], r[k], src & 3);
+        ring_put4(op + j, v, (int32_t)n - (int32_t)j);
+    }
+
     // n literal bytes from frame offset ip to output offset op
     __device__ __forceinline__ void copy_literals(uint32_t ip, uint32_t op, uint32_t n)
     {
@@ -242,7 +276,7 @@ __device__ uint32_t xxh32(uint32_t n, Get get)
     return acc;
 }
 
-template <int L, int RING, int WAVES, int CM, int DIAG>
+template <int L, int RING, int WAVES, int CM, int DIAG, bool FAST>
 __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc *__restrict__ desc,
                                                                 uint32_t nframes,
                                                                 const uint8_t *__restrict__ comp,
@@ -252,7 +286,7 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc 
 {
     using G = Group<L, RING, CM, DIAG>;
     constexpr int GPW = 64 / L;                     // frames per wave
-    constexpr uint32_t PER = RING + G::IWIN + 16;   // LDS bytes per frame
+    constexpr uint32_t PER = RING + G::IWIN + 32;   // ring, window + guard, dummy
     __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * GPW * PER];
 
     const uint32_t lane = threadIdx.x & 63;
@@ -379,7 +413,49 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc 
                 }
             }
         }
-        if (mode == M_SEQ) {
+        bool slow = mode == M_SEQ;
+        if (FAST && mode == M_SEQ) {
+            // ---- fast path: the common sequence shape in one step --------
+            // (no multi-byte length extensions, literals <= 4L bytes,
+            // match <= 8L bytes at a near distance >= 4L, not the block's last
+            // sequence, every bound satisfied).  Anything else re-runs the
+            // same sequence through the general path below.
+            if (ip + g.s0 + 6 * L > g.filled)
+                g.refill();   // keep >= 6L bytes of input ahead
+            const uint32_t a = g.peek32(ip + g.s0);
+            const uint32_t tok = a & 0xFF, lit4 = tok >> 4, mln = tok & 15;
+            const uint32_t b1 = (a >> 8) & 0xFF;
+            const bool litx = lit4 == 15;
+            const uint32_t lit = litx ? 15 + b1 : lit4;
+            const uint32_t lsrc = ip + 1 + (litx ? 1 : 0);
+            const uint32_t p = lsrc + lit;
+            const uint32_t o = g.peek32(p + g.s0);
+            const uint32_t off = o & 0xFFFF, b2 = (o >> 16) & 0xFF;
+            const bool mlx = mln == 15;
+            const uint32_t ml = (mlx ? 15 + b2 : mln) + kMinMatch;
+            const uint32_t np = p + 2 + (mlx ? 1 : 0);
+            const uint32_t mop = op + lit;
+            const uint32_t nop = mop + ml;
+            const bool ok = ip + g.s0 + 6 * L <= g.filled && ip + g.s0 >= g.filled - G::IWIN &&
+                            (!litx || (b1 != 255 && iend - (ip + 1) > 15)) &&
+                            (!mlx || (b2 != 255 && np < iend - (kLastLiterals - 1))) &&
+                            lit <= 4 * L && ml <= 8 * L && ip < iend &&
+                            op + lit <= oend - kMfLimit && iend - lsrc >= lit + 2 + 1 + kLastLiterals &&
+                            off >= 4 * L && off <= G::NEAR && off <= mop - floor_ &&
+                            nop <= oend - kLastLiterals && nop <= g.dlen;
+            if (ok) {
+                if (lit)
+                    g.lit_step(lsrc, op, lit, 0);
+                g.match_step(mop, off, ml, 0);
+                if (ml > 4 * L)
+                    g.match_step(mop, off, ml, 4 * L);
+                op = nop;
+                ip = np;
+                g.flush_upto(op);
+                slow = false;
+            }
+        }
+        if (slow) {
             // one LZ4 sequence (LZ4_decompress_safe semantics, 1.9.3)
             int32_t e = ST_OK;
             bool last = false;
@@ -517,13 +593,13 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_frames_kernel(const FrameDesc 
     }
 }
 
-template <int L, int RING, int WAVES, int CM = 1, int DIAG = 0>
+template <int L, int RING, int WAVES, int CM = 1, int DIAG = 0, bool FAST = true>
 int launch_variant(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                    uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
 {
     constexpr uint32_t per_block = WAVES * (64 / L);
     dim3 grid((nframes + per_block - 1) / per_block);
-    hipLaunchKernelGGL((lz4_frames_kernel<L, RING, WAVES, CM, DIAG>), grid, dim3(64 * WAVES), 0, stream,
+    hipLaunchKernelGGL((lz4_frames_kernel<L, RING, WAVES, CM, DIAG, FAST>), grid, dim3(64 * WAVES), 0, stream,
                        d_desc, nframes, d_comp, d_out, d_status, d_fail_at);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -536,8 +612,8 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
 {
     if (nframes == 0)
         return 0;
-    return launch_variant<16, 4096, 2>(d_desc, nframes, d_comp, d_out, d_status, d_fail_at,
-                                       stream);
+    // measured best so far: the wave-per-frame kernel (lz4_wave.hip)
+    return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
 }
 
 // Tuning hook: explicit (lanes per frame, ring, waves) variants for
@@ -548,20 +624,26 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
 {
     if (nframes == 0)
         return 0;
-#define ZSK_V(L, R, W, CM, D) \
-    launch_variant<L, R, W, CM, D>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream)
+#define ZSK_V(L, R, W, CM, D, F) \
+    launch_variant<L, R, W, CM, D, F>(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream)
     switch (variant) {
-    case 0: return ZSK_V(16, 4096, 2, 1, 0);
-    case 3: return ZSK_V(16, 2048, 2, 1, 0);
-    case 7: return ZSK_V(64, 4096, 4, 1, 0);
+    case 0: return ZSK_V(16, 4096, 2, 1, 0, true);
+    case 1: return ZSK_V(16, 2048, 2, 1, 0, true);
+    case 2: return ZSK_V(16, 8192, 1, 1, 0, true);
+    case 3: return ZSK_V(16, 2048, 2, 1, 0, false);
+    case 4: return ZSK_V(8, 2048, 1, 1, 0, true);
+    case 5: return ZSK_V(8, 4096, 1, 1, 0, true);
+    case 6: return ZSK_V(32, 4096, 2, 1, 0, true);
+    case 7: return ZSK_V(16, 4096, 1, 1, 0, true);
+    case 8: return ZSK_V(8, 8192, 1, 1, 0, true);
     // diagnostic builds (wrong output, timing only): 1 = all matches from
     // the ring, 2 = no output stores, 3 = both
-    case 10: return ZSK_V(16, 2048, 2, 1, 1);
-    case 11: return ZSK_V(16, 2048, 2, 1, 2);
-    case 12: return ZSK_V(16, 2048, 2, 1, 3);
-    case 13: return ZSK_V(64, 4096, 4, 1, 1);
-    case 14: return ZSK_V(64, 4096, 4, 1, 2);
-    case 15: return ZSK_V(64, 4096, 4, 1, 3);
+    case 10: return ZSK_V(16, 2048, 2, 1, 1, true);
+    case 11: return ZSK_V(16, 2048, 2, 1, 2, true);
+    case 12: return ZSK_V(16, 2048, 2, 1, 3, true);
+    case 20: return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 21: return launch_lz4_wave(1, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 22: return launch_lz4_wave(2, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
     default: return -1;
     }
 #undef ZSK_V

@@ -61,6 +61,11 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                       hipStream_t stream);
 
+// Wave-per-frame kernel (lz4_wave.hip): variant 0 = 4 KiB ring, 4 waves.
+int launch_lz4_wave(int variant, const FrameDesc *d_desc, uint32_t nframes,
+                    const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                    uint32_t *d_fail_at, hipStream_t stream);
+
 int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
                               const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
                               hipStream_t stream);

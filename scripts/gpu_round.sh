@@ -1,0 +1,17 @@
+# round evidence: GPU tests, smoke, bench (default config), rocprofv3 kernel
+# trace + PMC passes of the same bench command.  Each GPU step has its own
+# time limit and the steps are chained with &&.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/round
+mkdir -p $O
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1 && tail -3 $O/pytest_gpu.log &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log &&
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err && cat $O/bench.json &&
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -- python bench.py --profile --steps 5 --warmup 1 > $O/trace.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -- python bench.py --profile --steps 2 --warmup 1 > $O/pmc_fetch.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -- python bench.py --profile --steps 2 --warmup 1 > $O/pmc_write.log 2>&1
+rc=$?
+find $O -name "*.csv" | head -20
+exit $rc

@@ -1,0 +1,333 @@
+"""CPU-side checks (no GPU): the oracle against the reference's golden
+vectors, the C-ABI library's exports and its host logic (seek table, open /
+stats / error conventions, writer, the host zstd path, cache semantics)."""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, golden_file, sha
+
+LZ4 = [n for n in ["lz4_64k_direct", "lz4_64k_buffered", "lz4_4k_direct", "lz4_1m_direct",
+                   "lz4_1m_buffered", "lz4_odd_frames", "lz4_zeros", "lz4_random",
+                   "lz4_periodic", "lz4_text_hc", "lz4_single_byte"]]
+ZSTD = ["zstd_64k_direct", "zstd_64k_buffered"]
+
+
+# ---------------------------------------------------------------------------
+# the synthetic generator (SURVEY §8d check values)
+# ---------------------------------------------------------------------------
+def test_synthetic_check_values(oracle, zs):
+    a = oracle.synth(4 << 20, 1)
+    assert hashlib.sha256(a.tobytes()).hexdigest().startswith("33244cb45799614f")
+    b = zs.synth_buffer(4 << 20)
+    assert (a == b).all()
+    c = zs.synth_buffer((64 << 20) + 12345)
+    assert (c[: 64 << 20] == oracle.synth(64 << 20, 1)).all()
+    assert (c[64 << 20:] == oracle.synth(12345, 2)).all()
+
+
+# ---------------------------------------------------------------------------
+# oracle pinned against the reference's own outputs (golden.json)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", LZ4)
+def test_oracle_decodes_golden_files(oracle, golden, payloads, name):
+    img = golden_file(name)
+    assert sha(img) == golden["files"][name]["file_sha256"]
+    assert oracle.decode_file(img) == payloads[name]
+
+
+@pytest.mark.parametrize("name", LZ4)
+def test_oracle_pread_model_matches_reference(oracle, golden, name):
+    img = golden_file(name)
+    for q in golden["files"][name]["reads"]:
+        got = oracle.pread_model(img, q["count"], q["offset"])
+        assert len(got) == q["ret"] and sha(got) == q["sha256"], q
+
+
+@pytest.mark.parametrize("name", LZ4 + ZSTD)
+def test_oracle_seek_table_matches_reference(oracle, golden, name):
+    st = oracle.seek_table(golden_file(name))
+    ref = golden["files"][name]["stats_cache1"]
+    assert st["frames"] == ref["frames"]
+    assert int(st["d_off"][-1]) == ref["decompressed_size"]
+
+
+def _oracle_error(oracle, img, cache, off, cnt):
+    """What the reference reader reports, derived from the oracle's decode."""
+    st = oracle.seek_table(img)
+    i = int(np.searchsorted(st["d_off"], np.uint64(off), side="right") - 1)
+    c0, c1 = int(st["c_off"][i]), int(st["c_off"][i + 1])
+    dsz = int(st["d_off"][i + 1] - st["d_off"][i])
+    code, data, _, info = oracle.decode_frame(img[c0:c1], dsz)
+    if code == 0:
+        return None
+    rel = off - int(st["d_off"][i])
+    if cache:
+        prefix, room = "decompress frame", dsz - info["fail_at"]
+    elif info["fail_at"] < rel:
+        prefix, room = "decompress discard data", rel - info["fail_at"]
+    else:
+        prefix = "decompress user data"
+        room = min(cnt, dsz - rel) - (info["fail_at"] - rel)
+    name = oracle.error_name(code)
+    if info["block_fail"]:
+        name = "ERROR_GENERIC" if room >= info["max_block"] else "ERROR_decompressionFailed"
+    return f"{prefix}: {name}"
+
+
+@pytest.mark.parametrize("case", ["block_byte", "block_size_huge", "first_token_offset",
+                                  "frame_magic", "flg_version", "flg_reserved", "bd_reserved",
+                                  "bd_blocksize", "header_checksum"])
+def test_oracle_errors_match_reference(oracle, golden, case):
+    rec = golden["corrupt"][case]
+    img = bytearray(golden_file("lz4_64k_direct"))
+    for at, v in rec["mutations"]:
+        img[at] = v
+    img = bytes(img)
+    for q in rec["results"]:
+        err = _oracle_error(oracle, img, q["cache"], q["offset"], q["count"])
+        if q["ret"] == -1:
+            assert err == q["error"], q
+        else:
+            assert err is None, q
+            got = oracle.pread_model(img, q["count"], q["offset"])
+            assert sha(got) == q["sha256"], q
+
+
+def test_oracle_truncated_block_is_an_error(oracle, golden):
+    """The reference spins forever here (golden: 'hang'); the restatement
+    (and the GPU path) report an error instead."""
+    rec = golden["corrupt"]["block_size_short"]
+    assert any(q["ret"] == "hang" for q in rec["results"])
+    img = bytearray(golden_file("lz4_64k_direct"))
+    for at, v in rec["mutations"]:
+        img[at] = v
+    st = oracle.seek_table(bytes(img))
+    c0, c1 = int(st["c_off"][1]), int(st["c_off"][2])
+    code, _, _, _ = oracle.decode_frame(bytes(img[c0:c1]), 65536)
+    assert code != 0
+
+
+def test_xxhash_known_answers(oracle):
+    # published xxHash test vectors (empty input, seed 0)
+    assert oracle.xxh32(b"", 0) == 0x02CC5D05
+    assert oracle.xxh64(b"", 0) == 0xEF46DB3751D8E999
+    # the LZ4 frame header checksum byte of every golden frame verifies
+    img = golden_file("lz4_64k_buffered")
+    st = oracle.seek_table(img)
+    for i in range(st["frames"]):
+        c0 = int(st["c_off"][i])
+        flg = img[c0 + 4]
+        hdr = 7 + (8 if flg & 8 else 0) + (4 if flg & 1 else 0)
+        assert (oracle.xxh32(img[c0 + 4: c0 + hdr - 1]) >> 8) & 0xFF == img[c0 + hdr - 1]
+
+
+def test_oracle_vs_reference_roundtrip(oracle, ref):
+    """Fresh inputs through the reference writer, decoded by the oracle."""
+    rng = np.random.default_rng(11)
+    for frame, wsize in [(65536, 65536), (65536, 1000), (1 << 20, 1 << 20), (5000, 7000)]:
+        data = oracle.synth(700000, int(rng.integers(1, 1000))).tobytes()
+        img = ref.compress(data, 1, frame, wsize)
+        assert oracle.decode_file(img) == data
+
+
+# ---------------------------------------------------------------------------
+# the C-ABI library: exports, host logic (no GPU compute)
+# ---------------------------------------------------------------------------
+def _declared_symbols():
+    names = []
+    for h in ("zseek.h", "zseek_hip.h"):
+        text = "\n".join(ln for ln in open(os.path.join(ROOT, "include", h))
+                         if not ln.lstrip().startswith("#"))
+        names += re.findall(r"ZSEEK_EXPORT[^;(]*?\b(\w+)\s*\(", text, re.S)
+    return names
+
+
+def test_library_exports_every_declared_symbol(zs):
+    declared = _declared_symbols()
+    assert len(declared) == 18
+    for n in ("zseek_reader_open_full", "zseek_pread", "zseek_writer_close",
+              "zsk_lz4_decode_frames"):
+        assert n in declared
+    L = zs.lib()
+    for n in declared:
+        assert hasattr(L, n), n
+    assert set(declared) == set(zs.EXPORTED)
+
+
+def test_library_hides_internals(zs):
+    """Only the API is default-visible (the reference's -fvisibility=hidden)."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", zs.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    funcs = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert funcs - set(zs.EXPORTED) - {"zsk_dev_lz4_decode_variant"} == set()
+
+
+def test_null_handles(zs):
+    L = zs.lib()
+    err = C.create_string_buffer(80)
+    buf = C.create_string_buffer(16)
+    assert L.zseek_pread(None, buf, 16, 0, None, err) == 0
+    assert err.value == b"invalid reader"
+    assert L.zseek_reader_close(None, None, err)
+    assert not L.zseek_reader_stats(None, None, err)
+    assert L.zseek_write(None, buf, 1, None, err) is False
+    assert err.value == b"invalid writer"
+    assert L.zseek_writer_close(None, None, err)
+
+
+@pytest.mark.parametrize("name", LZ4 + ZSTD)
+def test_reader_open_and_stats(zs, golden, name):
+    entry = golden["files"][name]
+    if "open_error" in entry:
+        with pytest.raises(zs.ZseekError) as e:
+            zs.Reader(golden_file(name), 1)
+        assert str(e.value) == entry["open_error"]
+        return
+    with zs.Reader(golden_file(name), 1) as r:
+        st = r.stats()
+        assert st["frames"] == entry["stats_cache1"]["frames"]
+        assert st["decompressed_size"] == entry["stats_cache1"]["decompressed_size"]
+        assert st["cached_frames"] == 0
+        assert r.type == (zs.ZSEEK_LZ4 if entry["codec"] == "lz4" else zs.ZSEEK_ZSTD)
+        c_off, d_off = r.frames()
+        assert int(d_off[-1]) == entry["stats_cache1"]["decompressed_size"]
+        # a read past EOF returns 0 without touching the GPU
+        assert r.pread(10, int(d_off[-1]) + 5) == b""
+
+
+def test_empty_file_open_error(zs, golden):
+    """Zero-frame file: the reference says 'unrecognized file format'."""
+    with pytest.raises(zs.ZseekError) as e:
+        zs.Reader(golden_file("lz4_empty"), 1)
+    assert str(e.value) == golden["files"]["lz4_empty"]["open_error"]
+
+
+@pytest.mark.parametrize("case", ["seek_magic", "seek_descriptor", "file_magic", "truncated",
+                                  "zero_bytes", "three_bytes"])
+def test_open_errors_match_reference(zs, golden, case):
+    rec = golden["corrupt"][case]
+    base = golden_file("lz4_64k_direct")
+    if "truncate" in rec:
+        img = base[: rec["truncate"]]
+    else:
+        b = bytearray(base)
+        for at, v in rec["mutations"]:
+            b[at] = v
+        img = bytes(b)
+    if len(img) == 0:
+        img = b""
+    with pytest.raises(zs.ZseekError) as e:
+        zs.Reader(img if img else b"\0"[:0], 1)
+    assert str(e.value) == rec["open_error"]
+
+
+@pytest.mark.parametrize("name", [n for n in LZ4 if n != "lz4_text_hc"])
+def test_writer_byte_identical_to_reference(zs, golden, payloads, name):
+    entry = golden["files"][name]
+    data = payloads[name]
+    w = zs.Writer(zs.ZSEEK_LZ4, entry["min_frame_size"], level=entry["level"])
+    for s in range(0, len(data), entry["write_size"]):
+        w.write(data[s: s + entry["write_size"]])
+    assert sha(w.close()) == entry["file_sha256"]
+
+
+def test_writer_stats(zs):
+    w = zs.Writer(zs.ZSEEK_LZ4, 65536)
+    w.write(bytes(100000))          # >= min_frame_size: one direct frame
+    st = w.stats()
+    assert st["frames"] == 1 and st["seek_table_size"] == 8 + 8 * 1 + 9
+    w.write(bytes(1000))            # buffered: counted as a pending frame
+    st = w.stats()
+    assert st["frames"] == 2 and st["seek_table_size"] == 8 + 8 * 1 + 9 + 8
+    img = w.close()
+    with zs.Reader(img, 0) as r:
+        assert r.stats()["frames"] == 2
+
+
+def test_tools_image_equals_writer(zs):
+    data = zs.synth_buffer(3 << 20)
+    for frame in (4096, 65536, 1 << 20, 100000):
+        w = zs.Writer(zs.ZSEEK_LZ4, frame)
+        for s in range(0, data.size, frame):
+            w.write(data[s: s + frame].tobytes())
+        assert zs.lz4_seekable(data, frame).tobytes() == w.close()
+
+
+@pytest.mark.parametrize("name", ZSTD)
+def test_zstd_reads_match_reference(zs, golden, payloads, name):
+    """zstd files are served on the host with libzstd, one frame per call,
+    exactly like the reference (the GPU zstd decoder is SURVEY §8f #1)."""
+    entry = golden["files"][name]
+    readers = {c: zs.Reader(golden_file(name), c) for c in (0, 1)}
+    for q in entry["reads"]:
+        r = readers[q["cache"]]
+        out = np.empty(max(q["count"], 1), np.uint8)
+        ret = r.pread_raw(out.ctypes.data, q["count"], q["offset"])
+        assert ret == q["ret"], q
+        assert sha(out[:ret]) == q["sha256"]
+    assert readers[1].stats()["cached_frames"] == entry["stats_cache1"]["cached_frames"]
+    for r in readers.values():
+        r.close()
+
+
+def test_zstd_writer_roundtrip(zs, payloads):
+    data = payloads["zstd_64k_direct"]
+    # (nb_workers > 1 needs a multithreaded libzstd, as for the reference;
+    # the system library here is single-threaded)
+    for nb in (1,):
+        w = zs.Writer(zs.ZSEEK_ZSTD, 65536, nb_workers=nb)
+        for s in range(0, len(data), 65536):
+            w.write(data[s: s + 65536])
+        img = w.close()
+        with zs.Reader(img, 0) as r:
+            assert r.read_all(len(data), 0) == data
+
+
+def test_cache_lru_matches_reference(zs, ref, golden):
+    """Frame-cache semantics (ref src/cache.c): capacity in frames, LRU
+    eviction, find promotes — observed through cached_frames on the host
+    zstd path against the reference library."""
+    img = golden_file("zstd_64k_direct")
+    seq = [0, 65536, 0, 131072, 200000, 0, 70000, 300000, 5, 400000]
+    for cap in (1, 2, 3):
+        ours = zs.Reader(img, cap)
+        theirs = ref.open(img, cap)
+        for off in seq:
+            a = ours.pread(100, off)
+            rb, b = theirs.pread(100, off)
+            assert a == b
+            assert ours.stats()["cached_frames"] == theirs.stats()[1]["cached_frames"]
+        ours.close()
+        theirs.close()
+
+
+def test_seek_table_with_checksums(zs, oracle):
+    """Descriptor bit 7 (per-frame XXH64 low-32 checksums, ref
+    seek_table.c:95-97): parsed, entries 12 bytes wide."""
+    data = zs.synth_buffer(200000)
+    img = bytearray(zs.lz4_seekable(data, 65536).tobytes())
+    st = oracle.seek_table(bytes(img))
+    n = st["frames"]
+    body = img[: int(st["c_off"][-1])]
+    table = bytearray()
+    table += (0x184D2A5E).to_bytes(4, "little") + (12 * n + 9).to_bytes(4, "little")
+    for i in range(n):
+        c = int(st["c_off"][i + 1] - st["c_off"][i])
+        d = int(st["d_off"][i + 1] - st["d_off"][i])
+        ck = oracle.xxh64(data[int(st["d_off"][i]): int(st["d_off"][i + 1])].tobytes()) & 0xFFFFFFFF
+        table += c.to_bytes(4, "little") + d.to_bytes(4, "little") + ck.to_bytes(4, "little")
+    table += n.to_bytes(4, "little") + bytes([0x80]) + (0x8F92EAB1).to_bytes(4, "little")
+    img2 = bytes(body + table)
+    st2 = oracle.seek_table(img2)
+    assert st2["checksum_flag"] and st2["frames"] == n
+    with zs.Reader(img2, 0) as r:
+        c_off, d_off = r.frames()
+        assert (d_off == st["d_off"]).all() and (c_off == st["c_off"]).all()
