@@ -175,8 +175,8 @@ def main():
                    "parallelism": f"frames sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic_from_profile(),
-                     "kernel": "lz4_frames_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                     "traffic": traffic_from_profile(z.lib().zsk_lz4_kernel_name().decode()),
+                     "kernel": z.lib().zsk_lz4_kernel_name().decode(), "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,
         "decoded_gbs_per_gpu": round(dsum / avg_kernel_s / 1e9, 2),
@@ -224,17 +224,19 @@ def end_to_end(z, img, size):
     return {"GBps": round(n / dt / 1e9, 2), "bytes": int(n), "api": "zseek_pread (host buffer)"}
 
 
-def traffic_from_profile():
-    """HBM bytes per launch from a committed rocprofv3 PMC summary, if one
-    was recorded for this build (profiles/pmc_traffic.json)."""
+def traffic_from_profile(kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by scripts/round_profiles.py), used
+    only when it was recorded for the kernel this build launches."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(p):
-        try:
-            with open(p) as f:
-                return json.load(f).get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
+    try:
+        with open(p) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if kernel not in rec.get("kernel", ""):
+        return None
+    return rec.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(img, size, frame, threads):

@@ -616,6 +616,11 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
     return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
 }
 
+const char *lz4_kernel_name()
+{
+    return "lz4_wave_kernel<4096, 4>";
+}
+
 // Tuning hook: explicit (lanes per frame, ring, waves) variants for
 // scripts/kbench.py.
 int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,

@@ -589,6 +589,11 @@ extern "C" ZSEEK_EXPORT int zsk_dev_lz4_decode_variant(int variant, const zsk_fr
                                      static_cast<hipStream_t>(stream));
 }
 
+extern "C" ZSEEK_EXPORT const char *zsk_lz4_kernel_name(void)
+{
+    return zsk::lz4_kernel_name();
+}
+
 extern "C" ZSEEK_EXPORT const char *zsk_status_string(int32_t status)
 {
     return status_name(status);

@@ -57,6 +57,10 @@ inline uint32_t status_max_block(int32_t st)
 // Launch the LZ4 frame decoder over nframes frames (asynchronous on stream).
 // d_fail_at (optional) receives, per frame, the output offset of the block
 // whose decode failed.
+// Name (template instance) of the kernel launch_lz4_frames uses, for
+// matching profiler output.
+const char *lz4_kernel_name();
+
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                       hipStream_t stream);

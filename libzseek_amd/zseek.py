@@ -88,7 +88,7 @@ EXPORTED = [
     "zseek_writer_open_full", "zseek_writer_open", "zseek_writer_close", "zseek_write",
     "zseek_writer_stats", "zseek_reader_open_full", "zseek_reader_open", "zseek_reader_close",
     "zseek_pread", "zseek_read", "zseek_reader_stats",
-    "zsk_lz4_decode_frames", "zsk_status_string", "zsk_reader_frames", "zsk_reader_type",
+    "zsk_lz4_decode_frames", "zsk_status_string", "zsk_lz4_kernel_name", "zsk_reader_frames", "zsk_reader_type",
     "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
 ]
 
@@ -128,6 +128,8 @@ def lib() -> C.CDLL:
     L.zsk_lz4_decode_frames.restype = C.c_int
     L.zsk_lz4_decode_frames.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_void_p]
+    L.zsk_lz4_kernel_name.restype = C.c_char_p
+    L.zsk_lz4_kernel_name.argtypes = []
     L.zsk_status_string.restype = C.c_char_p
     L.zsk_status_string.argtypes = [C.c_int32]
     L.zsk_reader_frames.restype = C.c_ssize_t
