@@ -200,6 +200,7 @@ DeviceCtx::~DeviceCtx()
     (void)hipFree(d_desc);
     (void)hipFree(d_status);
     (void)hipFree(d_fail);
+    split_scratch_free(&split);
     (void)hipHostFree(h_fail);
     (void)hipHostFree(h_comp);
     (void)hipHostFree(h_desc);

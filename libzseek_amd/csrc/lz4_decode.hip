@@ -606,21 +606,6 @@ int launch_variant(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_c
 
 }   // namespace
 
-// Default launch configuration (see DESIGN.md §3 for the sweep).
-int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
-{
-    if (nframes == 0)
-        return 0;
-    // measured best so far: the wave-per-frame kernel (lz4_wave.hip)
-    return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
-}
-
-const char *lz4_kernel_name()
-{
-    return "lz4_wave_kernel<4096, 4>";
-}
-
 // Tuning hook: explicit (lanes per frame, ring, waves) variants for
 // scripts/kbench.py.
 int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
@@ -649,6 +634,14 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 20: return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
     case 21: return launch_lz4_wave(1, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
     case 22: return launch_lz4_wave(2, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 30: return launch_lz4_frames(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 31: return launch_lz4_split_stages(3, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 32: return launch_lz4_split_stages(7, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 33: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 40: return launch_lz4_split_stages(7, 1, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 41: return launch_lz4_split_stages(7, 2, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 42: return launch_lz4_split_stages(7, 4, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 43: return launch_lz4_split_stages(7, 8, d_desc, nframes, d_comp, d_out, d_status, stream);
     default: return -1;
     }
 #undef ZSK_V

@@ -453,7 +453,7 @@ struct WaveDec {
     }
 };
 
-template <int RING, int WAVES>
+template <int RING, int WAVES, bool DEFERRED = false>
 __global__ __launch_bounds__(64 * WAVES) void lz4_wave_kernel(const FrameDesc *__restrict__ desc,
                                                                 uint32_t nframes,
                                                                 const uint8_t *__restrict__ comp,
@@ -465,6 +465,8 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_wave_kernel(const FrameDesc *_
     const uint32_t wave = uni(threadIdx.x >> 6);
     const uint32_t f = uni(blockIdx.x * WAVES + wave);
     if (f >= nframes)
+        return;
+    if (DEFERRED && uni((uint32_t)status[f]) != (uint32_t)ST_NOT_RUN)
         return;
     const FrameDesc d = desc[f];
     WaveDec<RING> w;
@@ -501,6 +503,18 @@ int launch_wave(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp
 }
 
 }   // namespace
+
+int launch_lz4_wave_deferred(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                             uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
+                             hipStream_t stream)
+{
+    if (nframes == 0)
+        return 0;
+    dim3 grid((nframes + 3) / 4);
+    hipLaunchKernelGGL((lz4_wave_kernel<4096, 4, true>), grid, dim3(256), 0, stream, d_desc, nframes,
+                       d_comp, d_out, d_status, d_fail_at);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_lz4_wave(int variant, const FrameDesc *d_desc, uint32_t nframes,
                     const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,

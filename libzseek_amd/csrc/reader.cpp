@@ -234,8 +234,12 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
     if (e == hipSuccess)
         e = hipMemsetD32Async((hipDeviceptr_t)g.d_status, ST_NOT_RUN, n, g.stream);
     if (e == hipSuccess &&
-        launch_lz4_frames(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
-                          g.stream) != 0)
+        split_scratch_reserve(&g.split, (uint32_t)n, split_items_needed(g.h_desc, (uint32_t)n),
+                              g.stream) != 0)
+        e = hipErrorOutOfMemory;
+    if (e == hipSuccess &&
+        launch_lz4_split(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
+                         g.stream, &g.split) != 0)
         e = hipErrorLaunchFailure;
     if (e == hipSuccess)
         e = hipMemcpyAsync(g.h_status, g.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost,

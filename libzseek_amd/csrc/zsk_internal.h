@@ -65,6 +65,38 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                       hipStream_t stream);
 
+// Scratch of the two-phase decoder (lz4_split.hip): per-frame item slot
+// offsets and counts, and the items themselves (one u32 per LZ4 sequence).
+struct SplitScratch {
+    uint64_t *rec_base = nullptr;   // [frames_cap]
+    uint32_t *nitems = nullptr;     // [frames_cap]
+    uint32_t *items = nullptr;      // [items_cap]
+    uint64_t *total = nullptr;      // host-mapped: item slots the last plan needed
+    uint32_t frames_cap = 0;
+    uint64_t items_cap = 0;
+};
+
+// Item slots frame descriptors need (host-side mirror of the plan kernel).
+uint64_t split_items_needed(const FrameDesc *h_desc, uint32_t n);
+// Grow scratch to at least (frames, items); stream-ordered.  0 on success.
+int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipStream_t stream);
+void split_scratch_free(SplitScratch *s);
+
+// Two-phase decoder with caller-owned scratch (must cover nframes and the
+// frames' item slots; frames that do not fit are decoded by the wave kernel).
+int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                     uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
+                     hipStream_t stream, SplitScratch *s, int stages = 15, int diag = 0);
+int launch_lz4_split_stages(int stages, int diag, const FrameDesc *d_desc, uint32_t nframes,
+                            const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                            hipStream_t stream);
+
+// Wave-per-frame kernel over only the frames whose status is ST_NOT_RUN
+// (the split decoder's hand-offs).
+int launch_lz4_wave_deferred(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                             uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
+                             hipStream_t stream);
+
 // Wave-per-frame kernel (lz4_wave.hip): variant 0 = 4 KiB ring, 4 waves.
 int launch_lz4_wave(int variant, const FrameDesc *d_desc, uint32_t nframes,
                     const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
