@@ -175,8 +175,8 @@ def main():
                    "parallelism": f"frames sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic_from_profile(z.lib().zsk_lz4_kernel_name().decode()),
-                     "kernel": z.lib().zsk_lz4_kernel_name().decode(), "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                     "traffic": traffic_from_profile(z.lib().zsk_lz4_kernel_name(nfr).decode()),
+                     "kernel": z.lib().zsk_lz4_kernel_name(nfr).decode(), "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,
         "decoded_gbs_per_gpu": round(dsum / avg_kernel_s / 1e9, 2),

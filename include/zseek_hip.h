@@ -60,9 +60,11 @@ ZSEEK_EXPORT int zsk_lz4_decode_frames(const zsk_frame_desc_t *d_desc,
 /* Human-readable name of a frame status (LZ4F-style "ERROR_..." names). */
 ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
 
-/* Name of the HIP kernel zsk_lz4_decode_frames launches (as it appears in a
- * rocprofv3 kernel trace, without namespace), for tooling. */
-ZSEEK_EXPORT const char *zsk_lz4_kernel_name(void);
+/* Name of the main HIP kernel zsk_lz4_decode_frames launches for a batch of
+ * nframes frames (as it appears in a rocprofv3 kernel trace, without
+ * namespace), for tooling.  Large batches use the lane-per-frame decoder,
+ * small ones the wave-per-frame decoder (env ZSEEK_HIP_KERNEL overrides). */
+ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes);
 
 /* Number of frames of an open reader and its seek table as prefix sums:
  * c_off/d_off receive n+1 entries each (either may be NULL). */

@@ -100,7 +100,7 @@ struct DeviceCtx {
     bool reserve(size_t comp, size_t out, size_t nframes, char *errbuf);
     size_t device_bytes() const
     {
-        return d_comp_cap + d_out_cap + d_desc_cap * 28 + split.frames_cap * 12 + split.items_cap * 4;
+        return d_comp_cap + d_out_cap + d_desc_cap * 28 + split.frames_cap * 12 + split.items_cap * 8;
     }
     size_t host_bytes() const { return h_comp_cap + h_desc_cap * 28; }
 };

@@ -634,13 +634,21 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 20: return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
     case 21: return launch_lz4_wave(1, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
     case 22: return launch_lz4_wave(2, d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 50: return launch_lz4_lane(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    case 51: return launch_lz4_lane(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, 1);
+    case 54: return launch_lz4_lane(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, 4);
+    case 53: return launch_lz4_lane(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, 3);
     case 30: return launch_lz4_frames(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
     case 31: return launch_lz4_split_stages(3, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 32: return launch_lz4_split_stages(7, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 33: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 35: return launch_lz4_split_stages(15, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 34: return launch_lz4_split_stages(15, 0x200, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 40: return launch_lz4_split_stages(7, 1, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 41: return launch_lz4_split_stages(7, 2, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 42: return launch_lz4_split_stages(7, 4, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 44: return launch_lz4_split_stages(7, 16, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 45: return launch_lz4_split_stages(7, 0x106, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 46: return launch_lz4_split_stages(7, 0x108, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 43: return launch_lz4_split_stages(7, 8, d_desc, nframes, d_comp, d_out, d_status, stream);
     default: return -1;
     }

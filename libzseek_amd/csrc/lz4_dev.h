@@ -1,0 +1,129 @@
+// lz4_dev.h — device helpers shared by the LZ4 kernels (lz4_split.hip,
+// lz4_lane.hip): byte picking from 16-byte register vectors, range-checked
+// aligned buffer loads, exact-length stores, wave reductions.
+#ifndef ZSK_LZ4_DEV_H
+#define ZSK_LZ4_DEV_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zsk {
+namespace lz4d {
+
+constexpr uint32_t kRsrcDw3 = 0x00020000u;   // gfx9-family raw buffer, 32-bit data
+constexpr uint32_t kLz4Magic = 0x184D2204u;
+constexpr uint32_t kMinMatch = 4;
+constexpr uint32_t kMfLimit = 12;
+constexpr uint32_t kLastLiterals = 5;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+typedef uint64_t u64_u __attribute__((aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+
+__device__ __forceinline__ uint32_t uni(uint32_t v)
+{
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// byte i (0..15) of a 16-byte register vector
+__device__ __forceinline__ uint32_t vbyte(const u32x4 &w, uint32_t i)
+{
+    uint32_t d = (i & 8) ? ((i & 4) ? w.w : w.z) : ((i & 4) ? w.y : w.x);
+    return (d >> ((i & 3) * 8)) & 0xFF;
+}
+
+// 32 bits starting at byte i (0..12) of a 16-byte register vector
+__device__ __forceinline__ uint32_t vword(const u32x4 &w, uint32_t i)
+{
+    uint32_t k = i >> 2;
+    uint32_t lo = (k & 2) ? ((k & 1) ? w.w : w.z) : ((k & 1) ? w.y : w.x);
+    uint32_t hi = (k & 2) ? w.w : ((k & 1) ? w.z : w.y);
+    return __builtin_amdgcn_alignbyte(hi, lo, i & 3);
+}
+
+// 16 bytes at byte coordinate x of a buffer resource whose base is 4-byte
+// aligned.  Loads are dword-aligned: the hardware range-checks every dword
+// of a buffer load on its own (a dword straddling num_records reads as 0), so
+// unaligned 16-byte loads would lose the last bytes of a range; aligned
+// dwords with num_records rounded up to 4 never do.
+__device__ __forceinline__ u32x4 load16u(__amdgpu_buffer_rsrc_t r, uint32_t x)
+{
+    const uint32_t a = x & ~3u, sh = x & 3;
+    const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0));
+    const uint32_t e = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, a + 16, 0, 0);
+    u32x4 o;
+    o.x = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+    o.y = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+    o.z = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+    o.w = __builtin_amdgcn_alignbyte(e, v.w, sh);
+    return o;
+}
+
+// A byte range [p0, p0+len) of device memory as (aligned resource, bias):
+// frame offset p lives at resource coordinate p + s0.
+struct Span {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t s0;
+};
+
+__device__ __forceinline__ Span make_span(const uint8_t *p0, uint64_t len)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p0);
+    Span s;
+    s.s0 = (uint32_t)(a & 3);
+    s.r = __builtin_amdgcn_make_buffer_rsrc((void *)(a & ~(uintptr_t)3), 0,
+                                            (int)(uint32_t)((s.s0 + len + 3) & ~3ull), kRsrcDw3);
+    return s;
+}
+
+// store the first n (1..16) bytes of v at p, never touching p[n..]
+__device__ __forceinline__ void store_exact(uint8_t *p, u32x4 v, uint32_t n)
+{
+    if (n >= 16) {
+        *reinterpret_cast<u32x4_u *>(p) = v;
+        return;
+    }
+    if (n & 8) {
+        *reinterpret_cast<u64_u *>(p) = ((uint64_t)v.y << 32) | v.x;
+        p += 8;
+        v.x = v.z;
+        v.y = v.w;
+    }
+    if (n & 4) {
+        *reinterpret_cast<u32_u *>(p) = v.x;
+        p += 4;
+        v.x = v.y;
+    }
+    if (n & 2) {
+        p[0] = (uint8_t)v.x;
+        p[1] = (uint8_t)(v.x >> 8);
+        p += 2;
+        v.x >>= 16;
+    }
+    if (n & 1)
+        p[0] = (uint8_t)v.x;
+}
+
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v)
+{
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v)
+{
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+}   // namespace lz4d
+}   // namespace zsk
+
+#endif

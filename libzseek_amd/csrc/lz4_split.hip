@@ -34,92 +34,35 @@
 #include <stdint.h>
 
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include <map>
 #include <mutex>
 #include <utility>
 
+#include "lz4_dev.h"
 #include "zsk_internal.h"
 
 namespace zsk {
 
 namespace {
 
-constexpr uint32_t kRsrcDw3 = 0x00020000u;   // gfx9-family raw buffer, 32-bit data
-constexpr uint32_t kLz4Magic = 0x184D2204u;
-constexpr uint32_t kMinMatch = 4;
-constexpr uint32_t kMfLimit = 12;
-constexpr uint32_t kLastLiterals = 5;
-constexpr uint32_t kItemStored = 0x80000000u;
-constexpr uint32_t kItemLast = 0x40000000u;
+using namespace lz4d;
+
+constexpr uint32_t kItemExt = 0x80000000u;   // item w0: next item holds the full lengths
 constexpr uint32_t kItemPos = 0x3FFFFFFFu;
 constexpr uint32_t kExecWaves = 4;
-constexpr uint32_t kLongRun = 128;   // longer literal runs / matches: copied by the whole wave
+constexpr uint32_t kLongCopy = 256;   // longer literal runs / matches: copied by the whole wave
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef u32x4 u32x4_u __attribute__((aligned(1)));
-typedef uint64_t u64_u __attribute__((aligned(1)));
-typedef uint32_t u32_u __attribute__((aligned(1)));
-
-__device__ __forceinline__ uint32_t uni(uint32_t v)
+// Item slots of a frame.  An item is 8 bytes; a sequence takes one (>= 3
+// compressed bytes) or two (extended: >= 4 compressed bytes), a stored block
+// two.  Real LZ4 data spends ~10-25 compressed bytes per sequence; one slot
+// per 4 bytes (+16) covers all but adversarial frames, which do not fit and
+// are decoded by the wave kernel instead (parse reports ST_NOT_RUN).
+__host__ __device__ __forceinline__ uint32_t slots_of(uint32_t c_size)
 {
-    return __builtin_amdgcn_readfirstlane(v);
-}
-
-__device__ __forceinline__ uint32_t slots_of(uint32_t c_size)
-{
-    return (c_size / 3 + 2 + 3) & ~3u;
-}
-
-// byte i (0..15) of a 16-byte register vector
-__device__ __forceinline__ uint32_t vbyte(const u32x4 &w, uint32_t i)
-{
-    uint32_t d = (i & 8) ? ((i & 4) ? w.w : w.z) : ((i & 4) ? w.y : w.x);
-    return (d >> ((i & 3) * 8)) & 0xFF;
-}
-
-// 32 bits starting at byte i (0..12) of a 16-byte register vector
-__device__ __forceinline__ uint32_t vword(const u32x4 &w, uint32_t i)
-{
-    uint32_t k = i >> 2;
-    uint32_t lo = (k & 2) ? ((k & 1) ? w.w : w.z) : ((k & 1) ? w.y : w.x);
-    uint32_t hi = (k & 2) ? w.w : ((k & 1) ? w.z : w.y);
-    return __builtin_amdgcn_alignbyte(hi, lo, i & 3);
-}
-
-// 16 bytes at byte coordinate x of a buffer resource whose base is 4-byte
-// aligned.  Loads are dword-aligned: the hardware range-checks every dword
-// of a buffer load on its own (a dword straddling num_records reads as 0), so
-// unaligned 16-byte loads would lose the last bytes of a range; aligned
-// dwords with num_records rounded up to 4 never do.
-__device__ __forceinline__ u32x4 load16u(__amdgpu_buffer_rsrc_t r, uint32_t x)
-{
-    const uint32_t a = x & ~3u, sh = x & 3;
-    const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0));
-    const uint32_t e = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, a + 16, 0, 0);
-    u32x4 o;
-    o.x = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
-    o.y = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
-    o.z = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
-    o.w = __builtin_amdgcn_alignbyte(e, v.w, sh);
-    return o;
-}
-
-// A byte range [p0, p0+len) of device memory as (aligned resource, bias):
-// frame offset p lives at resource coordinate p + s0.
-struct Span {
-    __amdgpu_buffer_rsrc_t r;
-    uint32_t s0;
-};
-
-__device__ __forceinline__ Span make_span(const uint8_t *p0, uint64_t len)
-{
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p0);
-    Span s;
-    s.s0 = (uint32_t)(a & 3);
-    s.r = __builtin_amdgcn_make_buffer_rsrc((void *)(a & ~(uintptr_t)3), 0,
-                                            (int)(uint32_t)((s.s0 + len + 3) & ~3ull), kRsrcDw3);
-    return s;
+    return (c_size / 4 + 16 + 3) & ~3u;
 }
 
 // Per-lane reader over one frame of the compressed image with a 16-byte
@@ -173,30 +116,47 @@ __device__ uint32_t xxh32_short(LaneIn &in, uint32_t p, uint32_t n)
     return acc;
 }
 
-// Items of one frame, written 4 at a time (16-B aligned).
+// Items of one frame, two per 16-byte store.  Item = (w0, w1):
+//   w0 = frame offset of the sequence's first literal byte (bits 0-29),
+//        bit 31 = extended: the NEXT item is (literal length, match length);
+//   w1 = match offset (bits 0-15) | literal length (16-23) |
+//        match code (24-31: 0 = no match, else match length - 3).
+// Extended items (literal > 255 or match > 258: long runs, stored blocks)
+// never start at slot 63 of a 64-item batch (a zero padding item goes
+// first), so the exec kernel finds both halves in one wave.
 struct Sink {
-    uint32_t *base;
+    uint64_t *base;
     uint32_t k, cap;
     u32x4 acc;
 
-    __device__ __forceinline__ bool put(uint32_t x)
+    __device__ __forceinline__ bool put1(uint32_t w0, uint32_t w1)
     {
         if (k >= cap)
             return false;
-        uint32_t s = k & 3;
-        acc.x = s == 0 ? x : acc.x;
-        acc.y = s == 1 ? x : acc.y;
-        acc.z = s == 2 ? x : acc.z;
-        acc.w = s == 3 ? x : acc.w;
+        if (k & 1) {
+            acc.z = w0;
+            acc.w = w1;
+            *reinterpret_cast<u32x4 *>(base + k - 1) = acc;
+        } else {
+            acc.x = w0;
+            acc.y = w1;
+        }
         k++;
-        if ((k & 3) == 0)
-            *reinterpret_cast<u32x4 *>(base + k - 4) = acc;
         return true;
+    }
+    __device__ __forceinline__ bool seq(uint32_t lsrc, uint32_t lit, uint32_t off, uint32_t ml)
+    {
+        if (lit > 255 || ml > 258) {
+            if ((k & 63) == 63 && !put1(0, 0))
+                return false;
+            return put1(lsrc | kItemExt, off) && put1(lit, ml);
+        }
+        return put1(lsrc, off | (lit << 16) | ((ml ? ml - 3 : 0) << 24));
     }
     __device__ __forceinline__ void finish()
     {
-        if (k & 3)
-            *reinterpret_cast<u32x4 *>(base + (k & ~3u)) = acc;
+        if (k & 1)
+            *reinterpret_cast<u32x4 *>(base + k - 1) = acc;
     }
 };
 
@@ -234,13 +194,15 @@ __device__ int32_t parse_block(LaneIn &in, Sink &sink, uint32_t ip, uint32_t bsi
                 return ST_BLOCK_ERR;
             if (op + lit > dlen)
                 return ST_DST_OVERFLOW;
-            if (!sink.put(ip | kItemLast))
+            if (!sink.seq(p, lit, 0, 0))
                 return ST_NOT_RUN;
             *op_out = op + lit;
             return ST_OK;
         }
         if (op + lit > dlen)
             return ST_DST_OVERFLOW;
+        const uint32_t lsrc = p;
+        const uint32_t nlit = lit;
         p += lit;
         op += lit;
         uint32_t off = in.word(p) & 0xFFFF;
@@ -264,7 +226,7 @@ __device__ int32_t parse_block(LaneIn &in, Sink &sink, uint32_t ip, uint32_t bsi
             return ST_BLOCK_ERR;
         if (op + ml > dlen)
             return ST_DST_OVERFLOW;
-        if (!sink.put(ip))
+        if (!sink.seq(lsrc, nlit, off, ml))
             return ST_NOT_RUN;
         op += ml;
         ip = p;
@@ -329,7 +291,7 @@ __device__ int32_t parse_frame(LaneIn &in, Sink &sink, uint32_t clen, uint32_t d
         if (bh & 0x80000000u) {
             if (op + bsize > dlen)
                 return ST_DST_OVERFLOW;
-            if (!sink.put(ip | kItemStored))
+            if (!sink.seq(ip, bsize, 0, 0))
                 return ST_NOT_RUN;
             op += bsize;
         } else {
@@ -355,24 +317,6 @@ __device__ int32_t parse_frame(LaneIn &in, Sink &sink, uint32_t clen, uint32_t d
     if (op != dlen)
         return ST_SHORT_FRAME;
     return ST_OK;
-}
-
-__device__ __forceinline__ uint64_t wave_min64(uint64_t v)
-{
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint64_t o = __shfl_xor(v, m, 64);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-
-__device__ __forceinline__ uint64_t wave_max64(uint64_t v)
-{
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint64_t o = __shfl_xor(v, m, 64);
-        v = o > v ? o : v;
-    }
-    return v;
 }
 
 // ---- plan: per-frame item slot offsets ------------------------------------
@@ -409,7 +353,7 @@ __global__ __launch_bounds__(1024) void lz4_plan_kernel(const FrameDesc *__restr
 __global__ __launch_bounds__(256) void lz4_parse_kernel(const FrameDesc *__restrict__ desc,
                                                         uint32_t n, const uint8_t *__restrict__ comp,
                                                         const uint64_t *__restrict__ rec_base,
-                                                        uint64_t capacity, uint32_t *__restrict__ items,
+                                                        uint64_t capacity, uint64_t *__restrict__ items,
                                                         uint32_t *__restrict__ nitems,
                                                         int32_t *__restrict__ status,
                                                         uint32_t *__restrict__ fail_at)
@@ -451,34 +395,6 @@ __global__ __launch_bounds__(256) void lz4_parse_kernel(const FrameDesc *__restr
 }
 
 // ---- exec: one wave per frame ----------------------------------------------
-
-// store the first n (1..16) bytes of v at p, never touching p[n..]
-__device__ __forceinline__ void store_exact(uint8_t *p, u32x4 v, uint32_t n)
-{
-    if (n >= 16) {
-        *reinterpret_cast<u32x4_u *>(p) = v;
-        return;
-    }
-    if (n & 8) {
-        *reinterpret_cast<u64_u *>(p) = ((uint64_t)v.y << 32) | v.x;
-        p += 8;
-        v.x = v.z;
-        v.y = v.w;
-    }
-    if (n & 4) {
-        *reinterpret_cast<u32_u *>(p) = v.x;
-        p += 4;
-        v.x = v.y;
-    }
-    if (n & 2) {
-        p[0] = (uint8_t)v.x;
-        p[1] = (uint8_t)(v.x >> 8);
-        p += 2;
-        v.x >>= 16;
-    }
-    if (n & 1)
-        p[0] = (uint8_t)v.x;
-}
 
 // 16 bytes of the frame's output at offset p (bytes past the frame read as 0)
 __device__ __forceinline__ u32x4 load16_out(const Span &o, uint32_t p)
@@ -528,7 +444,7 @@ __device__ __forceinline__ uint32_t uni_lane(uint32_t v, int l)
 // produced `done` bytes, the source may be any multiple E of off with
 // E <= done + off (those bytes are already final); a step writes at most E
 // bytes so no lane reads what another lane of the same step writes.
-__device__ __noinline__ void copy_match_wave(uint8_t *out, const Span &orr, uint32_t dst,
+__device__ __forceinline__ void copy_match_wave(uint8_t *out, const Span &orr, uint32_t dst,
                                              uint32_t off, uint32_t n, uint32_t lane)
 {
     uint32_t done = 0;
@@ -553,18 +469,105 @@ __device__ __noinline__ void copy_match_wave(uint8_t *out, const Span &orr, uint
     }
 }
 
+// Largest lane k with ex[k] <= t (ex non-decreasing over lanes, ex[0] = 0).
+__device__ __forceinline__ int run_of(uint32_t ex, uint32_t t)
+{
+    int k = 0;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1)
+        if ((uint32_t)__shfl(ex, k + s, 64) <= t)
+            k += s;
+    return k;
+}
+
+__device__ __forceinline__ uint32_t excl_scan(uint32_t v, uint32_t lane, uint32_t *total)
+{
+    uint32_t inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        uint32_t u = __shfl_up(inc, d, 64);
+        if (lane >= d)
+            inc += u;
+    }
+    *total = (uint32_t)__shfl(inc, 63, 64);
+    return inc - v;
+}
+
+// Byte-parallel copy of two sets of runs, one of each per lane: a literal run
+// (ln bytes from compressed offset ls to output offset ld) and a match run
+// (mn bytes from output offset ms to output offset md; source and destination
+// must not overlap).  Every lane copies the first 16-byte piece of its own
+// runs; the remaining pieces of all runs are dealt round-robin over the wave
+// (run found by binary search over the piece prefix sums), so a batch with one
+// long run costs as many wave steps as its pieces / 64, not its length / 16.
+__device__ __forceinline__ void copy_runs(const Span &isp, const Span &osp, uint8_t *o,
+                                          uint32_t ls, uint32_t ld, uint32_t ln,
+                                          uint32_t ms, uint32_t md, uint32_t mn, uint32_t lane)
+{
+    u32x4 a, b;
+    if (ln)
+        a = load16u(isp.r, isp.s0 + ls);
+    if (mn)
+        b = load16_out(osp, ms);
+    const uint32_t lr = ln > 16 ? (ln - 1) >> 4 : 0;   // pieces after the first
+    const uint32_t mr = mn > 16 ? (mn - 1) >> 4 : 0;
+    uint32_t lt, mt;
+    const uint32_t lx = excl_scan(lr, lane, &lt);
+    const uint32_t mx = excl_scan(mr, lane, &mt);
+    if (ln)
+        store_exact(o + ld, a, ln < 16 ? ln : 16);
+    if (mn)
+        store_exact(o + md, b, mn < 16 ? mn : 16);
+    const uint32_t tt = lt > mt ? lt : mt;
+    for (uint32_t t = lane; t - lane < tt; t += 128) {
+        const uint32_t t1 = t + 64;
+        // literal pieces t, t1 and match pieces t, t1
+        const int kl0 = run_of(lx, t), kl1 = run_of(lx, t1);
+        const int km0 = run_of(mx, t), km1 = run_of(mx, t1);
+        const uint32_t il0 = 16 * (t - (uint32_t)__shfl(lx, kl0, 64) + 1);
+        const uint32_t il1 = 16 * (t1 - (uint32_t)__shfl(lx, kl1, 64) + 1);
+        const uint32_t im0 = 16 * (t - (uint32_t)__shfl(mx, km0, 64) + 1);
+        const uint32_t im1 = 16 * (t1 - (uint32_t)__shfl(mx, km1, 64) + 1);
+        const uint32_t sl0 = (uint32_t)__shfl(ls, kl0, 64) + il0, dl0 = (uint32_t)__shfl(ld, kl0, 64) + il0;
+        const uint32_t sl1 = (uint32_t)__shfl(ls, kl1, 64) + il1, dl1 = (uint32_t)__shfl(ld, kl1, 64) + il1;
+        const uint32_t sm0 = (uint32_t)__shfl(ms, km0, 64) + im0, dm0 = (uint32_t)__shfl(md, km0, 64) + im0;
+        const uint32_t sm1 = (uint32_t)__shfl(ms, km1, 64) + im1, dm1 = (uint32_t)__shfl(md, km1, 64) + im1;
+        const uint32_t nl0 = (uint32_t)__shfl(ln, kl0, 64) - il0, nl1 = (uint32_t)__shfl(ln, kl1, 64) - il1;
+        const uint32_t nm0 = (uint32_t)__shfl(mn, km0, 64) - im0, nm1 = (uint32_t)__shfl(mn, km1, 64) - im1;
+        const bool pl0 = t < lt, pl1 = t1 < lt, pm0 = t < mt, pm1 = t1 < mt;
+        u32x4 v0, v1, v2, v3;
+        if (pl0)
+            v0 = load16u(isp.r, isp.s0 + sl0);
+        if (pl1)
+            v1 = load16u(isp.r, isp.s0 + sl1);
+        if (pm0)
+            v2 = load16_out(osp, sm0);
+        if (pm1)
+            v3 = load16_out(osp, sm1);
+        if (pl0)
+            store_exact(o + dl0, v0, nl0 < 16 ? nl0 : 16);
+        if (pl1)
+            store_exact(o + dl1, v1, nl1 < 16 ? nl1 : 16);
+        if (pm0)
+            store_exact(o + dm0, v2, nm0 < 16 ? nm0 : 16);
+        if (pm1)
+            store_exact(o + dm1, v3, nm1 < 16 ? nm1 : 16);
+    }
+}
+
 // Diagnostic counters of the exec kernel (tuning builds only, DIAG & 8):
 // [0] batches, [1] resolution rounds, [2] long literal runs, [3] long matches,
-// [4] sequences, [5] matches resolved in round 1
+// [4] sequences, [5] matches copied in round 0
 __device__ unsigned long long g_exec_stats[8];
 
 // DIAG (tuning builds): 1 = no wait between resolution rounds, 2 = skip
-// back-references, 4 = skip all copies, 8 = count (g_exec_stats)
-template <int DIAG>
-__global__ __launch_bounds__(64 * kExecWaves) void lz4_exec_kernel(
+// back-references, 8 = count (g_exec_stats), 16 = round 0 only.  OCC: minimum
+// waves per SIMD the register allocation must allow.
+template <int DIAG, int OCC = 1>
+__global__ __launch_bounds__(64 * kExecWaves) __attribute__((amdgpu_waves_per_eu(OCC))) void lz4_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
-    const uint32_t *__restrict__ items, const uint32_t *__restrict__ nitems,
+    const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     const int32_t *__restrict__ status)
 {
     const uint32_t lane = threadIdx.x & 63;
@@ -575,53 +578,31 @@ __global__ __launch_bounds__(64 * kExecWaves) void lz4_exec_kernel(
         return;
     const FrameDesc d = desc[f];
     const uint32_t nit = uni(nitems[f]);
-    const uint32_t *it = items + rec_base[f];
+    const uint64_t *it = items + rec_base[f];
     uint8_t *o = out + d.d_off;
     const Span osp = make_span(o, d.d_size);
-    const Span sp = make_span(comp + d.c_off, d.c_size);
-    LaneIn in;
-    in.r = sp.r;
-    in.s0 = sp.s0;
-    in.wp = 0x80000000u;
+    const Span isp = make_span(comp + d.c_off, d.c_size);
     uint32_t obase = 0;
+    uint64_t cur = lane < nit ? it[lane] : 0;
     for (uint32_t b = 0; b < nit; b += 64) {
-        const uint32_t j = b + lane;
-        const bool act = j < nit;
-        uint32_t lit = 0, ml = 0, off = 0, src = 0;
-        if (act) {
-            const uint32_t item = it[j];
-            const uint32_t pos = item & kItemPos;
-            if (item & kItemStored) {
-                lit = in.word(pos - 4) & 0x7FFFFFFFu;
-                src = pos;
-            } else {
-                in.at(pos);
-                uint32_t tok = in.byte(pos);
-                lit = tok >> 4;
-                uint32_t p = pos + 1;
-                if (lit == 15) {
-                    uint32_t s;
-                    do {
-                        s = in.byte(p++);
-                        lit += s;
-                    } while (s == 255);
-                }
-                src = p;
-                if (!(item & kItemLast)) {
-                    p += lit;
-                    off = in.word(p) & 0xFFFF;
-                    p += 2;
-                    ml = tok & 15;
-                    if (ml == 15) {
-                        uint32_t s;
-                        do {
-                            s = in.byte(p++);
-                            ml += s;
-                        } while (s == 255);
-                    }
-                    ml += kMinMatch;
-                }
-            }
+        const uint64_t nxt = b + 64 + lane < nit ? it[b + 64 + lane] : 0;   // next batch, early
+        const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
+        const uint32_t w0n = __shfl_down(w0, 1, 64), w1n = __shfl_down(w1, 1, 64);
+        const uint32_t w0p = __shfl_up(w0, 1, 64);
+        const bool is_ext = lane > 0 && (w0p & kItemExt);
+        const uint32_t src = w0 & kItemPos;
+        const uint32_t off = w1 & 0xFFFF;
+        uint32_t lit, ml;
+        if (is_ext) {
+            lit = 0;
+            ml = 0;
+        } else if (w0 & kItemExt) {
+            lit = w0n;
+            ml = w1n;
+        } else {
+            lit = (w1 >> 16) & 0xFF;
+            const uint32_t mc = w1 >> 24;
+            ml = mc ? mc + 3 : 0;
         }
         // output positions: exclusive wave prefix sum of lit + ml
         const uint32_t len = lit + ml;
@@ -631,75 +612,57 @@ __global__ __launch_bounds__(64 * kExecWaves) void lz4_exec_kernel(
             if (lane >= dlt)
                 inc += v;
         }
+        const uint32_t bstart = obase;
         const uint32_t op = obase + inc - len;
         obase += (uint32_t)__shfl(inc, 63, 64);
-        if (DIAG & 8) {
-            if (lane == 0) {
-                atomicAdd(&g_exec_stats[0], 1ull);
-                atomicAdd(&g_exec_stats[4], (unsigned long long)(nit - b < 64 ? nit - b : 64));
-            }
-        }
-        if (DIAG & 4)
-            continue;
-        // literal runs: compressed image -> output; a lane copies its own
-        // short run, long runs (and stored blocks) are copied by the wave
-        if ((DIAG & 8) && lane == 0) {
-            atomicAdd(&g_exec_stats[2], (unsigned long long)__popcll(__ballot(lit > kLongRun)));
-            atomicAdd(&g_exec_stats[3], (unsigned long long)__popcll(__ballot(ml > kLongRun)));
-        }
-        if (lit <= kLongRun) {
-            for (uint32_t k = 0; k < lit; k += 16) {
-                u32x4 v = in.load16(src + k);
-                uint32_t r = lit - k;
-                store_exact(o + op + k, v, r < 16 ? r : 16);
-            }
-        }
-        for (uint64_t lm = __ballot(lit > kLongRun); lm; lm &= lm - 1) {
-            const int l = __builtin_ctzll(lm);
-            const uint32_t ls = uni_lane(src, l), lo = uni_lane(op, l), ln = uni_lane(lit, l);
-            for (uint32_t k = 16 * lane; k < ln; k += 1024) {
-                u32x4 v = in.load16(ls + k);
-                uint32_t r = ln - k;
-                store_exact(o + lo + k, v, r < 16 ? r : 16);
-            }
-        }
-        // back-references, multi-round resolution
         const uint32_t mb = op + lit;
         const uint32_t me = mb + ml;
         const uint32_t msrc = mb - off;
         const uint32_t need = off >= ml ? msrc + ml : mb;   // end of the bytes the copy reads
-        uint64_t pending = (DIAG & 2) ? 0 : __ballot(ml != 0);
-        bool first_round = true;
+        if (DIAG & 2)
+            ml = 0;
+        // round 0: literal runs and matches whose source lies before this
+        // batch (already final), loads of both in flight together
+        const bool early = ml != 0 && off >= ml && need <= bstart;
+        copy_runs(isp, osp, o, src, op, lit, msrc, mb, early ? ml : 0, lane);
+        if (DIAG & 8) {
+            const uint64_t bl = __ballot(lit > kLongCopy), bm = __ballot(ml > kLongCopy), be = __ballot(early);
+            if (lane == 0) {
+                atomicAdd(&g_exec_stats[0], 1ull);
+                atomicAdd(&g_exec_stats[4], (unsigned long long)(nit - b < 64 ? nit - b : 64));
+                atomicAdd(&g_exec_stats[2], (unsigned long long)__popcll(bl));
+                atomicAdd(&g_exec_stats[3], (unsigned long long)__popcll(bm));
+                atomicAdd(&g_exec_stats[5], (unsigned long long)__popcll(be));
+            }
+        }
+        // the rest: multi-round resolution.  Lane k may copy once its source
+        // range [msrc, need) misses every pending match below it: it ends
+        // before the lowest pending match starts, or starts after the nearest
+        // pending one below ends (pending ranges are ordered by lane).
+        uint64_t pending = (DIAG & 16) ? 0 : __ballot(ml != 0 && !early);
         while (pending) {
             if (!(DIAG & 1))
                 __builtin_amdgcn_s_waitcnt(0);   // earlier rounds' stores complete
-            // lane k may copy once its source range [msrc, need) misses every
-            // pending match below it: it ends before the lowest pending
-            // match starts, or starts after the nearest pending one below
-            // ends (pending ranges are ordered by lane)
             const uint64_t below = pending & ((1ull << lane) - 1);
             const int hb = below ? 63 - __builtin_clzll(below) : (int)lane;
             const uint32_t me_hb = (uint32_t)__shfl(me, hb, 64);
             const uint32_t frontier = uni_lane(mb, __builtin_ctzll(pending));
             const bool mine = (pending >> lane) & 1;
             const bool ready = mine && (below == 0 || need <= frontier || msrc >= me_hb);
-            if (ready && ml <= kLongRun)
+            const bool over = off < ml;   // overlapping copy: serial pieces
+            if (ready && over && ml <= kLongCopy)
                 copy_match(o, osp, mb, off, ml);
+            copy_runs(isp, osp, o, 0, 0, 0, msrc, mb, ready && !over ? ml : 0, lane);
             const uint64_t rmask = __ballot(ready);
-            for (uint64_t lm = __ballot(ready && ml > kLongRun); lm; lm &= lm - 1) {
+            for (uint64_t lm = __ballot(ready && over && ml > kLongCopy); lm; lm &= lm - 1) {
                 const int l = __builtin_ctzll(lm);
                 copy_match_wave(o, osp, uni_lane(mb, l), uni_lane(off, l), uni_lane(ml, l), lane);
             }
             pending &= ~rmask;
-            if (DIAG & 8) {
-                if (lane == 0) {
-                    atomicAdd(&g_exec_stats[1], 1ull);
-                    if (first_round)
-                        atomicAdd(&g_exec_stats[5], (unsigned long long)__popcll(rmask));
-                }
-            }
-            first_round = false;
+            if ((DIAG & 8) && lane == 0)
+                atomicAdd(&g_exec_stats[1], 1ull);
         }
+        cur = nxt;
     }
 }
 
@@ -711,7 +674,7 @@ uint64_t split_items_needed(const FrameDesc *h_desc, uint32_t n)
 {
     uint64_t s = 0;
     for (uint32_t i = 0; i < n; i++)
-        s += (h_desc[i].c_size / 3 + 2 + 3) & ~3u;
+        s += slots_of(h_desc[i].c_size);
     return s;
 }
 
@@ -757,7 +720,7 @@ int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipS
             (void)hipFree(s->items);
         s->items = nullptr;
         s->items_cap = 0;
-        if (hipMalloc((void **)&s->items, cap * 4 + 64) != hipSuccess)
+        if (hipMalloc((void **)&s->items, cap * 8 + 64) != hipSuccess)
             return -1;
         s->items_cap = cap;
     }
@@ -781,17 +744,22 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         hipLaunchKernelGGL(lz4_parse_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                            s->nitems, d_status, d_fail_at);
-    if (stages & 4) {
+    if ((stages & 4) && diag == 0x200) {
+        launch_lz4_exec_stage(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems,
+                              d_status, stream);
+    } else if (stages & 4) {
         const dim3 grid((nframes + kExecWaves - 1) / kExecWaves), block(64 * kExecWaves);
-#define ZSK_EXEC(D)                                                                            \
-    hipLaunchKernelGGL(lz4_exec_kernel<D>, grid, block, 0, stream, d_desc, nframes, d_comp, d_out, \
-                       s->rec_base, s->items, s->nitems, d_status)
+#define ZSK_EXEC(D, O)                                                                          \
+    hipLaunchKernelGGL((lz4_exec_kernel<D, O>), grid, block, 0, stream, d_desc, nframes, d_comp, \
+                       d_out, s->rec_base, s->items, s->nitems, d_status)
         switch (diag) {
-        case 1: ZSK_EXEC(1); break;
-        case 2: ZSK_EXEC(2); break;
-        case 4: ZSK_EXEC(4); break;
-        case 8: ZSK_EXEC(8); break;
-        default: ZSK_EXEC(0); break;
+        case 1: ZSK_EXEC(1, 1); break;
+        case 2: ZSK_EXEC(2, 1); break;
+        case 8: ZSK_EXEC(8, 1); break;
+        case 16: ZSK_EXEC(16, 1); break;
+        case 0x106: ZSK_EXEC(0, 6); break;
+        case 0x108: ZSK_EXEC(0, 8); break;
+        default: ZSK_EXEC(0, 1); break;
         }
 #undef ZSK_EXEC
     }
@@ -811,18 +779,55 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
 {
     if (nframes == 0)
         return 0;
+    switch (lz4_pick_engine(nframes)) {
+    case ENGINE_LANE: return launch_lz4_lane(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
+    case ENGINE_WAVE: return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
+    default: break;
+    }
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, SplitScratch> cache;
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> g(mu);
     SplitScratch &s = cache[{dev, stream}];
-    uint64_t want = (uint64_t)nframes * 21856;   // 64 KiB frames at any ratio
+    // first call: room for 64 KiB frames (capped at 2 GiB of items); later
+    // calls: what the previous plan on this stream needed
+    uint64_t want = (uint64_t)nframes * slots_of(65536 + 64);
+    if (want > (256ull << 20))
+        want = 256ull << 20;
     if (s.total && *s.total > want)
         want = *s.total;
     if (split_scratch_reserve(&s, nframes, want, stream) != 0)
         return launch_lz4_wave(0, d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
     return launch_lz4_split(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream, &s);
+}
+
+// Automatic choice: the lane-per-frame kernel needs about one
+// frame per lane of the chip to hide its per-frame latency (>= 32768 frames);
+// smaller batches go to the wave-per-frame kernel.
+int lz4_pick_engine(uint32_t nframes)
+{
+    const int e = lz4_engine();
+    if (e != ENGINE_AUTO)
+        return e;
+    return nframes >= 32768 ? ENGINE_LANE : ENGINE_WAVE;
+}
+
+int lz4_engine()
+{
+    static const int e = [] {
+        const char *v = getenv("ZSEEK_HIP_KERNEL");
+        if (!v)
+            return (int)ENGINE_AUTO;
+        if (!strcmp(v, "lane"))
+            return (int)ENGINE_LANE;
+        if (!strcmp(v, "split"))
+            return (int)ENGINE_SPLIT;
+        if (!strcmp(v, "wave"))
+            return (int)ENGINE_WAVE;
+        return (int)ENGINE_AUTO;
+    }();
+    return e;
 }
 
 // Tuning hook: the split decoder with a subset of its stages (bitmask:
@@ -834,7 +839,12 @@ int launch_lz4_split_stages(int stages, int diag, const FrameDesc *d_desc, uint3
     static std::mutex mu;
     static SplitScratch s;
     std::lock_guard<std::mutex> g(mu);
-    if (split_scratch_reserve(&s, nframes, (uint64_t)nframes * 21856, stream) != 0)
+    uint64_t want = (uint64_t)nframes * slots_of(65536 + 64);
+    if (want > (256ull << 20))
+        want = 256ull << 20;
+    if (s.total && *s.total > want)
+        want = *s.total;
+    if (split_scratch_reserve(&s, nframes, want, stream) != 0)
         return -1;
     if (diag & 8) {
         unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -856,9 +866,13 @@ int launch_lz4_split_stages(int stages, int diag, const FrameDesc *d_desc, uint3
     return rc;
 }
 
-const char *lz4_kernel_name()
+const char *lz4_kernel_name(uint32_t nframes)
 {
-    return "lz4_exec_kernel";
+    switch (lz4_pick_engine(nframes)) {
+    case ENGINE_LANE: return "lz4_lane_kernel";
+    case ENGINE_SPLIT: return "lz4_exec_kernel";
+    default: return "lz4_wave_kernel<4096, 4>";
+    }
 }
 
 }   // namespace zsk

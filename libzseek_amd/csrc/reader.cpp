@@ -233,11 +233,20 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
                            g.stream);
     if (e == hipSuccess)
         e = hipMemsetD32Async((hipDeviceptr_t)g.d_status, ST_NOT_RUN, n, g.stream);
-    if (e == hipSuccess &&
+    const int engine = lz4_pick_engine((uint32_t)n);
+    if (e == hipSuccess && engine == ENGINE_LANE &&
+        launch_lz4_lane(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
+                        g.stream) != 0)
+        e = hipErrorLaunchFailure;
+    if (e == hipSuccess && engine == ENGINE_WAVE &&
+        launch_lz4_wave(0, g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
+                        g.stream) != 0)
+        e = hipErrorLaunchFailure;
+    if (e == hipSuccess && engine == ENGINE_SPLIT &&
         split_scratch_reserve(&g.split, (uint32_t)n, split_items_needed(g.h_desc, (uint32_t)n),
                               g.stream) != 0)
         e = hipErrorOutOfMemory;
-    if (e == hipSuccess &&
+    if (e == hipSuccess && engine == ENGINE_SPLIT &&
         launch_lz4_split(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
                          g.stream, &g.split) != 0)
         e = hipErrorLaunchFailure;
@@ -593,9 +602,9 @@ extern "C" ZSEEK_EXPORT int zsk_dev_lz4_decode_variant(int variant, const zsk_fr
                                      static_cast<hipStream_t>(stream));
 }
 
-extern "C" ZSEEK_EXPORT const char *zsk_lz4_kernel_name(void)
+extern "C" ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes)
 {
-    return zsk::lz4_kernel_name();
+    return zsk::lz4_kernel_name(nframes);
 }
 
 extern "C" ZSEEK_EXPORT const char *zsk_status_string(int32_t status)

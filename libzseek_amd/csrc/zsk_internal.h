@@ -59,7 +59,7 @@ inline uint32_t status_max_block(int32_t st)
 // whose decode failed.
 // Name (template instance) of the kernel launch_lz4_frames uses, for
 // matching profiler output.
-const char *lz4_kernel_name();
+const char *lz4_kernel_name(uint32_t nframes);
 
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
@@ -70,7 +70,7 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
 struct SplitScratch {
     uint64_t *rec_base = nullptr;   // [frames_cap]
     uint32_t *nitems = nullptr;     // [frames_cap]
-    uint32_t *items = nullptr;      // [items_cap]
+    uint64_t *items = nullptr;      // [items_cap], 8-byte items
     uint64_t *total = nullptr;      // host-mapped: item slots the last plan needed
     uint32_t frames_cap = 0;
     uint64_t items_cap = 0;
@@ -90,6 +90,22 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 int launch_lz4_split_stages(int stages, int diag, const FrameDesc *d_desc, uint32_t nframes,
                             const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
                             hipStream_t stream);
+
+// Decoder selection (env ZSEEK_HIP_KERNEL = lane | split | wave; default auto).
+enum : int { ENGINE_AUTO = 0, ENGINE_LANE, ENGINE_SPLIT, ENGINE_WAVE };
+int lz4_engine();
+int lz4_pick_engine(uint32_t nframes);   // never ENGINE_AUTO
+
+// Execute phase with LDS-staged output (lz4_stage.hip), over the split
+// decoder's items.
+int launch_lz4_exec_stage(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                          uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
+                          const uint32_t *nitems, const int32_t *d_status, hipStream_t stream);
+
+// Lane-per-frame decoder (lz4_lane.hip) + hand-offs to the wave kernel.
+int launch_lz4_lane(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                    uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
+                    int diag = 0);
 
 // Wave-per-frame kernel over only the frames whose status is ST_NOT_RUN
 // (the split decoder's hand-offs).

@@ -128,8 +128,11 @@ def lib() -> C.CDLL:
     L.zsk_lz4_decode_frames.restype = C.c_int
     L.zsk_lz4_decode_frames.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_void_p]
+    L.zsk_dev_lz4_decode_variant.restype = C.c_int
+    L.zsk_dev_lz4_decode_variant.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p,
+                                             C.c_void_p, C.c_void_p, C.c_void_p]
     L.zsk_lz4_kernel_name.restype = C.c_char_p
-    L.zsk_lz4_kernel_name.argtypes = []
+    L.zsk_lz4_kernel_name.argtypes = [C.c_uint32]
     L.zsk_status_string.restype = C.c_char_p
     L.zsk_status_string.argtypes = [C.c_int32]
     L.zsk_reader_frames.restype = C.c_ssize_t
@@ -412,12 +415,19 @@ def seek_table_of(image: np.ndarray):
         r.close()
 
 
-def decode_frames(desc, comp, out, status, stream: int | None = None) -> None:
+# Decoder engines reachable through the (non-ABI) tuning hook
+# zsk_dev_lz4_decode_variant: each one a complete decoder incl. its hand-offs.
+ENGINES = {"wave": 20, "lane": 50, "split": 35, "stage": 34}
+
+
+def decode_frames(desc, comp, out, status, stream: int | None = None,
+                  engine: str | None = None) -> None:
     """Launch zsk_lz4_decode_frames on torch CUDA(HIP) tensors (async).
 
     desc: uint8 tensor holding N x 24-byte zsk_frame_desc_t; comp / out: uint8
     tensors; status: int32 tensor of N.  `stream` is a raw hipStream_t
     (torch.cuda.Stream.cuda_stream); None = the current torch stream.
+    `engine` forces one decoder (tests / tuning; None = the library's choice).
     """
     import torch
     n = status.numel()
@@ -428,7 +438,12 @@ def decode_frames(desc, comp, out, status, stream: int | None = None) -> None:
             raise ValueError("decode_frames needs contiguous device tensors")
     if stream is None:
         stream = torch.cuda.current_stream().cuda_stream
-    rc = lib().zsk_lz4_decode_frames(desc.data_ptr(), n, comp.data_ptr(), out.data_ptr(),
-                                     status.data_ptr(), stream)
+    if engine is None:
+        rc = lib().zsk_lz4_decode_frames(desc.data_ptr(), n, comp.data_ptr(), out.data_ptr(),
+                                         status.data_ptr(), stream)
+    else:
+        rc = lib().zsk_dev_lz4_decode_variant(ENGINES[engine], desc.data_ptr(), n,
+                                              comp.data_ptr(), out.data_ptr(),
+                                              status.data_ptr(), stream)
     if rc != 0:
         raise ZseekError("zsk_lz4_decode_frames launch failed")
