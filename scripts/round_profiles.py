@@ -28,8 +28,12 @@ def one(pattern):
     return f[0]
 
 
+bench = json.load(open(os.path.join(src, "bench.json")))
+KERNEL = bench["roofline"]["kernel"]   # the dominant kernel bench.py reports
+
+
 def is_decode(name):
-    return "lz4" in name and "zsk" in name
+    return KERNEL in name
 
 
 stats = one("trace/*/*_kernel_stats.csv")
@@ -48,7 +52,6 @@ for name in ("fetch", "write"):
             counters.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
 fetch = statistics.median(counters["FETCH_SIZE"]) * 1024
 write = statistics.median(counters["WRITE_SIZE"]) * 1024
-bench = json.load(open(os.path.join(src, "bench.json")))
 alg = bench["roofline"]["algorithmic_bytes_per_launch"]
 out = {
     "round": tag,
