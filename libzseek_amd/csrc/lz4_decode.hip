@@ -642,6 +642,7 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 31: return launch_lz4_split_stages(3, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 32: return launch_lz4_split_stages(7, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 33: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 36: return launch_lz4_split_stages(15, 0x201, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 35: return launch_lz4_split_stages(15, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0x200, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 40: return launch_lz4_split_stages(7, 1, d_desc, nframes, d_comp, d_out, d_status, stream);

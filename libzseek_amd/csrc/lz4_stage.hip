@@ -450,16 +450,289 @@ __global__ __launch_bounds__(64 * kSW) void lz4_stage_kernel(
     }
 }
 
+// ---- pipelined variant: the next batch's loads fly while this one is staged
+
+constexpr uint32_t kOff = 0xFFFFFFFFu;   // no piece
+constexpr uint32_t kPF = 6;          // prefetched 16-byte pieces per lane per batch
+constexpr uint32_t kBatch2 = 6144;   // output bytes per batch at most (2 batches + carry fit the ring)
+
+struct PBatch {
+    uint32_t b, nb, used;            // first item, items staged (0 = one long sequence), items consumed
+    uint32_t bs, be;                 // frame output range
+    uint32_t hv;                     // frame bytes below this were in HBM when prepared
+    uint32_t lit, ml, off, src, op;  // this lane's sequence
+    uint32_t early;                  // 1: match source final at prepare and in HBM (prefetched),
+                                     // 2: final but (partly) in the ring
+    uint32_t tp;                     // prefetched pieces (literal + HBM match) in the batch
+    u32x4 pd[kPF];                   // prefetched piece data, pieces lane + 64 j
+    uint32_t pdst[kPF], pn[kPF];     // piece output offset (kOff = none), bytes
+};
+
+// Decode the items at B.b (lane's item: itc), cut the batch, lay out its
+// output from `produced`, and issue the loads of its literal pieces and of
+// the pieces of matches whose source is already in HBM (below hv).
+__device__ __forceinline__ void prepare(PBatch &B, uint64_t itc, uint32_t nit, uint32_t produced,
+                                        uint32_t hv, const Span &isp, const Out &O, uint32_t lane)
+{
+    const uint32_t w0 = (uint32_t)itc, w1 = (uint32_t)(itc >> 32);
+    const uint32_t w0n = __shfl_down(w0, 1, 64), w1n = __shfl_down(w1, 1, 64);
+    const uint32_t w0p = __shfl_up(w0, 1, 64);
+    const bool act0 = B.b + lane < nit;
+    const bool is_ext = lane > 0 && (w0p & kItemExt);
+    uint32_t lit = 0, ml = 0;
+    if (act0 && !is_ext) {
+        if (w0 & kItemExt) {
+            lit = w0n;
+            ml = w1n;
+        } else {
+            lit = (w1 >> 16) & 0xFF;
+            const uint32_t mc = w1 >> 24;
+            ml = mc ? mc + 3 : 0;
+        }
+    }
+    const uint32_t len = lit + ml;
+    uint32_t tot;
+    const uint32_t ex = excl_scan(len, lane, &tot);
+    const uint64_t over = __ballot(act0 && ex + len > kBatch2);
+    uint32_t nb = over ? (uint32_t)__builtin_ctzll(over) : 64;
+    if (nb == 64 && (uni_lane(w0, 63) & kItemExt))
+        nb = 63;
+    else if (nb > 0 && nb < 64 && (uni_lane(w0, (int)nb - 1) & kItemExt))
+        nb++;
+    if (B.b + nb > nit)
+        nb = nit - B.b;
+    B.nb = nb;
+    B.bs = produced;
+    B.hv = hv;
+    B.src = w0 & kItemPos;
+    B.off = w1 & 0xFFFF;
+    B.tp = 0;
+#pragma unroll
+    for (int j = 0; j < (int)kPF; j++)
+        B.pdst[j] = kOff;
+    if (nb == 0) {
+        // one sequence too long to stage: copied in HBM when processed
+        B.used = (uni_lane(w0, 0) & kItemExt) ? 2 : 1;
+        B.lit = lit;
+        B.ml = ml;
+        B.op = produced;
+        B.early = 0;
+        B.be = produced + uni_lane(len, 0);
+        return;
+    }
+    B.used = nb;
+    const bool act = lane < nb;
+    if (!act) {
+        lit = 0;
+        ml = 0;
+    }
+    B.lit = lit;
+    B.ml = ml;
+    B.op = produced + ex;
+    B.be = produced + (uint32_t)__shfl(ex + len, (int)nb - 1, 64);
+    const uint32_t mb = B.op + lit;
+    const uint32_t msrc = mb - B.off;
+    const bool overlap = ml != 0 && B.off < ml;
+    const bool early = ml != 0 && !overlap && msrc + ml <= produced;
+    const bool in_hbm = early && msrc + ml <= hv;
+    B.early = early ? (in_hbm ? 1 : 2) : 0;
+    const uint32_t lp = npieces(lit), mp = in_hbm ? npieces(ml) : 0;
+    uint32_t lt, mt;
+    const uint32_t lx = excl_scan(lp, lane, &lt);
+    const uint32_t mx = excl_scan(mp, lane, &mt);
+    B.tp = lt + mt;
+#pragma unroll
+    for (int j = 0; j < (int)kPF; j++) {
+        const uint32_t t = lane + 64 * j;
+        if ((uint32_t)(64 * j) >= lt + mt)
+            break;
+        const int kl = run_of(lx, t);
+        const uint32_t tm = t - lt;
+        const int km = run_of(mx, tm);
+        const uint32_t nl = (uint32_t)__shfl(lit, kl, 64), nm = (uint32_t)__shfl(ml, km, 64);
+        const uint32_t ol = piece_off(nl, t - (uint32_t)__shfl(lx, kl, 64));
+        const uint32_t om = piece_off(nm, tm - (uint32_t)__shfl(mx, km, 64));
+        const uint32_t sl = (uint32_t)__shfl(B.src, kl, 64) + ol, dl = (uint32_t)__shfl(B.op, kl, 64) + ol;
+        const uint32_t sm = (uint32_t)__shfl(msrc, km, 64) + om, dm = (uint32_t)__shfl(mb, km, 64) + om;
+        if (t < lt) {
+            B.pd[j] = load16u(isp.r, isp.s0 + sl);
+            B.pdst[j] = dl;
+            B.pn[j] = nl < 16 ? nl : 16;
+        } else if (t < lt + mt) {
+            B.pd[j] = load16u(O.sp.r, O.sp.s0 + sm);
+            B.pdst[j] = dm;
+            B.pn[j] = nm < 16 ? nm : 16;
+        }
+    }
+}
+
+__global__ __launch_bounds__(64 * kSW) void lz4_stage2_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
+    uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
+    const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
+    const int32_t *__restrict__ status)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kSW * kStageRegion];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t f = uni(blockIdx.x * kSW + w);
+    if (f >= n)
+        return;
+    if (uni((uint32_t)status[f]) != (uint32_t)ST_OK)
+        return;
+    const FrameDesc d = desc[f];
+    const uint32_t nit = uni(nitems[f]);
+    const uint64_t *it = items + rec_base[f];
+    Out O;
+    O.o = out + d.d_off;
+    O.dlen = d.d_size;
+    O.sp = make_span(O.o, d.d_size);
+    const Span isp = make_span(comp + d.c_off, d.c_size);
+    Ring R;
+    R.base = (uint32_t)(uintptr_t)(lds + w * kStageRegion + 16);
+    R.a0 = (uint32_t)(reinterpret_cast<uintptr_t>(O.o) & 15);
+    uint32_t fc = 0;   // ring chunks [0, fc) are in HBM
+    PBatch A, B;
+    A.b = 0;
+    uint64_t itc = lane < nit ? it[lane] : 0;
+    if (nit)
+        prepare(A, itc, nit, 0, 0, isp, O, lane);
+    uint32_t nextb = A.used;
+    itc = nextb + lane < nit ? it[nextb + lane] : 0;
+    bool have_next = false;
+    while (A.b < nit) {
+        const uint32_t hv = 16 * fc > R.a0 ? 16 * fc - R.a0 : 0;   // frame bytes < hv are in HBM
+        // the next batch's loads fly while this one is staged (not after a
+        // long sequence: the ring restarts there)
+        have_next = false;
+        if (A.nb != 0 && nextb < nit) {
+            B.b = nextb;
+            prepare(B, itc, nit, A.be, hv, isp, O, lane);
+            nextb = B.b + B.used;
+            itc = nextb + lane < nit ? it[nextb + lane] : 0;
+            have_next = true;
+        }
+        if (A.nb == 0) {
+            // one sequence too long to stage: flush the ring, copy in HBM
+            const uint32_t l0 = uni_lane(A.lit, 0), m0 = uni_lane(A.ml, 0);
+            const uint32_t s0 = uni_lane(A.src, 0), o0 = uni_lane(A.off, 0);
+            const uint32_t produced = A.bs;
+            flush_range(R, O, fc, (produced + R.a0 + 15) >> 4, lane);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (l0)
+                hbm_run(isp, s0, O.o + produced, l0, lane);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (m0) {
+                const uint32_t mb = produced + l0;
+                if (o0 >= m0)
+                    hbm_run(O.sp, mb - o0, O.o + mb, m0, lane);
+                else
+                    hbm_match(O, mb, o0, m0, lane);
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint32_t end = produced + l0 + m0;
+            fc = (end + R.a0) >> 4;
+            if (lane < 2) {
+                const uint32_t c = fc - 1 + lane;   // ring chunks fc-1, fc from HBM
+                const int64_t x0 = (int64_t)16 * c - R.a0;
+                if ((fc > 0 || lane == 1) && x0 >= 0) {
+                    const u32x4 v = load16u(O.sp.r, (uint32_t)((int64_t)O.sp.s0 + x0));
+                    const uint32_t i = (16 * c) & (kStage - 1);
+                    *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(lds_p(R.base + i)) = v;
+                    if (i == 0)
+                        *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(lds_p(R.base + kStage)) = v;
+                    if (i == kStage - 16)
+                        *reinterpret_cast<__attribute__((address_space(3))) u32x4 *>(lds_p(R.base - 16)) = v;
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            if (nextb < nit) {
+                const uint32_t hv2 = 16 * fc > R.a0 ? 16 * fc - R.a0 : 0;
+                B.b = nextb;
+                prepare(B, itc, nit, end, hv2, isp, O, lane);
+                nextb = B.b + B.used;
+                itc = nextb + lane < nit ? it[nextb + lane] : 0;
+                have_next = true;
+            }
+        } else {
+            // prefetched pieces: literal runs, matches sourced in HBM
+#pragma unroll
+            for (int j = 0; j < (int)kPF; j++)
+                if (A.pdst[j] != kOff)
+                    put_piece(R, A.pdst[j], A.pd[j], A.pn[j]);
+            const uint32_t mb = A.op + A.lit;
+            const uint32_t me = mb + A.ml;
+            const uint32_t msrc = mb - A.off;
+            const bool overlap = A.ml != 0 && A.off < A.ml;
+            const uint32_t need = overlap ? mb : msrc + A.ml;
+            if (A.tp > 64 * kPF) {
+                // pieces beyond the prefetch budget: copied now
+                const bool in_hbm = A.early == 1;
+                const uint32_t lp = npieces(A.lit), mp = in_hbm ? npieces(A.ml) : 0;
+                uint32_t lt, mt;
+                const uint32_t lx = excl_scan(lp, lane, &lt);
+                const uint32_t mx = excl_scan(mp, lane, &mt);
+                for (uint32_t t = 64 * kPF + lane; t - lane < lt + mt; t += 64) {
+                    const int kl = run_of(lx, t);
+                    const uint32_t tm = t - lt;
+                    const int km = run_of(mx, tm);
+                    const uint32_t nl = (uint32_t)__shfl(A.lit, kl, 64), nm = (uint32_t)__shfl(A.ml, km, 64);
+                    const uint32_t ol = piece_off(nl, t - (uint32_t)__shfl(lx, kl, 64));
+                    const uint32_t om = piece_off(nm, tm - (uint32_t)__shfl(mx, km, 64));
+                    const uint32_t sl = (uint32_t)__shfl(A.src, kl, 64) + ol, dl = (uint32_t)__shfl(A.op, kl, 64) + ol;
+                    const uint32_t sm = (uint32_t)__shfl(msrc, km, 64) + om, dm = (uint32_t)__shfl(mb, km, 64) + om;
+                    if (t < lt) {
+                        const u32x4 v = load16u(isp.r, isp.s0 + sl);
+                        put_piece(R, dl, v, nl < 16 ? nl : 16);
+                    } else if (t < lt + mt) {
+                        const u32x4 v = load16u(O.sp.r, O.sp.s0 + sm);
+                        put_piece(R, dm, v, nm < 16 ? nm : 16);
+                    }
+                }
+            }
+            const uint32_t flushed = 16 * fc > R.a0 ? 16 * fc - R.a0 : 0;
+            // matches with final sources still (partly) in the ring
+            stage_runs(R, O, isp, flushed, 0, 0, 0, msrc, mb, A.early == 2 ? A.ml : 0, lane);
+            // the rest: multi-round resolution inside the ring
+            uint64_t pending = __ballot(A.ml != 0 && A.early == 0);
+            while (pending) {
+                const uint64_t below = pending & ((1ull << lane) - 1);
+                const int hb = below ? 63 - __builtin_clzll(below) : (int)lane;
+                const uint32_t me_hb = (uint32_t)__shfl(me, hb, 64);
+                const uint32_t frontier = uni_lane(mb, __builtin_ctzll(pending));
+                const bool mine = (pending >> lane) & 1;
+                const bool ready = mine && (below == 0 || need <= frontier || msrc >= me_hb);
+                if (ready && overlap)
+                    stage_overlap(R, O, flushed, mb, A.off, A.ml);
+                stage_runs(R, O, isp, flushed, 0, 0, 0, msrc, mb, ready && !overlap ? A.ml : 0, lane);
+                pending &= ~__ballot(ready);
+            }
+            const bool last = A.b + A.used >= nit;
+            const uint32_t end_c = last ? (A.be + R.a0 + 15) >> 4 : (A.be + R.a0) >> 4;
+            flush_range(R, O, fc, end_c, lane);
+            fc = end_c;
+        }
+        if (!have_next)
+            break;
+        A = B;
+    }
+}
+
 }   // namespace
 
 int launch_lz4_exec_stage(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                           uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
-                          const uint32_t *nitems, const int32_t *d_status, hipStream_t stream)
+                          const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
+                          int version)
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL(lz4_stage_kernel, dim3((nframes + kSW - 1) / kSW), dim3(64 * kSW), 0, stream,
-                       d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status);
+    if (version == 2)
+        hipLaunchKernelGGL(lz4_stage2_kernel, dim3((nframes + kSW - 1) / kSW), dim3(64 * kSW), 0,
+                           stream, d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status);
+    else
+        hipLaunchKernelGGL(lz4_stage_kernel, dim3((nframes + kSW - 1) / kSW), dim3(64 * kSW), 0,
+                           stream, d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

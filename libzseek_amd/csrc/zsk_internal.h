@@ -100,7 +100,8 @@ int lz4_pick_engine(uint32_t nframes);   // never ENGINE_AUTO
 // decoder's items.
 int launch_lz4_exec_stage(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                           uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
-                          const uint32_t *nitems, const int32_t *d_status, hipStream_t stream);
+                          const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
+                          int version = 1);
 
 // Lane-per-frame decoder (lz4_lane.hip) + hand-offs to the wave kernel.
 int launch_lz4_lane(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
