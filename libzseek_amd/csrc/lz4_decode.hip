@@ -644,6 +644,10 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 33: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 36: return launch_lz4_split_stages(15, 0x201, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 35: return launch_lz4_split_stages(15, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 37: return launch_lz4_split_stages(15, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 39: return launch_lz4_split_stages(15, 0x603, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 60: return launch_lz4_split_stages(2, 0x400, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 38: return launch_lz4_split_stages(7, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0x200, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 40: return launch_lz4_split_stages(7, 1, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 41: return launch_lz4_split_stages(7, 2, d_desc, nframes, d_comp, d_out, d_status, stream);

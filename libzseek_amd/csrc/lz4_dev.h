@@ -105,6 +105,39 @@ __device__ __forceinline__ void store_exact(uint8_t *p, u32x4 v, uint32_t n)
         p[0] = (uint8_t)v.x;
 }
 
+// ---- DPP lane exchange (no LDS, a few cycles each; pinned by
+// scripts/microtests/dpp_scan.hip and dpp_shift.hip)
+
+// lane i receives lane i+1's x (lane 63 receives `fill`)
+__device__ __forceinline__ uint32_t dpp_next(uint32_t x, uint32_t fill)
+{
+    return __builtin_amdgcn_update_dpp(fill, x, 0x130, 0xf, 0xf, false);   // wave_shl:1
+}
+
+// lane i receives lane i-1's x (lane 0 receives `fill`)
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t x, uint32_t fill)
+{
+    return __builtin_amdgcn_update_dpp(fill, x, 0x138, 0xf, 0xf, false);   // wave_shr:1
+}
+
+// inclusive prefix sum over the wave: row shifts, then row broadcasts
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v)
+{
+    uint32_t x = v;
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
+}
+
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v)
 {
     for (int m = 32; m >= 1; m >>= 1) {

@@ -1,0 +1,407 @@
+// seq_exec.hip — sequence execution for the two-phase decoders (gfx950).
+//
+// Input: per-sequence items (lz4_parse_kernel, lz4_split.hip) = literal run
+// (source offset + length) followed by a match (offset, length).  One wave
+// executes one frame, 64 sequences (one per lane) per batch; the batch's
+// output is assembled in a small per-wave *linear* LDS stage and leaves it as
+// aligned 16-byte chunks, consecutive lanes -> consecutive chunks, so HBM
+// sees only full coalesced writes of exactly the output bytes.
+//
+// Versus lz4_stage.hip (v1/v2) this engine is built for occupancy and short
+// dependency chains:
+//   * 4 KiB stage per wave (no ring, no mirror pads): ~8 waves per SIMD;
+//   * prefix sums and neighbour exchange on DPP (row_shr / row_bcast /
+//     wave_shl), not ds_bpermute chains;
+//   * each lane copies its own runs, 16-byte pieces, two pieces of each run
+//     per step with every load issued before any write (no piece->run
+//     search);
+//   * loads that a lane does not need are disabled by an out-of-range buffer
+//     offset instead of a branch, so the compiler can keep them in flight
+//     together.
+//
+// Stage layout: stage index i holds frame output byte x = i + 16*cb - a0,
+// a0 = output address & 15, so stage chunk k (16 bytes at 16k) is output
+// chunk cb + k, 16-byte aligned in HBM.  The stage always holds chunk fc - 1
+// (flushed, kept for sources in [flushed - 16, flushed)) and the partial
+// chunk fc onward; after a batch, those two chunks move to index 0.
+//
+// Semantics follow LZ4_decompress_safe (liblz4 1.9.3) sequence execution as
+// used by the reference reader (decompress.c:631,653,762); validation already
+// happened in the parse phase, which only hands frames with status ST_OK here.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lz4_dev.h"
+#include "zsk_internal.h"
+
+namespace zsk {
+
+namespace {
+
+using namespace lz4d;
+
+constexpr uint32_t kItemExt = 0x80000000u;
+constexpr uint32_t kItemPos = 0x3FFFFFFFu;
+constexpr uint32_t kXW = 4;                 // waves (frames) per workgroup
+constexpr uint32_t kXOut = 4096;            // output bytes staged per batch at most
+constexpr uint32_t kXBuf = kXOut + 80;      // stage bytes per wave (2 kept chunks + read slack)
+constexpr uint32_t kBad = 0x80000000u;      // buffer offset past any range: load returns 0
+
+typedef u32x4 u32x4_l __attribute__((aligned(1)));
+typedef uint64_t u64_l __attribute__((aligned(1)));
+typedef uint32_t u32_l __attribute__((aligned(1)));
+typedef uint16_t u16_l __attribute__((aligned(1)));
+
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T *lp(uint32_t a)
+{
+    return (__attribute__((address_space(3))) T *)(uintptr_t)a;
+}
+
+struct Stage {
+    uint32_t base;   // LDS address of stage index 0
+    uint32_t a0;     // output address & 15
+    uint32_t cb;     // output chunk at stage index 0 (int32 -1 at frame start)
+};
+
+// LDS address of frame output byte x
+__device__ __forceinline__ uint32_t saddr(const Stage &S, uint32_t x)
+{
+    return S.base + x + S.a0 - 16u * S.cb;
+}
+
+__device__ __forceinline__ u32x4 lds16(uint32_t a)
+{
+    return *lp<u32x4_l>(a);
+}
+
+// the first n (1..16) bytes of v at LDS address a, nothing beyond
+__device__ __forceinline__ void lds_put(uint32_t a, u32x4 v, uint32_t n)
+{
+    if (n >= 16) {
+        *lp<u32x4_l>(a) = v;
+        return;
+    }
+    if (n & 8) {
+        *lp<u64_l>(a) = ((uint64_t)v.y << 32) | v.x;
+        a += 8;
+        v.x = v.z;
+        v.y = v.w;
+    }
+    if (n & 4) {
+        *lp<u32_l>(a) = v.x;
+        a += 4;
+        v.x = v.y;
+    }
+    if (n & 2) {
+        *lp<u16_l>(a) = (uint16_t)v.x;
+        a += 2;
+        v.x >>= 16;
+    }
+    if (n & 1)
+        *lp<uint8_t>(a) = (uint8_t)v.x;
+}
+
+// A run of n bytes is covered by ceil(n/16) pieces: piece i is
+// [min(16 i, n - 16), +16) when n >= 16 (overlapping pieces rewrite equal
+// bytes), else the single piece [0, n).
+__device__ __forceinline__ uint32_t npieces(uint32_t n)
+{
+    return (n + 15) >> 4;
+}
+
+__device__ __forceinline__ uint32_t piece_off(uint32_t n, uint32_t i)
+{
+    return n < 16 ? 0 : (16 * i < n - 16 ? 16 * i : n - 16);
+}
+
+struct Out {
+    uint8_t *o;      // frame output byte 0
+    uint32_t dlen;
+    Span sp;         // range-checked reads of the frame output
+};
+
+// 16 output bytes at frame offset s for a match piece: HBM below `flushed`
+// (issued as a disabled load otherwise), else the stage
+__device__ __forceinline__ u32x4 src16(const Stage &S, const Out &O, uint32_t flushed, uint32_t s,
+                                       bool on)
+{
+    const bool h = s + 16 <= flushed;
+    const u32x4 vh = load16u(O.sp.r, on && h ? O.sp.s0 + s : kBad);
+    const u32x4 vl = lds16(on && !h ? saddr(S, s) : S.base);
+    return h ? vh : vl;
+}
+
+// Copy this lane's literal run (lit bytes of the literal source at src ->
+// output op) and a match run (mn bytes from output msrc -> mb; final source,
+// no overlap) into the stage: pieces j, j+1 of both runs per step, all four
+// loads issued before the writes.
+__device__ __forceinline__ void copy_own(const Stage &S, const Out &O, const Span &lsp,
+                                         uint32_t flushed, uint32_t src, uint32_t op,
+                                         uint32_t lit, uint32_t msrc, uint32_t mb, uint32_t mn)
+{
+    const uint32_t lpn = npieces(lit), mpn = npieces(mn);
+    const uint32_t ln = lit < 16 ? lit : 16, mnn = mn < 16 ? mn : 16;
+    for (uint32_t j = 0; __ballot(j < lpn || j < mpn); j += 2) {
+        const bool l0 = j < lpn, l1 = j + 1 < lpn, m0 = j < mpn, m1 = j + 1 < mpn;
+        const uint32_t ol0 = piece_off(lit, j), ol1 = piece_off(lit, j + 1);
+        const uint32_t om0 = piece_off(mn, j), om1 = piece_off(mn, j + 1);
+        const u32x4 vl0 = load16u(lsp.r, l0 ? lsp.s0 + src + ol0 : kBad);
+        const u32x4 vl1 = load16u(lsp.r, l1 ? lsp.s0 + src + ol1 : kBad);
+        const u32x4 vm0 = src16(S, O, flushed, msrc + om0, m0);
+        const u32x4 vm1 = src16(S, O, flushed, msrc + om1, m1);
+        if (l0)
+            lds_put(saddr(S, op + ol0), vl0, ln);
+        if (l1)
+            lds_put(saddr(S, op + ol1), vl1, 16);
+        if (m0)
+            lds_put(saddr(S, mb + om0), vm0, mnn);
+        if (m1)
+            lds_put(saddr(S, mb + om1), vm1, 16);
+    }
+}
+
+// Overlapping match (off < n), this lane alone: out[x] = out[x - off], 16
+// bytes at a time from distance eoff >= 16 (a multiple of off).
+__device__ __forceinline__ void copy_overlap(const Stage &S, const Out &O, uint32_t flushed,
+                                             uint32_t dst, uint32_t off, uint32_t n)
+{
+    uint32_t k = 0, eoff = off;
+    if (off < 16) {
+        const u32x4 pat = src16(S, O, flushed, dst - off, true);
+        uint32_t w[4] = {0, 0, 0, 0};
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            w[i >> 2] |= vbyte(pat, m) << (8 * (i & 3));
+            m = m + 1 == off ? 0 : m + 1;
+        }
+        lds_put(saddr(S, dst), (u32x4){w[0], w[1], w[2], w[3]}, n < 16 ? n : 16);
+        k = 16;
+        eoff = off * ((16 + off - 1) / off);
+    }
+    for (; k < n; k += 16) {
+        const u32x4 v = src16(S, O, flushed, dst + k - eoff, true);
+        const uint32_t r = n - k;
+        lds_put(saddr(S, dst + k), v, r < 16 ? r : 16);
+    }
+}
+
+// stage chunk k (output chunk cb + k) -> HBM; exact at the frame's edges
+__device__ __forceinline__ void flush_chunk(const Stage &S, const Out &O, uint32_t c)
+{
+    const u32x4 v = *lp<u32x4>(S.base + 16u * (c - S.cb));
+    const int64_t x0 = (int64_t)16 * c - S.a0;
+    if (x0 >= 0 && x0 + 16 <= O.dlen) {
+        *reinterpret_cast<u32x4 *>(O.o + x0) = v;
+    } else {
+        for (int k = 0; k < 16; k++) {
+            const int64_t x = x0 + k;
+            if (x >= 0 && x < O.dlen)
+                O.o[x] = (uint8_t)vbyte(v, k);
+        }
+    }
+}
+
+// whole-wave copy in HBM for sequences too long to stage (source and
+// destination do not overlap within one 1 KiB step)
+__device__ __forceinline__ void hbm_run(const Span &s, uint32_t src, uint8_t *dst, uint32_t n,
+                                        uint32_t lane)
+{
+    for (uint32_t k = 16 * lane; k < n; k += 1024) {
+        const u32x4 v = load16u(s.r, s.s0 + src + k);
+        store_exact(dst + k, v, n - k < 16 ? n - k : 16);
+    }
+}
+
+__device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t off, uint32_t n,
+                                          uint32_t lane)
+{
+    uint32_t done = 0;
+    while (done < n) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint32_t e = off * ((done + off) / off);   // a multiple of off, <= done + off
+        uint32_t step = e < 1024 ? e : 1024;
+        if (step > n - done)
+            step = n - done;
+        if (e < 16) {
+            if (lane == 0)
+                for (uint32_t k = 0; k < step; k++)
+                    O.o[dst + done + k] = O.o[dst + done + k - e];
+        } else {
+            for (uint32_t k = 16 * lane; k < step; k += 1024) {
+                const uint32_t x = dst + done + k;
+                const u32x4 v = load16u(O.sp.r, O.sp.s0 + x - e);
+                const uint32_t r = step - k;
+                store_exact(O.o + x, v, r < 16 ? r : 16);
+            }
+        }
+        done += step;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+}
+
+__global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
+    uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
+    const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
+    const int32_t *__restrict__ status)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * kXBuf];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t f = uni(blockIdx.x * kXW + w);
+    if (f >= n)
+        return;
+    if (uni((uint32_t)status[f]) != (uint32_t)ST_OK)
+        return;
+    const FrameDesc d = desc[f];
+    const uint32_t nit = uni(nitems[f]);
+    const uint64_t *it = items + rec_base[f];
+    Out O;
+    O.o = out + d.d_off;
+    O.dlen = d.d_size;
+    O.sp = make_span(O.o, d.d_size);
+    const Span lsp = make_span(comp + d.c_off, d.c_size);   // literal source: the compressed frame
+    Stage S;
+    S.base = (uint32_t)(uintptr_t)(lds + w * kXBuf);
+    S.a0 = (uint32_t)(reinterpret_cast<uintptr_t>(O.o) & 15);
+    S.cb = 0xFFFFFFFFu;      // chunk -1 at index 0: chunk 0 starts at index 16
+    uint32_t produced = 0;   // frame bytes decoded
+    uint32_t fc = 0;         // output chunks [0, fc) are in HBM
+    uint64_t cur = lane < nit ? it[lane] : 0;
+    uint32_t b = 0;
+    while (b < nit) {
+        const uint64_t nxt = b + 64 + lane < nit ? it[b + 64 + lane] : 0;
+        const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
+        const uint32_t w0n = dpp_next(w0, 0), w1n = dpp_next(w1, 0);
+        const uint32_t w0p = dpp_prev(w0, 0);
+        const bool act0 = b + lane < nit;
+        const uint32_t src = w0 & kItemPos;
+        const uint32_t off = w1 & 0xFFFF;
+        uint32_t lit = 0, ml = 0;
+        if (act0 && !(w0p & kItemExt)) {
+            if (w0 & kItemExt) {
+                lit = w0n;
+                ml = w1n;
+            } else {
+                lit = (w1 >> 16) & 0xFF;
+                const uint32_t mc = w1 >> 24;
+                ml = mc ? mc + 3 : 0;
+            }
+        }
+        // batch = the lanes before the first whose output would pass kXOut;
+        // an extended item keeps its second half
+        const uint32_t len = lit + ml;
+        const uint32_t inc = wave_incl_add(len);
+        const uint64_t over = __ballot(act0 && inc > kXOut);
+        uint32_t nb = over ? (uint32_t)__builtin_ctzll(over) : 64;
+        if (nb == 64 && (lane_val(w0, 63) & kItemExt))
+            nb = 63;
+        else if (nb > 0 && nb < 64 && (lane_val(w0, (int)nb - 1) & kItemExt))
+            nb++;
+        if (b + nb > nit)
+            nb = nit - b;
+        const uint32_t flushed = 16 * fc > S.a0 ? 16 * fc - S.a0 : 0;   // frame bytes < this are in HBM
+        if (nb == 0) {
+            // lane 0 alone is too long to stage: flush, copy in HBM, reload
+            const uint32_t l0 = lane_val(lit, 0), m0 = lane_val(ml, 0);
+            const uint32_t s0 = lane_val(src, 0), o0 = lane_val(off, 0);
+            const uint32_t end_c = (produced + S.a0 + 15) >> 4;
+            for (uint32_t c = fc + lane; c < end_c; c += 64)
+                flush_chunk(S, O, c);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (l0)
+                hbm_run(lsp, s0, O.o + produced, l0, lane);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (m0) {
+                const uint32_t mb = produced + l0;
+                if (o0 >= m0)
+                    hbm_run(O.sp, mb - o0, O.o + mb, m0, lane);
+                else
+                    hbm_match(O, mb, o0, m0, lane);
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            produced += l0 + m0;
+            fc = (produced + S.a0) >> 4;
+            S.cb = fc - 1;
+            if (lane < 2) {
+                const uint32_t c = fc - 1 + lane;   // chunks fc-1, fc back from HBM
+                const int64_t x0 = (int64_t)16 * c - S.a0;
+                if ((fc > 0 || lane == 1) && x0 >= 0)
+                    *lp<u32x4>(S.base + 16 * lane) =
+                        load16u(O.sp.r, (uint32_t)((int64_t)O.sp.s0 + x0));
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint32_t used = lane_val(w0, 0) & kItemExt ? 2 : 1;
+            b += used;
+            const uint64_t a = __shfl_down(cur, used, 64);
+            const uint64_t c2 = __shfl(nxt, (int)((lane + used) & 63), 64);
+            cur = lane + used < 64 ? a : c2;
+            continue;
+        }
+        if (lane >= nb) {
+            lit = 0;
+            ml = 0;
+        }
+        const uint32_t bstart = produced;
+        const uint32_t op = produced + inc - len;
+        const uint32_t mb = op + lit;
+        const uint32_t me = mb + ml;
+        const uint32_t msrc = mb - off;
+        const bool overlap = ml != 0 && off < ml;
+        const uint32_t need = overlap ? mb : msrc + ml;   // end of the bytes the copy reads
+        const bool early = ml != 0 && !overlap && need <= bstart;
+        produced += lane_val(inc, (int)nb - 1);
+        // round 0: literal runs + matches whose source precedes the batch
+        copy_own(S, O, lsp, flushed, src, op, lit, msrc, mb, early ? ml : 0);
+        // rounds: matches reading bytes of this batch
+        uint64_t pending = __ballot(ml != 0 && !early);
+        while (pending) {
+            const uint64_t below = pending & ((1ull << lane) - 1);
+            const int hb = below ? 63 - __builtin_clzll(below) : (int)lane;
+            const uint32_t me_hb = (uint32_t)__shfl(me, hb, 64);
+            const uint32_t frontier = lane_val(mb, __builtin_ctzll(pending));
+            const bool mine = (pending >> lane) & 1;
+            const bool ready = mine && (below == 0 || need <= frontier || msrc >= me_hb);
+            if (ready && overlap)
+                copy_overlap(S, O, flushed, mb, off, ml);
+            copy_own(S, O, lsp, flushed, 0, 0, 0, msrc, mb, ready && !overlap ? ml : 0);
+            pending &= ~__ballot(ready);
+        }
+        // flush complete chunks (the frame's last chunk exactly)
+        const bool last = b + nb >= nit;
+        const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
+        for (uint32_t c = fc + lane; c < end_c; c += 64)
+            flush_chunk(S, O, c);
+        fc = end_c;
+        // keep chunks fc-1 (flushed) and fc (partial) at stage index 0
+        if (!last && fc - 1 != S.cb) {
+            u32x4 v;
+            if (lane < 2)
+                v = *lp<u32x4>(S.base + 16u * (fc - 1 + lane - S.cb));
+            if (lane < 2)
+                *lp<u32x4>(S.base + 16 * lane) = v;
+            S.cb = fc - 1;
+        }
+        b += nb;
+        const uint64_t a = __shfl_down(cur, nb & 63, 64);
+        const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
+        cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
+    }
+}
+
+}   // namespace
+
+int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                    uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
+                    const uint32_t *nitems, const int32_t *d_status, hipStream_t stream)
+{
+    if (nframes == 0)
+        return 0;
+    hipLaunchKernelGGL(seq_exec_kernel, dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0, stream,
+                       d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}   // namespace zsk

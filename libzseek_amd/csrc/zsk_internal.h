@@ -103,6 +103,18 @@ int launch_lz4_exec_stage(const FrameDesc *d_desc, uint32_t nframes, const uint8
                           const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
                           int version = 1);
 
+// Execute phase v3 (seq_exec.hip): linear per-wave LDS stage, DPP scans,
+// lane-owned piece copies.
+int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                    uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
+                    const uint32_t *nitems, const int32_t *d_status, hipStream_t stream);
+
+// Parse phase, streaming lane-per-frame (lz4_scan.hip): same outputs as
+// lz4_parse_kernel.
+int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                    const uint64_t *rec_base, uint64_t capacity, uint64_t *items,
+                    uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream);
+
 // Lane-per-frame decoder (lz4_lane.hip) + hand-offs to the wave kernel.
 int launch_lz4_lane(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,

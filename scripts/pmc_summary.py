@@ -12,7 +12,7 @@ names = {}
 for f in glob.glob(os.path.join(root, "p*", "*", "*_counter_collection.csv")):
     for row in csv.DictReader(open(f)):
         name = row["Kernel_Name"]
-        if "lz4" not in name:
+        if "lz4" not in name and "seq_" not in name and "zstd" not in name:
             continue
         # dispatches of one kernel in the same position across passes line up
         key = (name, os.path.basename(os.path.dirname(os.path.dirname(f))), row["Dispatch_Id"])
