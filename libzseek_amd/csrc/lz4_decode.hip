@@ -646,6 +646,14 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 35: return launch_lz4_split_stages(15, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 37: return launch_lz4_split_stages(15, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 39: return launch_lz4_split_stages(15, 0x603, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 61: return launch_lz4_split_stages(15, 0x604, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 62: return launch_lz4_split_stages(7, 0x604, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 63: return launch_lz4_split_stages(4, 0x205, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 64: return launch_lz4_split_stages(4, 0x206, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 65: return launch_lz4_split_stages(4, 0x207, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 66: return launch_lz4_split_stages(4, 0x204, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 68: return launch_lz4_split_stages(4, 0x208, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 67: return launch_lz4_split_stages(4, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 60: return launch_lz4_split_stages(2, 0x400, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 38: return launch_lz4_split_stages(7, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0x200, d_desc, nframes, d_comp, d_out, d_status, stream);

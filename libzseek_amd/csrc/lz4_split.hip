@@ -749,9 +749,9 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         hipLaunchKernelGGL(lz4_parse_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                            s->nitems, d_status, d_fail_at);
-    if ((stages & 4) && diag == 0x203) {
+    if ((stages & 4) && diag >= 0x203 && diag <= 0x208) {
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                        stream);
+                        stream, diag & 0xF);
     } else if ((stages & 4) && (diag == 0x200 || diag == 0x201)) {
         launch_lz4_exec_stage(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems,
                               d_status, stream, diag == 0x201 ? 2 : 1);

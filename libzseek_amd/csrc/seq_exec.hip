@@ -30,6 +30,7 @@
 // happened in the parse phase, which only hands frames with status ST_OK here.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "lz4_dev.h"
 #include "zsk_internal.h"
@@ -45,6 +46,8 @@ constexpr uint32_t kItemPos = 0x3FFFFFFFu;
 constexpr uint32_t kXW = 4;                 // waves (frames) per workgroup
 constexpr uint32_t kXOut = 4096;            // output bytes staged per batch at most
 constexpr uint32_t kXBuf = kXOut + 80;      // stage bytes per wave (2 kept chunks + read slack)
+constexpr uint32_t kXPieces = kXOut / 16 + 2 * 64;   // pieces of a batch at most
+constexpr uint32_t kXWave = kXBuf + 8 * kXPieces;    // stage + piece descriptors
 constexpr uint32_t kBad = 0x80000000u;      // buffer offset past any range: load returns 0
 
 typedef u32x4 u32x4_l __attribute__((aligned(1)));
@@ -161,6 +164,108 @@ __device__ __forceinline__ void copy_own(const Stage &S, const Out &O, const Spa
     }
 }
 
+// 16 bytes at byte offset x of a resource: one unaligned load.  Safe for the
+// LZ4 sources because the hardware range-checks per dword and every byte a
+// piece needs lies at least 4 bytes before its span's end (literal runs are
+// followed by a block header / end mark; a match source ends before its
+// destination, which ends at most at the frame end).
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t x)
+{
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, x, 0, 0));
+}
+
+enum : uint32_t { K_LIT = 0, K_HBM = 1, K_STAGE = 2 };
+
+__device__ unsigned long long g_xstats[12];   // DIAG 16: cycles per section, counts
+
+// Copy, for every lane, a literal run (lit bytes of the literal source at src
+// -> output op) and a match run (mn bytes from output msrc -> mb; final
+// source, no overlap) into the stage.  Each lane first writes one 8-byte
+// descriptor per 16-byte piece (source, stage destination, length, kind) at
+// its piece-prefix position in LDS; then the wave's pieces are dealt one per
+// lane per slot, four slots' loads in flight before any write.
+template <int DIAG>
+__device__ __forceinline__ void copy_desc(const Stage &S, const Out &O, const Span &lsp,
+                                          uint32_t descs, uint32_t flushed, uint32_t lane,
+                                          uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
+                                          uint32_t mb, uint32_t mn)
+{
+    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
+    const uint32_t inc = wave_incl_add(np);
+    const uint32_t T = lane_val(inc, 63);
+    if (T == 0)
+        return;
+    const uint32_t x = inc - np;
+    for (uint32_t i = 0; __ballot(i < np); i++) {
+        if (i < np) {
+            const bool isl = i < lpn;
+            const uint32_t n = isl ? lit : mn;
+            const uint32_t o = piece_off(n, isl ? i : i - lpn);
+            const uint32_t sx = (isl ? src : msrc) + o;
+            const uint32_t kind = isl ? K_LIT : (sx + 16 <= flushed ? K_HBM : K_STAGE);
+            const uint32_t da = saddr(S, (isl ? op : mb) + o) - S.base;   // < 8 KiB
+            *lp<uint64_t>(descs + 8 * (x + i)) =
+                ((uint64_t)(da | (n < 16 ? n : 16) << 16 | kind << 24) << 32) | sx;
+        }
+    }
+    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
+        u32x4 vl[4], vm[4];
+        uint32_t dw[4], sx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t t = t0 + 64 * j + lane;
+            const bool on = t < T;
+            const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
+            sx[j] = (uint32_t)D;
+            dw[j] = on ? (uint32_t)(D >> 32) : 0;
+            const uint32_t kind = dw[j] >> 24;
+            vl[j] = bload16(lsp.r, on && kind == K_LIT && !(DIAG & 1) ? lsp.s0 + sx[j] : kBad);
+            vm[j] = bload16(O.sp.r, on && kind == K_HBM && !(DIAG & 1) ? O.sp.s0 + sx[j] : kBad);
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t n = (dw[j] >> 16) & 0xFF;
+            if (n) {
+                u32x4 v = vl[j] | vm[j];   // the disabled load returned zeros
+                if ((dw[j] >> 24) == K_STAGE)
+                    v = lds16(saddr(S, sx[j]));
+                lds_put(S.base + (dw[j] & 0xFFFF), v, n);
+            }
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+    }
+}
+
+// A ready match (mn bytes, msrc -> mb, no overlap) whose source lies in this
+// batch: lane-owned pieces, two per step, from the stage (the HBM path only
+// runs when some lane's piece lies below `flushed`).
+__device__ __forceinline__ void copy_round(const Stage &S, const Out &O, uint32_t flushed,
+                                           uint32_t msrc, uint32_t mb, uint32_t mn)
+{
+    const uint32_t mpn = npieces(mn), n0 = mn < 16 ? mn : 16;
+    for (uint32_t j = 0; __ballot(j < mpn); j += 2) {
+        const bool m0 = j < mpn, m1 = j + 1 < mpn;
+        const uint32_t o0 = piece_off(mn, j), o1 = piece_off(mn, j + 1);
+        const uint32_t s0 = msrc + o0, s1 = msrc + o1;
+        const bool h0 = m0 && s0 + 16 <= flushed, h1 = m1 && s1 + 16 <= flushed;
+        u32x4 v0 = lds16(m0 && !h0 ? saddr(S, s0) : S.base);
+        u32x4 v1 = lds16(m1 && !h1 ? saddr(S, s1) : S.base);
+        if (__ballot(h0 || h1)) {
+            const u32x4 w0 = bload16(O.sp.r, h0 ? O.sp.s0 + s0 : kBad);
+            const u32x4 w1 = bload16(O.sp.r, h1 ? O.sp.s0 + s1 : kBad);
+            v0 = h0 ? w0 : v0;
+            v1 = h1 ? w1 : v1;
+        }
+        if (m0)
+            lds_put(saddr(S, mb + o0), v0, n0);
+        if (m1)
+            lds_put(saddr(S, mb + o1), v1, 16);
+    }
+}
+
 // Overlapping match (off < n), this lane alone: out[x] = out[x - off], 16
 // bytes at a time from distance eoff >= 16 (a multiple of off).
 __device__ __forceinline__ void copy_overlap(const Stage &S, const Out &O, uint32_t flushed,
@@ -241,13 +346,15 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
     __builtin_amdgcn_s_waitcnt(0);
 }
 
+// DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores
+template <bool DIST, int DIAG>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     const int32_t *__restrict__ status)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * kXBuf];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * kXWave];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t f = uni(blockIdx.x * kXW + w);
@@ -264,13 +371,24 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     O.sp = make_span(O.o, d.d_size);
     const Span lsp = make_span(comp + d.c_off, d.c_size);   // literal source: the compressed frame
     Stage S;
-    S.base = (uint32_t)(uintptr_t)(lds + w * kXBuf);
+    S.base = (uint32_t)(uintptr_t)(lds + w * kXWave);
+    const uint32_t descs = S.base + kXBuf;
     S.a0 = (uint32_t)(reinterpret_cast<uintptr_t>(O.o) & 15);
     S.cb = 0xFFFFFFFFu;      // chunk -1 at index 0: chunk 0 starts at index 16
     uint32_t produced = 0;   // frame bytes decoded
     uint32_t fc = 0;         // output chunks [0, fc) are in HBM
     uint64_t cur = lane < nit ? it[lane] : 0;
     uint32_t b = 0;
+    uint64_t tsec[4] = {0, 0, 0, 0};
+    uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tmark = (DIAG & 16) ? __builtin_readcyclecounter() : 0;
+#define ZSK_T(i)                                                      \
+    if (DIAG & 16) {                                                  \
+        __builtin_amdgcn_s_waitcnt(0);                                \
+        const uint64_t tn = __builtin_readcyclecounter();             \
+        tsec[i] += tn - tmark;                                        \
+        tmark = tn;                                                   \
+    }
     while (b < nit) {
         const uint64_t nxt = b + 64 + lane < nit ? it[b + 64 + lane] : 0;
         const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
@@ -353,27 +471,61 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         const uint32_t need = overlap ? mb : msrc + ml;   // end of the bytes the copy reads
         const bool early = ml != 0 && !overlap && need <= bstart;
         produced += lane_val(inc, (int)nb - 1);
+        ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        copy_own(S, O, lsp, flushed, src, op, lit, msrc, mb, early ? ml : 0);
+        if (DIST)
+            copy_desc<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
+        else
+            copy_own(S, O, lsp, flushed, src, op, lit, msrc, mb, early ? ml : 0);
+        ZSK_T(1)
         // rounds: matches reading bytes of this batch
         uint64_t pending = __ballot(ml != 0 && !early);
+        if (DIAG & 16) {
+            tsec[4 - 4] += 0;
+            cnt[0] += 1;
+            cnt[1] += __builtin_popcountll(pending);
+            cnt[2] += __builtin_popcountll(__ballot(ml != 0 && !early && msrc < bstart));
+            cnt[3] += __builtin_popcountll(__ballot(overlap));
+            cnt[4] += nb;
+        }
         while (pending) {
-            const uint64_t below = pending & ((1ull << lane) - 1);
-            const int hb = below ? 63 - __builtin_clzll(below) : (int)lane;
-            const uint32_t me_hb = (uint32_t)__shfl(me, hb, 64);
-            const uint32_t frontier = lane_val(mb, __builtin_ctzll(pending));
             const bool mine = (pending >> lane) & 1;
-            const bool ready = mine && (below == 0 || need <= frontier || msrc >= me_hb);
+            bool ready;
+            if (DIST) {
+                // blocked while the source meets a lower pending match's destination
+                bool blocked = false;
+                uint64_t pj = pending;
+                while (pj) {
+                    const int j = __builtin_ctzll(pj);
+                    pj &= pj - 1;
+                    const uint32_t mbj = lane_val(mb, j), mej = lane_val(me, j);
+                    blocked = blocked || ((uint32_t)j < lane && mbj < need && mej > msrc);
+                }
+                ready = mine && !blocked;
+            } else {
+                const uint64_t below = pending & ((1ull << lane) - 1);
+                const int hb = below ? 63 - __builtin_clzll(below) : (int)lane;
+                const uint32_t me_hb = (uint32_t)__shfl(me, hb, 64);
+                const uint32_t frontier = lane_val(mb, __builtin_ctzll(pending));
+                ready = mine && (below == 0 || need <= frontier || msrc >= me_hb);
+            }
             if (ready && overlap)
                 copy_overlap(S, O, flushed, mb, off, ml);
-            copy_own(S, O, lsp, flushed, 0, 0, 0, msrc, mb, ready && !overlap ? ml : 0);
+            if (DIST)
+                copy_round(S, O, flushed, msrc, mb, ready && !overlap ? ml : 0);
+            else
+                copy_own(S, O, lsp, flushed, 0, 0, 0, msrc, mb, ready && !overlap ? ml : 0);
             pending &= ~__ballot(ready);
+            if (DIAG & 16)
+                cnt[5] += 1;
         }
+        ZSK_T(2)
         // flush complete chunks (the frame's last chunk exactly)
         const bool last = b + nb >= nit;
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
-        for (uint32_t c = fc + lane; c < end_c; c += 64)
-            flush_chunk(S, O, c);
+        if (!(DIAG & 2))
+            for (uint32_t c = fc + lane; c < end_c; c += 64)
+                flush_chunk(S, O, c);
         fc = end_c;
         // keep chunks fc-1 (flushed) and fc (partial) at stage index 0
         if (!last && fc - 1 != S.cb) {
@@ -388,19 +540,52 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         const uint64_t a = __shfl_down(cur, nb & 63, 64);
         const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
         cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
+        ZSK_T(3)
     }
+#undef ZSK_T
+    if ((DIAG & 16) && lane == 0)
+        for (int i = 0; i < 4; i++)
+            atomicAdd(&g_xstats[i], (unsigned long long)tsec[i]);
+    if ((DIAG & 16) && lane == 0)
+        for (int i = 0; i < 6; i++)
+            atomicAdd(&g_xstats[4 + i], (unsigned long long)cnt[i]);
 }
 
 }   // namespace
 
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
-                    const uint32_t *nitems, const int32_t *d_status, hipStream_t stream)
+                    const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
+                    int version)
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL(seq_exec_kernel, dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0, stream,
-                       d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status);
+    const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
+#define ZSK_X(D, G)                                                                            \
+    hipLaunchKernelGGL((seq_exec_kernel<D, G>), grid, block, 0, stream, d_desc, nframes, d_comp, \
+                       d_out, rec_base, items, nitems, d_status)
+    switch (version) {
+    case 3: ZSK_X(false, 0); break;
+    case 5: ZSK_X(true, 1); break;
+    case 6: ZSK_X(true, 2); break;
+    case 7: ZSK_X(true, 3); break;
+    case 8: {
+        unsigned long long z[12] = {0};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+        ZSK_X(true, 16);
+        (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_xstats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        const double t = (double)(z[0] + z[1] + z[2] + z[3]);
+        fprintf(stderr, "exec sections (wave cycles): items+scan %.1f%%  round0 %.1f%%  rounds %.1f%%  flush %.1f%%  total %.3g\n",
+                100 * z[0] / t, 100 * z[1] / t, 100 * z[2] / t, 100 * z[3] / t, t);
+        const double nb = (double)z[4];
+        fprintf(stderr, "per batch: seqs %.1f pending %.2f (src below batch %.2f) overlap %.3f rounds %.2f\n",
+                z[8] / nb, z[5] / nb, z[6] / nb, z[7] / nb, z[9] / nb);
+        break;
+    }
+    default: ZSK_X(true, 0); break;
+    }
+#undef ZSK_X
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

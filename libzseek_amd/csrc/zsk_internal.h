@@ -107,7 +107,8 @@ int launch_lz4_exec_stage(const FrameDesc *d_desc, uint32_t nframes, const uint8
 // lane-owned piece copies.
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
-                    const uint32_t *nitems, const int32_t *d_status, hipStream_t stream);
+                    const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
+                    int version = 4);
 
 // Parse phase, streaming lane-per-frame (lz4_scan.hip): same outputs as
 // lz4_parse_kernel.
