@@ -60,11 +60,21 @@ ZSEEK_EXPORT int zsk_lz4_decode_frames(const zsk_frame_desc_t *d_desc,
 /* Human-readable name of a frame status (LZ4F-style "ERROR_..." names). */
 ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
 
-/* Name of the main HIP kernel zsk_lz4_decode_frames launches for a batch of
- * nframes frames (as it appears in a rocprofv3 kernel trace, without
- * namespace), for tooling.  Large batches use the lane-per-frame decoder,
- * small ones the wave-per-frame decoder (env ZSEEK_HIP_KERNEL overrides). */
+/* Name of the dominant HIP kernel zsk_lz4_decode_frames launches for a
+ * batch of nframes frames (as it appears in a rocprofv3 kernel trace,
+ * without namespace), for tooling.  Large batches use the two-phase decoder
+ * (lz4_scan_kernel parse + seq_exec_kernel execute), small ones the
+ * wave-per-frame decoder (env ZSEEK_HIP_KERNEL=lane|split|wave overrides). */
 ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes);
+
+/* Measurement hook: while on, every two-phase decode launch records HIP
+ * events between its stages (plan, parse, execute, hand-off) on its stream.
+ * zsk_kernel_timing(on) switches it and clears the totals;
+ * zsk_kernel_times(ms, cap) waits for the recorded launches and writes the
+ * average milliseconds per stage into ms[0..min(cap,4)), returning the
+ * number of launches averaged.  Not on any decode path's critical path. */
+ZSEEK_EXPORT int zsk_kernel_timing(int on);
+ZSEEK_EXPORT int zsk_kernel_times(double *ms, int cap);
 
 /* Number of frames of an open reader and its seek table as prefix sums:
  * c_off/d_off receive n+1 entries each (either may be NULL). */

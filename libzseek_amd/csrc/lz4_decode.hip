@@ -639,30 +639,30 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 54: return launch_lz4_lane(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, 4);
     case 53: return launch_lz4_lane(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, 3);
     case 30: return launch_lz4_frames(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
-    case 31: return launch_lz4_split_stages(3, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 32: return launch_lz4_split_stages(7, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 33: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 36: return launch_lz4_split_stages(15, 0x201, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 35: return launch_lz4_split_stages(15, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 37: return launch_lz4_split_stages(15, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 31: return launch_lz4_split_stages(3, 0x800, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 32: return launch_lz4_split_stages(7, 0x1800, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 33: return launch_lz4_split_stages(2, 0x800, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 36: return launch_lz4_split_stages(15, 0xA01, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 35: return launch_lz4_split_stages(15, 0x1800, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 37: return launch_lz4_split_stages(15, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 39: return launch_lz4_split_stages(15, 0x603, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 61: return launch_lz4_split_stages(15, 0x604, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 62: return launch_lz4_split_stages(7, 0x604, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 61: return launch_lz4_split_stages(15, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 62: return launch_lz4_split_stages(7, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 63: return launch_lz4_split_stages(4, 0x205, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 64: return launch_lz4_split_stages(4, 0x206, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 65: return launch_lz4_split_stages(4, 0x207, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 66: return launch_lz4_split_stages(4, 0x204, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 68: return launch_lz4_split_stages(4, 0x208, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 67: return launch_lz4_split_stages(4, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 60: return launch_lz4_split_stages(2, 0x400, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 38: return launch_lz4_split_stages(7, 0x203, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 34: return launch_lz4_split_stages(15, 0x200, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 40: return launch_lz4_split_stages(7, 1, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 41: return launch_lz4_split_stages(7, 2, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 44: return launch_lz4_split_stages(7, 16, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 45: return launch_lz4_split_stages(7, 0x106, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 46: return launch_lz4_split_stages(7, 0x108, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 43: return launch_lz4_split_stages(7, 8, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 60: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 38: return launch_lz4_split_stages(7, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 34: return launch_lz4_split_stages(15, 0xA00, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 40: return launch_lz4_split_stages(7, 0x1801, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 41: return launch_lz4_split_stages(7, 0x1802, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 44: return launch_lz4_split_stages(7, 0x1810, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 45: return launch_lz4_split_stages(7, 0x1906, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 46: return launch_lz4_split_stages(7, 0x1908, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 43: return launch_lz4_split_stages(7, 0x1808, d_desc, nframes, d_comp, d_out, d_status, stream);
     default: return -1;
     }
 #undef ZSK_V

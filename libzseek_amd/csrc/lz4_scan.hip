@@ -533,7 +533,7 @@ __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))
     if (act) {
         d = desc[f];
         rb0 = rec_base[f];
-        cap = (d.c_size / 4 + 16 + 3) & ~3u;   // slots_of (lz4_split.hip)
+        cap = slots_of(d.c_size);
     }
     const uint64_t clo = uni64(wave_min64(act ? d.c_off : ~0ull));
     const uint64_t chi = uni64(wave_max64(act ? d.c_off + d.c_size : 0ull));

@@ -37,9 +37,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <array>
 #include <map>
 #include <mutex>
 #include <utility>
+#include <vector>
 
 #include "lz4_dev.h"
 #include "zsk_internal.h"
@@ -54,16 +56,6 @@ constexpr uint32_t kItemExt = 0x80000000u;   // item w0: next item holds the ful
 constexpr uint32_t kItemPos = 0x3FFFFFFFu;
 constexpr uint32_t kExecWaves = 4;
 constexpr uint32_t kLongCopy = 256;   // longer literal runs / matches: copied by the whole wave
-
-// Item slots of a frame.  An item is 8 bytes; a sequence takes one (>= 3
-// compressed bytes) or two (extended: >= 4 compressed bytes), a stored block
-// two.  Real LZ4 data spends ~10-25 compressed bytes per sequence; one slot
-// per 4 bytes (+16) covers all but adversarial frames, which do not fit and
-// are decoded by the wave kernel instead (parse reports ST_NOT_RUN).
-__host__ __device__ __forceinline__ uint32_t slots_of(uint32_t c_size)
-{
-    return (c_size / 4 + 16 + 3) & ~3u;
-}
 
 // Per-lane reader over one frame of the compressed image with a 16-byte
 // register window on dword-aligned coordinates.
@@ -727,6 +719,91 @@ int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipS
     return 0;
 }
 
+// ---- per-stage launch timing (zsk_kernel_timing / zsk_kernel_times) ----------
+// Events around the stages of each launch on its stream: [plan, parse,
+// execute, hand-off]; read back (and averaged) on request.
+namespace {
+struct StageTimer {
+    std::mutex mu;
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    std::vector<std::array<hipEvent_t, kTimedStages + 1>> pend;
+    double sum[kTimedStages] = {};
+    uint64_t n = 0;
+};
+StageTimer g_timer;
+thread_local std::array<hipEvent_t, kTimedStages + 1> t_ev;
+thread_local bool t_active = false;
+
+hipEvent_t timer_event()
+{
+    if (!g_timer.pool.empty()) {
+        hipEvent_t e = g_timer.pool.back();
+        g_timer.pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+}   // namespace
+
+void stage_mark(int boundary, hipStream_t stream)
+{
+    if (boundary == 0) {
+        std::lock_guard<std::mutex> g(g_timer.mu);
+        t_active = g_timer.on;
+        if (!t_active)
+            return;
+        for (auto &e : t_ev)
+            e = timer_event();
+    }
+    if (!t_active)
+        return;
+    (void)hipEventRecord(t_ev[boundary], stream);
+    if (boundary == kTimedStages) {
+        std::lock_guard<std::mutex> g(g_timer.mu);
+        g_timer.pend.push_back(t_ev);
+        t_active = false;
+    }
+}
+
+int kernel_timing(int on)
+{
+    std::lock_guard<std::mutex> g(g_timer.mu);
+    for (auto &a : g_timer.pend) {
+        (void)hipEventSynchronize(a[kTimedStages]);
+        for (auto e : a)
+            g_timer.pool.push_back(e);
+    }
+    g_timer.pend.clear();
+    g_timer.on = on != 0;
+    for (double &x : g_timer.sum)
+        x = 0;
+    g_timer.n = 0;
+    return 0;
+}
+
+int kernel_times(double *ms, int cap)
+{
+    std::lock_guard<std::mutex> g(g_timer.mu);
+    for (auto &a : g_timer.pend) {
+        (void)hipEventSynchronize(a[kTimedStages]);
+        for (int i = 0; i < kTimedStages; i++) {
+            float t = 0;
+            if (hipEventElapsedTime(&t, a[i], a[i + 1]) == hipSuccess)
+                g_timer.sum[i] += t;
+        }
+        g_timer.n++;
+        for (auto e : a)
+            g_timer.pool.push_back(e);
+    }
+    g_timer.pend.clear();
+    for (int i = 0; i < cap && i < kTimedStages; i++)
+        ms[i] = g_timer.n ? g_timer.sum[i] / g_timer.n : 0.0;
+    return (int)g_timer.n;
+}
+
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                      hipStream_t stream, SplitScratch *s, int stages, int diag)
@@ -737,30 +814,40 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         return -1;
     uint64_t *total_dev = nullptr;
     (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
+    stage_mark(0, stream);
     if (stages & 1)
         hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
                            s->rec_base, total_dev);
-    const bool scan = (diag & 0x400) != 0;
-    diag &= ~0x400;
-    if ((stages & 2) && scan)
+    stage_mark(1, stream);
+    // diag (tuning builds): 0x800 = the first-generation parse kernel,
+    // 0x1000 = the first-generation execute kernel (low bits: its variants),
+    // 0x200/0x201 = LDS-ring staged execute v1/v2, 0x203..0x208 = seq_exec
+    // versions; 0 = the production pair lz4_scan_kernel + seq_exec v4
+    const bool old_parse = (diag & 0x800) != 0, old_exec = (diag & 0x1000) != 0;
+    const int xd = diag & 0x3FF;
+    if ((stages & 2) && !old_parse)
         launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                         s->nitems, d_status, d_fail_at, stream);
     else if (stages & 2)
         hipLaunchKernelGGL(lz4_parse_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                            s->nitems, d_status, d_fail_at);
-    if ((stages & 4) && diag >= 0x203 && diag <= 0x208) {
+    stage_mark(2, stream);
+    if ((stages & 4) && !old_exec && xd >= 0x203 && xd <= 0x208) {
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                        stream, diag & 0xF);
-    } else if ((stages & 4) && (diag == 0x200 || diag == 0x201)) {
+                        stream, xd & 0xF);
+    } else if ((stages & 4) && !old_exec && (xd == 0x200 || xd == 0x201)) {
         launch_lz4_exec_stage(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems,
-                              d_status, stream, diag == 0x201 ? 2 : 1);
+                              d_status, stream, xd == 0x201 ? 2 : 1);
+    } else if ((stages & 4) && !old_exec) {
+        launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
+                        stream, 4);
     } else if (stages & 4) {
         const dim3 grid((nframes + kExecWaves - 1) / kExecWaves), block(64 * kExecWaves);
 #define ZSK_EXEC(D, O)                                                                          \
     hipLaunchKernelGGL((lz4_exec_kernel<D, O>), grid, block, 0, stream, d_desc, nframes, d_comp, \
                        d_out, s->rec_base, s->items, s->nitems, d_status)
-        switch (diag) {
+        switch (xd) {
         case 1: ZSK_EXEC(1, 1); break;
         case 2: ZSK_EXEC(2, 1); break;
         case 8: ZSK_EXEC(8, 1); break;
@@ -771,11 +858,16 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         }
 #undef ZSK_EXEC
     }
-    if (hipGetLastError() != hipSuccess)
+    stage_mark(3, stream);
+    if (hipGetLastError() != hipSuccess) {
+        stage_mark(4, stream);
         return -1;
+    }
+    int rc = 0;
     if (stages & 8)
-        return launch_lz4_wave_deferred(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
-    return 0;
+        rc = launch_lz4_wave_deferred(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
+    stage_mark(4, stream);
+    return rc;
 }
 
 // Public device API (zsk_lz4_decode_frames): the host does not see the
@@ -801,8 +893,8 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
     // first call: room for 64 KiB frames (capped at 2 GiB of items); later
     // calls: what the previous plan on this stream needed
     uint64_t want = (uint64_t)nframes * slots_of(65536 + 64);
-    if (want > (256ull << 20))
-        want = 256ull << 20;
+    if (want > (512ull << 20))
+        want = 512ull << 20;
     if (s.total && *s.total > want)
         want = *s.total;
     if (split_scratch_reserve(&s, nframes, want, stream) != 0)
@@ -818,7 +910,7 @@ int lz4_pick_engine(uint32_t nframes)
     const int e = lz4_engine();
     if (e != ENGINE_AUTO)
         return e;
-    return nframes >= 32768 ? ENGINE_LANE : ENGINE_WAVE;
+    return nframes >= 32768 ? ENGINE_SPLIT : ENGINE_WAVE;
 }
 
 int lz4_engine()
@@ -854,14 +946,14 @@ int launch_lz4_split_stages(int stages, int diag, const FrameDesc *d_desc, uint3
         want = *s.total;
     if (split_scratch_reserve(&s, nframes, want, stream) != 0)
         return -1;
-    if (diag & 8) {
+    if ((diag & 0x1000) && (diag & 8)) {
         unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_exec_stats), z, sizeof(z), 0,
                                      hipMemcpyHostToDevice, stream);
     }
     int rc = launch_lz4_split(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, &s,
                               stages, diag);
-    if (diag & 8) {
+    if ((diag & 0x1000) && (diag & 8)) {
         unsigned long long z[8];
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_exec_stats), sizeof(z), 0,
                                        hipMemcpyDeviceToHost, stream);
@@ -878,7 +970,7 @@ const char *lz4_kernel_name(uint32_t nframes)
 {
     switch (lz4_pick_engine(nframes)) {
     case ENGINE_LANE: return "lz4_lane_kernel";
-    case ENGINE_SPLIT: return "lz4_exec_kernel";
+    case ENGINE_SPLIT: return "seq_exec_kernel";
     default: return "lz4_wave_kernel<4096, 4>";
     }
 }

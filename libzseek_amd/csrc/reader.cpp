@@ -607,6 +607,16 @@ extern "C" ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes)
     return zsk::lz4_kernel_name(nframes);
 }
 
+extern "C" ZSEEK_EXPORT int zsk_kernel_timing(int on)
+{
+    return zsk::kernel_timing(on);
+}
+
+extern "C" ZSEEK_EXPORT int zsk_kernel_times(double *ms, int cap)
+{
+    return zsk::kernel_times(ms, cap);
+}
+
 extern "C" ZSEEK_EXPORT const char *zsk_status_string(int32_t status)
 {
     return status_name(status);

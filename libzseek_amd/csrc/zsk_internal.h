@@ -92,7 +92,25 @@ int launch_lz4_split_stages(int stages, int diag, const FrameDesc *d_desc, uint3
                             hipStream_t stream);
 
 // Decoder selection (env ZSEEK_HIP_KERNEL = lane | split | wave; default auto).
+// Item slots of a frame in the split decoder's scratch.  An item is 8 bytes;
+// a sequence takes one (two when extended), a stored block two.  LZ4 data
+// spends >= 3 compressed bytes per sequence and typically 8-25; one slot per
+// 8 compressed bytes (+32) covers all but pathological frames, which do not
+// fit and are decoded by the wave kernel instead (parse reports ST_NOT_RUN).
+__host__ __device__ __forceinline__ uint32_t slots_of(uint32_t c_size)
+{
+    return (c_size / 8 + 32 + 3) & ~3u;
+}
+
 enum : int { ENGINE_AUTO = 0, ENGINE_LANE, ENGINE_SPLIT, ENGINE_WAVE };
+
+// Per-stage launch timing: stages [plan, parse, execute, hand-off]; marks
+// 0..4 are the boundaries, recorded as HIP events on the launch's stream
+// while enabled.
+constexpr int kTimedStages = 4;
+void stage_mark(int boundary, hipStream_t stream);
+int kernel_timing(int on);
+int kernel_times(double *ms, int cap);
 int lz4_engine();
 int lz4_pick_engine(uint32_t nframes);   // never ENGINE_AUTO
 

@@ -90,6 +90,7 @@ EXPORTED = [
     "zseek_pread", "zseek_read", "zseek_reader_stats",
     "zsk_lz4_decode_frames", "zsk_status_string", "zsk_lz4_kernel_name", "zsk_reader_frames", "zsk_reader_type",
     "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
+    "zsk_kernel_timing", "zsk_kernel_times",
 ]
 
 _lib = None
@@ -133,6 +134,10 @@ def lib() -> C.CDLL:
                                              C.c_void_p, C.c_void_p, C.c_void_p]
     L.zsk_lz4_kernel_name.restype = C.c_char_p
     L.zsk_lz4_kernel_name.argtypes = [C.c_uint32]
+    L.zsk_kernel_timing.restype = C.c_int
+    L.zsk_kernel_timing.argtypes = [C.c_int]
+    L.zsk_kernel_times.restype = C.c_int
+    L.zsk_kernel_times.argtypes = [C.POINTER(C.c_double), C.c_int]
     L.zsk_status_string.restype = C.c_char_p
     L.zsk_status_string.argtypes = [C.c_int32]
     L.zsk_reader_frames.restype = C.c_ssize_t
@@ -447,3 +452,18 @@ def decode_frames(desc, comp, out, status, stream: int | None = None,
                                               status.data_ptr(), stream)
     if rc != 0:
         raise ZseekError("zsk_lz4_decode_frames launch failed")
+
+
+STAGES = ("plan", "parse", "execute", "hand-off")
+
+
+def kernel_timing(on: bool) -> None:
+    """Switch per-stage event timing of the two-phase decoder (and clear it)."""
+    lib().zsk_kernel_timing(1 if on else 0)
+
+
+def kernel_times() -> tuple[int, dict]:
+    """(launches averaged, {stage: average ms}) since kernel_timing(True)."""
+    ms = (C.c_double * 4)()
+    n = lib().zsk_kernel_times(ms, 4)
+    return n, {k: float(ms[i]) for i, k in enumerate(STAGES)}

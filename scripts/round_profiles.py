@@ -3,9 +3,10 @@ and derive profiles/pmc_traffic.json for bench.py's roofline.traffic.
 
   python scripts/round_profiles.py r01 [gpurun_out/round]
 
-HBM bytes per launch of the decode kernel = 2 x FETCH_SIZE (gfx950 reports
-half the bytes of a wide streaming read, MI355X_MICROARCH.md HBM section) +
-WRITE_SIZE, both in KiB from separate --pmc passes, median over dispatches.
+HBM bytes per decode launch = sum over its kernels of 2 x FETCH_SIZE (gfx950
+reports half the bytes of a wide streaming read, MI355X_MICROARCH.md HBM
+section) + WRITE_SIZE, both in KiB from separate --pmc passes, median over
+dispatches per kernel.
 """
 import csv
 import glob
@@ -22,43 +23,58 @@ os.makedirs(dst, exist_ok=True)
 
 
 def one(pattern):
+    """the newest match (gpurun_out/ accumulates earlier calls' files)"""
     f = glob.glob(os.path.join(src, pattern))
     if not f:
         raise SystemExit(f"missing {pattern} under {src}")
-    return f[0]
+    return max(f, key=os.path.getmtime)
 
 
 bench = json.load(open(os.path.join(src, "bench.json")))
 KERNEL = bench["roofline"]["kernel"]   # the dominant kernel bench.py reports
+# kernels of one decode launch (zsk_lz4_decode_frames): the two-phase decoder
+# runs plan + parse + execute + the (normally empty) hand-off pass
+LAUNCH = ("lz4_plan_kernel", "lz4_scan_kernel", "seq_exec_kernel", "lz4_wave_kernel",
+          "lz4_lane_kernel", "lz4_parse_kernel", "lz4_exec_kernel")
 
 
-def is_decode(name):
-    return KERNEL in name
+def part(name):
+    for k in LAUNCH:
+        if k in name:
+            return k
+    return None
 
 
 stats = one("trace/*/*_kernel_stats.csv")
 shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
-kern = None
+kern = {}
 for row in csv.DictReader(open(stats)):
-    if is_decode(row["Name"]):
-        kern = (row["Name"], float(row["AverageNs"]), int(row["Calls"]))
-        break
+    k = part(row["Name"])
+    if k:
+        nm = row["Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        kern[k] = {"name": nm, "avg_ns": float(row["AverageNs"]),
+                   "calls": int(row["Calls"])}
 counters = {}
 for name in ("fetch", "write"):
     f = one(f"pmc_{name}/*/*_counter_collection.csv")
     shutil.copy(f, os.path.join(dst, f"{tag}_pmc_{name}.csv"))
     for row in csv.DictReader(open(f)):
-        if is_decode(row["Kernel_Name"]):
-            counters.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-fetch = statistics.median(counters["FETCH_SIZE"]) * 1024
-write = statistics.median(counters["WRITE_SIZE"]) * 1024
+        k = part(row["Kernel_Name"])
+        if k:
+            counters.setdefault((k, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
+per = {}
+for (k, c), v in counters.items():
+    per.setdefault(k, {})[c] = statistics.median(v) * 1024
+fetch = sum(d.get("FETCH_SIZE", 0.0) for d in per.values())
+write = sum(d.get("WRITE_SIZE", 0.0) for d in per.values())
 alg = bench["roofline"]["algorithmic_bytes_per_launch"]
 out = {
     "round": tag,
-    "kernel": kern[0],
-    "avg_kernel_ns_rocprof": kern[1],
-    "calls": kern[2],
-    "bench_avg_kernel_ms": bench["roofline"]["avg_kernel_ms"],
+    "kernel": KERNEL,
+    "launch_kernels": {k: {**kern.get(k, {}), "fetch_bytes_raw": per.get(k, {}).get("FETCH_SIZE"),
+                           "write_bytes": per.get(k, {}).get("WRITE_SIZE")} for k in sorted(set(kern) | set(per))},
+    "launch_avg_ns_rocprof": sum(v["avg_ns"] for v in kern.values()),
+    "bench_avg_launch_ms": bench["roofline"]["avg_launch_ms"],
     "fetch_size_bytes_raw": fetch,
     "fetch_bytes_corrected_x2": 2 * fetch,
     "write_size_bytes": write,
