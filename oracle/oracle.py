@@ -70,6 +70,8 @@ class Oracle:
                                            C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]
         L.orc_synth_gen.restype = None
         L.orc_synth_gen.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.orc_zstd_decode.restype = C.c_longlong
+        L.orc_zstd_decode.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
 
     # -- hashes -----------------------------------------------------------
     def xxh32(self, data: bytes, seed: int = 0) -> int:
@@ -107,6 +109,15 @@ class Oracle:
                                       C.byref(mb))
         info = {"fail_at": fa.value, "block_fail": bool(bf.value), "max_block": mb.value}
         return st, d[: dl.value].tobytes(), su.value, info
+
+    def zstd_decode(self, src: bytes, dst_cap: int):
+        """ZSTD_decompressDCtx restated -> (decoded bytes, 0) or (b"", zstd error code)."""
+        s = np.frombuffer(src, np.uint8)
+        d = np.empty(max(dst_cap, 1), np.uint8)
+        r = self.lib.orc_zstd_decode(s.ctypes.data, s.size, d.ctypes.data, dst_cap)
+        if r < 0:
+            return b"", -r
+        return d[:r].tobytes(), 0
 
     def seek_table(self, file: bytes):
         """-> dict(c_off, d_off, checksum, checksum_flag) or None."""
