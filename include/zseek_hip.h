@@ -10,6 +10,9 @@
  *                            /root/reference/src/decompress.c:752-773 (and
  *                            :627-664 for the no-cache variant), batched over
  *                            every frame of a request in one grid.
+ *   zsk_zstd_decode_frames — ZSTD_decompressDCtx (decompress.c:537) /
+ *                            ZSTD_decompressStream (:414-454), batched the
+ *                            same way.
  *   zsk_reader_frames      — the seek-table accessors frame_offset_c/d and
  *                            frame_size_c/d, seek_table.c:204-226.
  *   zsk_pread_device       — zseek_pread (decompress.c:806-824) with the
@@ -57,7 +60,22 @@ ZSEEK_EXPORT int zsk_lz4_decode_frames(const zsk_frame_desc_t *d_desc,
     uint32_t nframes, const void *d_comp, void *d_out, int32_t *d_status,
     void *stream);
 
-/* Human-readable name of a frame status (LZ4F-style "ERROR_..." names). */
+/*
+ * Decode @nframes independent zstd frames (each seek-table entry: the zstd
+ * frames and skippable frames it holds, as ZSTD_decompressDCtx decodes them)
+ * on the GPU, on @stream.  Same descriptors and per-frame status as
+ * zsk_lz4_decode_frames; a failed frame's status is ZSK_STATUS_ZSTD | the
+ * ZSTD_ErrorCode libzstd 1.4.9 reports for it.  The call synchronizes
+ * @stream once, after the planning kernel (a frame's sequence count sizes its
+ * scratch), and returns with the decode queued.  Returns 0 or -1.
+ */
+ZSEEK_EXPORT int zsk_zstd_decode_frames(const zsk_frame_desc_t *d_desc,
+    uint32_t nframes, const void *d_comp, void *d_out, int32_t *d_status,
+    void *stream);
+#define ZSK_STATUS_ZSTD 0x4000000 /* zstd frame failure: low bits = ZSTD_ErrorCode */
+
+/* Human-readable name of a frame status (LZ4F-style "ERROR_..." names for
+ * LZ4 frames, ZSTD_getErrorName strings for zstd frames). */
 ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
 
 /* Name of the dominant HIP kernel zsk_lz4_decode_frames launches for a

@@ -93,6 +93,7 @@ struct DeviceCtx {
     uint32_t *h_fail = nullptr;
     size_t h_fail_cap = 0;
     SplitScratch split;            // two-phase decoder scratch (lz4_split.hip)
+    ZstdScratch zs;                // zstd decoder scratch (zstd_decode.hip)
     uint64_t batches = 0, frames_decoded = 0, bytes_decoded = 0, bytes_uploaded = 0;
 
     ~DeviceCtx();
@@ -100,7 +101,8 @@ struct DeviceCtx {
     bool reserve(size_t comp, size_t out, size_t nframes, char *errbuf);
     size_t device_bytes() const
     {
-        return d_comp_cap + d_out_cap + d_desc_cap * 28 + split.frames_cap * 12 + split.items_cap * 8;
+        return d_comp_cap + d_out_cap + d_desc_cap * 28 + split.frames_cap * 12 + split.items_cap * 8 +
+               zs.frames_cap * 24 + zs.lit_cap + zs.items_cap * 8;
     }
     size_t host_bytes() const { return h_comp_cap + h_desc_cap * 28; }
 };

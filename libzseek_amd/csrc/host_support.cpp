@@ -201,6 +201,7 @@ DeviceCtx::~DeviceCtx()
     (void)hipFree(d_status);
     (void)hipFree(d_fail);
     split_scratch_free(&split);
+    zstd_scratch_free(&zs);
     (void)hipHostFree(h_fail);
     (void)hipHostFree(h_comp);
     (void)hipHostFree(h_desc);
@@ -290,8 +291,32 @@ bool DeviceCtx::reserve(size_t comp, size_t out, size_t nframes, char *errbuf)
 // ---------------------------------------------------------------------------
 // status names (LZ4F_getErrorName strings of liblz4 1.9.3 for 1..19)
 // ---------------------------------------------------------------------------
+// ZSTD_getErrorName strings of libzstd 1.4.9 (zstd_errors.h codes)
+static const char *zstd_name(int32_t code)
+{
+    switch (code) {
+    case 1: return "Error (generic)";
+    case 10: return "Unknown frame descriptor";
+    case 12: return "Version not supported";
+    case 14: return "Unsupported frame parameter";
+    case 16: return "Frame requires too much memory for decoding";
+    case 20: return "Corrupted block detected";
+    case 22: return "Restored data doesn't match checksum";
+    case 30: return "Dictionary is corrupted";
+    case 32: return "Dictionary mismatch";
+    case 44: return "tableLog requires too much memory : unsupported";
+    case 46: return "Unsupported max Symbol Value : too large";
+    case 48: return "Specified maxSymbolValue is too small";
+    case 70: return "Destination buffer is too small";
+    case 72: return "Src size is incorrect";
+    default: return "Unspecified error code";
+    }
+}
+
 const char *status_name(int32_t st)
 {
+    if (st & ST_ZSTD_FLAG)
+        return zstd_name(st & 0xFFFF);
     static const char *const names[] = {
         "OK_NoError", "ERROR_GENERIC", "ERROR_maxBlockSize_invalid",
         "ERROR_blockMode_invalid", "ERROR_contentChecksumFlag_invalid",

@@ -5,13 +5,15 @@
 // conventions follow it line for line in behaviour (cited per function);
 // the pread hot path is redesigned:
 //
-//   reference (decompress.c:685-804)       this file (pread_lz4)
+//   reference (decompress.c:377-804)       this file (pread_frames)
 //   -------------------------------------  -------------------------------------
 //   1 frame per call                        every frame covered by
 //                                           [offset, offset+count) per call
 //   1 user pread per frame                  1 user pread per batch (contiguous
 //                                           compressed span, pinned staging)
-//   LZ4F_decompress on the CPU              one HIP grid over the batch
+//   LZ4F_decompress / ZSTD_decompress*      HIP kernels over the batch (LZ4:
+//   on the CPU                              lz4_*.hip + seq_exec.hip; zstd:
+//                                           zstd_decode.hip + seq_exec.hip)
 //   cache every decoded frame               cache the last cache_size frames of
 //                                           the request (same final LRU state
 //                                           as the reference's call loop)
@@ -27,10 +29,11 @@
 #include <sys/stat.h>
 
 #include <mutex>
+#include <map>
 #include <new>
+#include <utility>
 
 #include <hip/hip_runtime_api.h>
-#include <zstd.h>
 
 #include "../../include/zseek_hip.h"
 #include "host.h"
@@ -52,10 +55,6 @@ struct zseek_reader {
     size_t pos = 0;                // zseek_read cursor (ref :826-835)
     size_t batch_bytes = kDefaultBatch;
     DeviceCtx gpu;
-    // zstd (host libzstd until the GPU zstd decoder lands)
-    ZSTD_DCtx *zdctx = nullptr;
-    ZSTD_DStream *zds = nullptr;
-    std::vector<uint8_t> zcbuf, zdbuf;
 };
 
 // ---------------------------------------------------------------------------
@@ -123,21 +122,8 @@ extern "C" ZSEEK_EXPORT zseek_reader_t *zseek_reader_open_full(zseek_read_file_t
     }
     r->type = type;
     r->user_file = user_file;
-    if (type == ZSEEK_ZSTD) {
-        r->zdctx = ZSTD_createDCtx();
-        r->zds = ZSTD_createDStream();
-        if (!r->zdctx || !r->zds) {
-            set_error(errbuf, r->zdctx ? "dstream creation failed" : "context creation failed");
-            ZSTD_freeDCtx(r->zdctx);
-            ZSTD_freeDStream(r->zds);
-            delete r;
-            return nullptr;
-        }
-    }
     if (!read_seek_table(user_file, call_data, &r->st)) {
         set_error(errbuf, "read_seek_table failed");
-        ZSTD_freeDCtx(r->zdctx);
-        ZSTD_freeDStream(r->zds);
         delete r;
         return nullptr;
     }
@@ -145,8 +131,6 @@ extern "C" ZSEEK_EXPORT zseek_reader_t *zseek_reader_open_full(zseek_read_file_t
         r->cache = new (std::nothrow) FrameCache(cache_size);
     if (cache_size > 0 && !r->cache) {
         set_error(errbuf, "cache creation failed");
-        ZSTD_freeDCtx(r->zdctx);
-        ZSTD_freeDStream(r->zds);
         delete r;
         return nullptr;
     }
@@ -173,8 +157,6 @@ extern "C" ZSEEK_EXPORT bool zseek_reader_close(zseek_reader_t *reader, void *ca
     (void)errbuf;
     if (!reader)
         return true;   // ref decompress.c:362-363
-    ZSTD_freeDStream(reader->zds);
-    ZSTD_freeDCtx(reader->zdctx);
     delete reader->cache;
     delete reader;
     return true;
@@ -233,7 +215,15 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
                            g.stream);
     if (e == hipSuccess)
         e = hipMemsetD32Async((hipDeviceptr_t)g.d_status, ST_NOT_RUN, n, g.stream);
-    const int engine = lz4_pick_engine((uint32_t)n);
+    if (r->type == ZSEEK_ZSTD) {
+        // zstd: plan + decode (zstd_decode.hip); failures carry no output offset
+        if (e == hipSuccess)
+            e = hipMemsetD32Async((hipDeviceptr_t)g.d_fail, 0, n, g.stream);
+        if (e == hipSuccess && zstd_decode_frames(g.d_desc, (uint32_t)n, g.d_comp, g.d_out,
+                                                  g.d_status, &g.zs, g.stream) != 0)
+            e = hipErrorLaunchFailure;
+    }
+    const int engine = r->type == ZSEEK_ZSTD ? -1 : lz4_pick_engine((uint32_t)n);
     if (e == hipSuccess && engine == ENGINE_LANE &&
         launch_lz4_lane(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
                         g.stream) != 0)
@@ -308,6 +298,17 @@ void frame_error(zseek_reader *r, const BatchResult &br, size_t frame, size_t of
         uint64_t used = at - offset_in_frame;
         room = want > used ? want - used : 0;
     }
+    if (r->type == ZSEEK_ZSTD) {
+        // libzstd: ZSTD_decompressDCtx (cached) or ZSTD_decompressStream
+        // (discard the in-frame prefix, then the caller's bytes,
+        // decompress.c:434-451); a whole-frame decode cannot tell in which
+        // of the two streaming calls libzstd would have met the failure, so
+        // a request starting inside the frame reports the discard phase
+        if (!r->cache)
+            prefix = offset_in_frame ? "decompress discard data" : "decompress user data";
+        set_error(errbuf, "%s: %s", prefix, status_name(st));
+        return;
+    }
     const char *name = status_name(st);
     if (st & ST_BLOCK_FAIL_FLAG)
         name = status_name(room >= status_max_block(st) ? ST_GENERIC : ST_DECOMPRESS_FAILED);
@@ -356,8 +357,9 @@ bool cache_frames(zseek_reader *r, size_t f0, size_t a, size_t b, char *errbuf)
     return true;
 }
 
-// LZ4 range read: [offset, offset+count) into buf (host or device memory).
-ssize_t pread_lz4(zseek_reader *r, void *buf, size_t count, size_t offset, void *call_data,
+// Range read: [offset, offset+count) into buf (host or device memory), both
+// codecs (ref decompress.c:685-804 LZ4, :377-574 zstd).
+ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, void *call_data,
                   char *errbuf, bool device_dst)
 {
     const SeekTable &st = r->st;
@@ -438,89 +440,6 @@ ssize_t pread_lz4(zseek_reader *r, void *buf, size_t count, size_t offset, void 
     return (ssize_t)done;
 }
 
-// zstd frame read on the host with libzstd, one frame per call, exactly as
-// the reference does (decompress.c:377-574).  Interim: the GPU zstd decoder
-// is the next row of SURVEY §8f.
-ssize_t pread_zstd(zseek_reader *r, void *buf, size_t count, size_t offset, void *call_data,
-                   char *errbuf)
-{
-    const SeekTable &st = r->st;
-    int64_t fi = st.frame_of(offset);
-    if (fi < 0)
-        return 0;
-    std::lock_guard<std::mutex> guard(r->lock);
-    const size_t f = (size_t)fi;
-    const size_t rel = offset - st.d_off[f];
-    const size_t dsz = st.dsize(f);
-    if (r->cache) {
-        size_t len = 0;
-        const uint8_t *data = r->cache->find(f, &len);
-        if (!data) {
-            r->zcbuf.resize(st.csize(f));
-            if (!read_span(r, r->zcbuf.data(), r->zcbuf.size(), st.c_off[f], call_data, errbuf))
-                return -1;
-            uint8_t *p = (uint8_t *)malloc(dsz ? dsz : 1);
-            if (!p) {
-                set_error_errno(errbuf, "allocate decompressed buffer", errno);
-                return -1;
-            }
-            size_t rr = ZSTD_decompressDCtx(r->zdctx, p, dsz, r->zcbuf.data(), r->zcbuf.size());
-            if (ZSTD_isError(rr)) {
-                set_error(errbuf, "%s: %s", "decompress frame", ZSTD_getErrorName(rr));
-                free(p);
-                return -1;
-            }
-            if (!r->cache->insert(f, p, dsz)) {
-                free(p);
-                set_error(errbuf, "frame caching failed");
-                return -1;
-            }
-            data = r->cache->find(f, &len);
-        }
-        size_t n = count < len - rel ? count : len - rel;
-        memcpy(buf, data + rel, n);
-        return (ssize_t)n;
-    }
-    r->zcbuf.resize(st.csize(f));
-    if (!read_span(r, r->zcbuf.data(), r->zcbuf.size(), st.c_off[f], call_data, errbuf))
-        return -1;
-    size_t rr = ZSTD_initDStream(r->zds);
-    if (ZSTD_isError(rr)) {
-        set_error(errbuf, "%s: %s", "initialize dstream", ZSTD_getErrorName(rr));
-        return -1;
-    }
-    ZSTD_inBuffer in = {r->zcbuf.data(), r->zcbuf.size(), 0};
-    if (rel > 0) {
-        r->zdbuf.resize(rel);
-        ZSTD_outBuffer ob = {r->zdbuf.data(), rel, 0};
-        while (ob.pos < ob.size) {
-            rr = ZSTD_decompressStream(r->zds, &ob, &in);
-            if (ZSTD_isError(rr)) {
-                set_error(errbuf, "%s: %s", "decompress discard data", ZSTD_getErrorName(rr));
-                return -1;
-            }
-            if (rr == 0 && ob.pos < ob.size) {
-                set_error(errbuf, "decompress discard data: frame shorter than seek table");
-                return -1;
-            }
-        }
-    }
-    size_t n = count < dsz - rel ? count : dsz - rel;
-    ZSTD_outBuffer ob = {buf, n, 0};
-    while (ob.pos < ob.size) {
-        rr = ZSTD_decompressStream(r->zds, &ob, &in);
-        if (ZSTD_isError(rr)) {
-            set_error(errbuf, "%s: %s", "decompress user data", ZSTD_getErrorName(rr));
-            return -1;
-        }
-        if (rr == 0 && ob.pos < ob.size) {
-            set_error(errbuf, "decompress user data: frame shorter than seek table");
-            return -1;
-        }
-    }
-    return (ssize_t)n;
-}
-
 }   // namespace
 
 // ---------------------------------------------------------------------------
@@ -533,9 +452,7 @@ extern "C" ZSEEK_EXPORT ssize_t zseek_pread(zseek_reader_t *reader, void *buf, s
         set_error(errbuf, "invalid reader");
         return 0;   // ref decompress.c:809-812 returns false (0)
     }
-    if (reader->type == ZSEEK_ZSTD)
-        return pread_zstd(reader, buf, count, offset, call_data, errbuf);
-    return pread_lz4(reader, buf, count, offset, call_data, errbuf, false);
+    return pread_frames(reader, buf, count, offset, call_data, errbuf, false);
 }
 
 extern "C" ZSEEK_EXPORT ssize_t zseek_read(zseek_reader_t *reader, void *buf, size_t count,
@@ -568,10 +485,7 @@ extern "C" ZSEEK_EXPORT bool zseek_reader_stats(zseek_reader_t *reader,
     stats->decompressed_size = reader->st.decompressed_size();
     stats->cache_memory = reader->cache ? reader->cache->memory_usage() : 0;
     stats->cached_frames = reader->cache ? reader->cache->entries() : 0;
-    size_t buffered = reader->gpu.host_bytes() + reader->zcbuf.capacity() +
-                      reader->zdbuf.capacity();
-    if (reader->type == ZSEEK_ZSTD)
-        buffered += ZSTD_sizeof_DCtx(reader->zdctx) + ZSTD_sizeof_DStream(reader->zds);
+    size_t buffered = reader->gpu.host_bytes();
     stats->buffer_size = buffered;
     return true;
 }
@@ -605,6 +519,22 @@ extern "C" ZSEEK_EXPORT int zsk_dev_lz4_decode_variant(int variant, const zsk_fr
 extern "C" ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes)
 {
     return zsk::lz4_kernel_name(nframes);
+}
+
+extern "C" ZSEEK_EXPORT int zsk_zstd_decode_frames(const zsk_frame_desc_t *d_desc,
+                                                   uint32_t nframes, const void *d_comp,
+                                                   void *d_out, int32_t *d_status, void *stream)
+{
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, ZstdScratch> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    ZstdScratch &s = cache[{dev, static_cast<hipStream_t>(stream)}];
+    return zsk::zstd_decode_frames(reinterpret_cast<const FrameDesc *>(d_desc), nframes,
+                                   static_cast<const uint8_t *>(d_comp),
+                                   static_cast<uint8_t *>(d_out), d_status, &s,
+                                   static_cast<hipStream_t>(stream));
 }
 
 extern "C" ZSEEK_EXPORT int zsk_kernel_timing(int on)
@@ -648,11 +578,7 @@ extern "C" ZSEEK_EXPORT ssize_t zsk_pread_device(zseek_reader_t *reader, void *d
         set_error(errbuf, "invalid reader");
         return 0;
     }
-    if (reader->type != ZSEEK_LZ4) {
-        set_error(errbuf, "device reads need an LZ4 file");
-        return -1;
-    }
-    return pread_lz4(reader, d_buf, count, offset, call_data, errbuf, true);
+    return pread_frames(reader, d_buf, count, offset, call_data, errbuf, true);
 }
 
 extern "C" ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader, zsk_gpu_stats_t *s)

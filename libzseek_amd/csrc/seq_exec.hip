@@ -352,7 +352,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
-    const int32_t *__restrict__ status)
+    const int32_t *__restrict__ status, const uint8_t *__restrict__ lit)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * kXWave];
     const uint32_t lane = threadIdx.x & 63;
@@ -369,7 +369,10 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     O.o = out + d.d_off;
     O.dlen = d.d_size;
     O.sp = make_span(O.o, d.d_size);
-    const Span lsp = make_span(comp + d.c_off, d.c_size);   // literal source: the compressed frame
+    // literal source: the compressed frame (LZ4), or the frame's decoded
+    // literals (zstd scratch laid out like the output, 16 bytes of slack)
+    const Span lsp = lit ? make_span(lit + d.d_off, (uint64_t)d.d_size + 16)
+                         : make_span(comp + d.c_off, d.c_size);
     Stage S;
     S.base = (uint32_t)(uintptr_t)(lds + w * kXWave);
     const uint32_t descs = S.base + kXBuf;
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         const uint32_t w0p = dpp_prev(w0, 0);
         const bool act0 = b + lane < nit;
         const uint32_t src = w0 & kItemPos;
-        const uint32_t off = w1 & 0xFFFF;
+        const uint32_t off = (w0 & kItemExt) ? w1 : (w1 & 0xFFFF);   // extended: full offset
         uint32_t lit = 0, ml = 0;
         if (act0 && !(w0p & kItemExt)) {
             if (w0 & kItemExt) {
@@ -563,7 +566,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
 #define ZSK_X(D, G)                                                                            \
     hipLaunchKernelGGL((seq_exec_kernel<D, G>), grid, block, 0, stream, d_desc, nframes, d_comp, \
-                       d_out, rec_base, items, nitems, d_status)
+                       d_out, rec_base, items, nitems, d_status, nullptr)
     switch (version) {
     case 3: ZSK_X(false, 0); break;
     case 5: ZSK_X(true, 1); break;
@@ -586,6 +589,17 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     default: ZSK_X(true, 0); break;
     }
 #undef ZSK_X
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *lit,
+                        uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
+                        const uint32_t *nitems, const int32_t *d_status, hipStream_t stream)
+{
+    if (nframes == 0)
+        return 0;
+    hipLaunchKernelGGL((seq_exec_kernel<true, 0>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+                       stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

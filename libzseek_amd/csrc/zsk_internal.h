@@ -47,6 +47,7 @@ enum : int32_t {
     ST_DIRECT_FLAG = 0x10000,
     ST_BLOCK_FAIL_FLAG = 0x20000,   // failure inside an LZ4 block (fail_at valid)
     ST_BSID_SHIFT = 24,             // bits 24-25: block size id - 4 of the frame
+    ST_ZSTD_FLAG = 0x4000000,       // zstd frame failure: low bits = ZSTD_ErrorCode
 };
 
 inline uint32_t status_max_block(int32_t st)
@@ -127,6 +128,36 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
                     int version = 4);
+
+// Execute phase over items whose literal runs come from a literal scratch
+// laid out like the output (zstd): frame f's literals at lit + d_off[f].
+int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *lit,
+                        uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
+                        const uint32_t *nitems, const int32_t *d_status, hipStream_t stream);
+
+// zstd decoder (zstd_decode.hip): plan (item bounds -> rec_base[0..n]) and
+// decode (frame kernel -> items + literal scratch, execute, checksums).
+struct ZstdScratch {
+    uint32_t *bound = nullptr;     // per-frame item bound
+    uint64_t *rec_base = nullptr;  // n + 1 slot offsets
+    uint32_t *nitems = nullptr;
+    uint64_t *ck = nullptr;        // per-frame checksum request
+    uint8_t *lit = nullptr;        // literal scratch (output-sized + 64)
+    uint64_t *items = nullptr;
+    uint64_t *total = nullptr;     // host-mapped: [0] item total, [1] output extent of the last plan
+    uint32_t frames_cap = 0;
+    uint64_t lit_cap = 0, items_cap = 0;
+};
+int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, uint64_t items,
+                         hipStream_t stream);
+void zstd_scratch_free(ZstdScratch *s);
+int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                     ZstdScratch *s, hipStream_t stream);
+int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream);
+// plan + synchronize + reserve + decode
+int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream);
 
 // Parse phase, streaming lane-per-frame (lz4_scan.hip): same outputs as
 // lz4_parse_kernel.

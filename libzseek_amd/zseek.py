@@ -90,7 +90,7 @@ EXPORTED = [
     "zseek_pread", "zseek_read", "zseek_reader_stats",
     "zsk_lz4_decode_frames", "zsk_status_string", "zsk_lz4_kernel_name", "zsk_reader_frames", "zsk_reader_type",
     "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
-    "zsk_kernel_timing", "zsk_kernel_times",
+    "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
 ]
 
 _lib = None
@@ -129,6 +129,9 @@ def lib() -> C.CDLL:
     L.zsk_lz4_decode_frames.restype = C.c_int
     L.zsk_lz4_decode_frames.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_void_p]
+    L.zsk_zstd_decode_frames.restype = C.c_int
+    L.zsk_zstd_decode_frames.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p]
     L.zsk_dev_lz4_decode_variant.restype = C.c_int
     L.zsk_dev_lz4_decode_variant.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p,
                                              C.c_void_p, C.c_void_p, C.c_void_p]
@@ -452,6 +455,24 @@ def decode_frames(desc, comp, out, status, stream: int | None = None,
                                               status.data_ptr(), stream)
     if rc != 0:
         raise ZseekError("zsk_lz4_decode_frames launch failed")
+
+
+def zstd_decode_frames(desc, comp, out, status, stream: int | None = None) -> None:
+    """zsk_zstd_decode_frames on torch device tensors (same layout as
+    decode_frames; synchronizes the stream once, after its planning kernel)."""
+    import torch
+    n = status.numel()
+    if desc.numel() != n * 24:
+        raise ValueError("desc must hold 24 bytes per frame")
+    for t in (desc, comp, out, status):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("zstd_decode_frames needs contiguous device tensors")
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    rc = lib().zsk_zstd_decode_frames(desc.data_ptr(), n, comp.data_ptr(), out.data_ptr(),
+                                      status.data_ptr(), stream)
+    if rc != 0:
+        raise ZseekError("zsk_zstd_decode_frames launch failed")
 
 
 STAGES = ("plan", "parse", "execute", "hand-off")

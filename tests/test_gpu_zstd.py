@@ -1,0 +1,250 @@
+"""GPU parity for zstd: zsk_zstd_decode_frames and the
+reader's zstd preads vs the reference's own outputs (golden files made by
+oracle/_ref), libzstd 1.4.9 itself, and the oracle (oracle/zstd_oracle.c) on
+corrupt frames.  Bit-exact outputs; per-frame statuses equal the libzstd
+error code the oracle restates."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import golden_file, sha
+from zstd_util import (P_CHECKSUM, P_CSIZE, P_LEVEL, P_MINMATCH, P_STRAT, P_WLOG, compress,
+                       compress_stream, load)
+
+pytestmark = pytest.mark.gpu
+
+ZSTD_FILES = ["zstd_64k_direct", "zstd_64k_buffered"]
+ZSK_STATUS_ZSTD = 0x4000000
+
+
+@pytest.fixture(scope="module")
+def zstd():
+    z = load()
+    if z is None:
+        pytest.skip("libzstd 1.4.9 not present")
+    return z
+
+
+def device_decode(zs, gpu, frames, sizes, pad=0):
+    """decode a list of compressed frames (bytes) with decoded sizes via the
+    device API -> (list of decoded bytes, status array)"""
+    import torch
+    n = len(frames)
+    desc = np.zeros(n, zs.FRAME_DESC_DTYPE)
+    c = d = 0
+    for i, (f, s) in enumerate(zip(frames, sizes)):
+        desc[i]["c_off"], desc[i]["d_off"] = c, d
+        desc[i]["c_size"], desc[i]["d_size"] = len(f), s
+        c += len(f) + pad
+        d += s
+    blob = bytearray()
+    for f in frames:
+        blob += f + bytes(pad)
+    comp = torch.zeros(len(blob) + 64, dtype=torch.uint8, device=gpu)
+    if blob:
+        comp[: len(blob)].copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+    out = torch.zeros(max(d, 1), dtype=torch.uint8, device=gpu)
+    status = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    dt = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
+    zs.zstd_decode_frames(dt, comp, out, status)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().tobytes()
+    res, p = [], 0
+    for s in sizes:
+        res.append(o[p: p + s])
+        p += s
+    return res, status.cpu().numpy()
+
+
+def datasets(oracle):
+    rng = np.random.default_rng(7)
+    synth = oracle.synth(400_000, 5).tobytes()
+    words = [b"seek", b"frame", b"table", b"zstd", b"lz4", b"gpu", b"wave", b"lane", b"the", b"of"]
+    text = b" ".join(words[i] for i in rng.integers(0, len(words), 50_000))
+    return {
+        "synth": synth,
+        "text": text,
+        "random": rng.integers(0, 256, 150_000, dtype=np.uint8).tobytes(),
+        "zeros": bytes(140_000),
+        "periodic": bytes(range(13)) * 9000,
+        "mixed": synth[:60_000] + bytes(50_000) + rng.integers(0, 256, 30_000, dtype=np.uint8).tobytes() + text[:60_000],
+        "tiny": b"zseek",
+    }
+
+
+@pytest.mark.parametrize("level", [-5, 1, 3, 9, 19])
+def test_device_zstd_levels(gpu, zs, oracle, zstd, level):
+    """every dataset, one frame each, compressed by libzstd at several levels"""
+    data = datasets(oracle)
+    names = sorted(data)
+    frames = [compress(zstd, data[k], {P_LEVEL: level}) for k in names]
+    out, st = device_decode(zs, gpu, frames, [len(data[k]) for k in names])
+    for k, o, s in zip(names, out, st):
+        assert s == 0, (k, hex(int(s)))
+        assert o == data[k], k
+
+
+def test_device_zstd_frame_variants(gpu, zs, oracle, zstd):
+    """unknown content size + multi-block streamed frames (treeless literals,
+    repeat-mode tables, window descriptors), checksums, other strategies and
+    parameters, concatenated and skippable frames in one entry"""
+    data = datasets(oracle)
+    frames, sizes = [], []
+    for k in ("synth", "text", "mixed"):
+        for chunk in (1000, 30_000):
+            frames.append(compress_stream(zstd, data[k], chunk))
+            sizes.append(len(data[k]))
+        for params in ({P_LEVEL: 3, P_CHECKSUM: 1}, {P_LEVEL: 3, P_STRAT: 1},
+                       {P_LEVEL: 7, P_WLOG: 10}, {P_LEVEL: 12, P_MINMATCH: 3},
+                       {P_LEVEL: 3, P_CSIZE: 0}):
+            frames.append(compress(zstd, data[k], params))
+            sizes.append(len(data[k]))
+    a, b = data["synth"][:70_000], data["text"][:40_000]
+    skip = (0x184D2A5E).to_bytes(4, "little") + (3).to_bytes(4, "little") + b"abc"
+    frames.append(compress(zstd, a, {P_LEVEL: 3}) + skip + compress(zstd, b, {P_LEVEL: 1}))
+    sizes.append(len(a) + len(b))
+    want = [data[k] for k in ("synth", "text", "mixed") for _ in range(7)] + [a + b]
+    out, st = device_decode(zs, gpu, frames, sizes, pad=3)
+    for i, (o, s) in enumerate(zip(out, st)):
+        assert s == 0, (i, hex(int(s)))
+        assert o == want[i], i
+
+
+@pytest.mark.parametrize("frame", [4096, 65536, 1 << 20, 100_000])
+def test_device_zstd_synthetic(gpu, zs, frame):
+    """the §8d synthetic as the reference writer compresses it (level 3,
+    strategy 1), several frame sizes, through the device API"""
+    data = zs.synth_buffer(24 << 20)
+    img = zs.zstd_seekable(data, frame)
+    c_off, d_off = zs.seek_table_of(img)
+    n = len(c_off) - 1
+    frames = [img[c_off[i]: c_off[i + 1]].tobytes() for i in range(n)]
+    sizes = [int(d_off[i + 1] - d_off[i]) for i in range(n)]
+    out, st = device_decode(zs, gpu, frames, sizes)
+    assert int((st != 0).sum()) == 0
+    assert b"".join(out) == data.tobytes()
+
+
+def test_device_zstd_corrupt_status(gpu, zs, oracle, zstd):
+    """single-byte corruptions and truncations: every frame's status is the
+    libzstd error code the oracle gives, intact frames decode bit-exact"""
+    rng = np.random.default_rng(3)
+    data = datasets(oracle)
+    frames, sizes = [], []
+    for k, level in (("synth", 3), ("text", 19), ("mixed", 1)):
+        src = data[k][:60_000]
+        comp = compress(zstd, src, {P_LEVEL: level})
+        for pos in rng.integers(0, len(comp), 60):
+            c = bytearray(comp)
+            c[pos] ^= int(rng.integers(1, 256))
+            frames.append(bytes(c))
+            sizes.append(len(src))
+        for cut in (1, 5, 9, 20, len(comp) // 2, len(comp) - 1):
+            frames.append(comp[:cut])
+            sizes.append(len(src))
+    out, st = device_decode(zs, gpu, frames, sizes)
+    for i, (f, n) in enumerate(zip(frames, sizes)):
+        want, err = oracle.zstd_decode(f, n)
+        if err:
+            assert st[i] == ZSK_STATUS_ZSTD | err, (i, hex(int(st[i])), err)
+        else:
+            ok = len(want) == n
+            assert st[i] == (0 if ok else 101), (i, hex(int(st[i])))
+            if ok:
+                assert out[i] == want, i
+
+
+# ---------------------------------------------------------------------------
+# the reader (zseek_pread) on the reference-generated golden files
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ZSTD_FILES)
+@pytest.mark.parametrize("cache", [0, 1])
+def test_zstd_full_range_pread(gpu, zs, golden, payloads, name, cache):
+    data = payloads[name]
+    with zs.Reader(golden_file(name), cache) as r:
+        got = r.pread(len(data) + 17, 0)
+        assert len(got) == len(data)
+        assert sha(got) == golden["files"][name]["payload_sha256"]
+
+
+@pytest.mark.parametrize("name", ZSTD_FILES)
+def test_zstd_reference_queries(gpu, zs, golden, payloads, name):
+    """every query the reference answered: our (possibly longer, multi-frame)
+    answer starts with exactly its bytes; the cache ends in its state"""
+    entry = golden["files"][name]
+    data = payloads[name]
+    readers = {c: zs.Reader(golden_file(name), c) for c in (0, 1)}
+    try:
+        for q in entry["reads"]:
+            r = readers[q["cache"]]
+            off, cnt, ref_ret = q["offset"], q["count"], q["ret"]
+            out = np.empty(max(cnt, 1), np.uint8)
+            ret = r.pread_raw(out.ctypes.data, cnt, off)
+            assert ret == max(0, min(cnt, len(data) - off)), q
+            assert ret >= ref_ret
+            assert sha(out[:ref_ret]) == q["sha256"], q
+        assert readers[1].stats()["cached_frames"] == entry["stats_cache1"]["cached_frames"]
+    finally:
+        for r in readers.values():
+            r.close()
+
+
+def test_zstd_writer_roundtrip(gpu, zs, payloads):
+    data = payloads["zstd_64k_direct"]
+    w = zs.Writer(zs.ZSEEK_ZSTD, 65536, nb_workers=1)
+    for s in range(0, len(data), 65536):
+        w.write(data[s: s + 65536])
+    img = w.close()
+    with zs.Reader(img, 0) as r:
+        assert r.read_all(len(data), 0) == data
+
+
+def test_cache_lru_matches_reference(gpu, zs, ref):
+    """Frame-cache semantics (ref src/cache.c): capacity in frames, LRU
+    eviction, find promotes — cached_frames after single-frame zstd reads
+    equals the reference library's."""
+    img = golden_file("zstd_64k_direct")
+    seq = [0, 65536, 0, 131072, 200000, 0, 70000, 300000, 5, 400000]
+    for cap in (1, 2, 3):
+        ours = zs.Reader(img, cap)
+        theirs = ref.open(img, cap)
+        for off in seq:
+            a = ours.pread(100, off)
+            rb, b = theirs.pread(100, off)
+            assert a == b
+            assert ours.stats()["cached_frames"] == theirs.stats()[1]["cached_frames"]
+        ours.close()
+        theirs.close()
+
+
+@pytest.mark.parametrize("cache", [0, 1])
+def test_zstd_corrupt_frame_error_text(gpu, zs, oracle, cache):
+    """a corrupt frame: the bytes before it, then -1 with libzstd's wording
+    (the corruption is one libzstd detects, found with the oracle)"""
+    data = zs.synth_buffer(5 * 65536)
+    img = bytearray(zs.zstd_seekable(data, 65536).tobytes())
+    c_off, d_off = zs.seek_table_of(np.frombuffer(bytes(img), np.uint8))
+    f0, f1 = int(c_off[2]), int(c_off[3])
+    for pos in range(f0 + 20, f1):
+        frame = bytearray(img[f0:f1])
+        frame[pos - f0] ^= 0xFF
+        if oracle.zstd_decode(bytes(frame), 65536)[1] == 20:   # corruption_detected
+            img[pos] ^= 0xFF
+            break
+    else:
+        pytest.fail("no detectable corruption found")
+    with zs.Reader(np.frombuffer(bytes(img), np.uint8), cache) as r:
+        got = r.pread(5 * 65536, 0)
+        assert got == data[: 2 * 65536].tobytes()
+        with pytest.raises(zs.ZseekError) as e:
+            r.pread(100, 2 * 65536)
+        msg = str(e.value)
+        assert msg == ("decompress frame: " if cache else "decompress user data: ") + \
+            "Corrupted block detected"
+        # a request starting inside the corrupt frame: libzstd's streaming
+        # decoder meets the damage while discarding the prefix
+        if not cache:
+            with pytest.raises(zs.ZseekError) as e:
+                r.pread(100, 2 * 65536 + 1000)
+            assert str(e.value) == "decompress discard data: Corrupted block detected"

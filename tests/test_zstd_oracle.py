@@ -3,7 +3,6 @@ decoder, the third-party code the reference calls at decompress.c:434-538)
 against libzstd 1.4.9 itself on this host: frames compressed by libzstd with
 many parameter sets must decode to the original bytes, and corrupted frames
 must fail with the error code libzstd reports.  CPU only."""
-import ctypes as C
 import os
 
 import numpy as np
@@ -11,36 +10,15 @@ import pytest
 
 from oracle.oracle import Oracle
 
-ZSTD_SO = "/opt/conda/lib/libzstd.so.1.4.9"
-
-# ZSTD_cParameter values (zstd.h, 1.4.9)
-P_LEVEL, P_WLOG, P_HLOG, P_CLOG, P_SLOG, P_MINMATCH, P_TLEN, P_STRAT = 100, 101, 102, 103, 104, 105, 106, 107
-P_CSIZE, P_CHECKSUM = 200, 201
+from zstd_util import (P_CHECKSUM, P_CSIZE, P_LEVEL, P_MINMATCH, P_STRAT, P_WLOG, compress,
+                       compress_stream, decode, load)
 
 
 @pytest.fixture(scope="module")
 def zstd():
-    if not os.path.exists(ZSTD_SO):
+    z = load()
+    if z is None:
         pytest.skip("libzstd 1.4.9 not present")
-    z = C.CDLL(ZSTD_SO)
-    z.ZSTD_createCCtx.restype = C.c_void_p
-    z.ZSTD_CCtx_setParameter.argtypes = [C.c_void_p, C.c_int, C.c_int]
-    z.ZSTD_CCtx_setParameter.restype = C.c_size_t
-    z.ZSTD_compress2.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
-    z.ZSTD_compress2.restype = C.c_size_t
-    z.ZSTD_compressBound.argtypes = [C.c_size_t]
-    z.ZSTD_compressBound.restype = C.c_size_t
-    z.ZSTD_isError.argtypes = [C.c_size_t]
-    z.ZSTD_isError.restype = C.c_uint
-    z.ZSTD_getErrorCode.argtypes = [C.c_size_t]
-    z.ZSTD_getErrorCode.restype = C.c_int
-    z.ZSTD_freeCCtx.argtypes = [C.c_void_p]
-    z.ZSTD_createDCtx.restype = C.c_void_p
-    z.ZSTD_decompressDCtx.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
-    z.ZSTD_decompressDCtx.restype = C.c_size_t
-    z.ZSTD_CCtx_reset.argtypes = [C.c_void_p, C.c_int]
-    z.ZSTD_compressStream2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
-    z.ZSTD_compressStream2.restype = C.c_size_t
     return z
 
 
@@ -49,49 +27,12 @@ def orc():
     return Oracle()
 
 
-class _InBuf(C.Structure):
-    _fields_ = [("src", C.c_void_p), ("size", C.c_size_t), ("pos", C.c_size_t)]
+def _compress(z, data, params):
+    return compress(z, data, params)
 
 
-class _OutBuf(C.Structure):
-    _fields_ = [("dst", C.c_void_p), ("size", C.c_size_t), ("pos", C.c_size_t)]
-
-
-def compress_stream(z, data: bytes, chunk: int) -> bytes:
-    """Streaming compression without a pledged size: no content size in the
-    header, window descriptor present, blocks flushed per chunk."""
-    cctx = z.ZSTD_createCCtx()
-    out = bytearray()
-    try:
-        dst = C.create_string_buffer(1 << 20)
-        src = C.create_string_buffer(data, len(data))
-        pos = 0
-        while True:
-            end = min(len(data), pos + chunk)
-            ib = _InBuf(C.addressof(src) + pos, end - pos, 0)
-            mode = 2 if end == len(data) else 1   # ZSTD_e_end / ZSTD_e_flush
-            while True:
-                ob = _OutBuf(C.addressof(dst), len(dst), 0)
-                r = z.ZSTD_compressStream2(cctx, C.byref(ob), C.byref(ib), mode)
-                assert not z.ZSTD_isError(r)
-                out += dst.raw[: ob.pos]
-                if r == 0 and ib.pos == ib.size:
-                    break
-            pos = end
-            if end == len(data):
-                break
-        return bytes(out)
-    finally:
-        z.ZSTD_freeCCtx(cctx)
-
-
-def libzstd_decode(z, src: bytes, cap: int):
-    d = z.ZSTD_createDCtx()
-    out = C.create_string_buffer(max(cap, 1))
-    r = z.ZSTD_decompressDCtx(d, out, cap, src, len(src))
-    if z.ZSTD_isError(r):
-        return b"", z.ZSTD_getErrorCode(r)
-    return out.raw[:r], 0
+def libzstd_decode(z, src, cap):
+    return decode(z, src, cap)
 
 
 def datasets():
@@ -124,20 +65,6 @@ def test_oracle_matches_libzstd(zstd, orc, name, level):
     out, err = orc.zstd_decode(comp, len(data))
     assert err == 0
     assert out == data
-
-
-def _compress(z, data, params):
-    cctx = z.ZSTD_createCCtx()
-    try:
-        for k, v in params.items():
-            assert not z.ZSTD_isError(z.ZSTD_CCtx_setParameter(cctx, k, v))
-        cap = z.ZSTD_compressBound(len(data))
-        out = C.create_string_buffer(cap)
-        n = z.ZSTD_compress2(cctx, out, cap, data, len(data))
-        assert not z.ZSTD_isError(n)
-        return out.raw[:n]
-    finally:
-        z.ZSTD_freeCCtx(cctx)
 
 
 @pytest.mark.parametrize("name", ["synth", "text", "mixed"])
