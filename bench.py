@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "decompressed GB/s whole-node + achieved %HBM-read, LZ4 64KiB frames"
+METRIC_ZSTD = "decompressed GB/s whole-node, zstd 64KiB frames (config 5)"
 
 
 def log(*a):
@@ -50,6 +51,8 @@ def parse():
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--reassemble", type=int, default=-1, help="1/0; default on when N>1")
     p.add_argument("--profile", action="store_true", help="few steps, no extras (rocprof runs)")
+    p.add_argument("--codec", choices=["lz4", "zstd"], default="lz4",
+                   help="lz4 = config 2 (the headline metric); zstd = config 5")
     return p.parse_args()
 
 
@@ -73,7 +76,9 @@ def main():
     # ---- input: synthetic -> seekable LZ4 (the reference writer's bytes) ----
     t0 = time.time()
     data = z.synth_buffer(args.size, args.threads)
-    img = z.lz4_seekable(data, args.frame, 0, args.threads)
+    zstd = args.codec == "zstd"
+    img = (z.zstd_seekable(data, args.frame, 3, 1, args.threads) if zstd
+           else z.lz4_seekable(data, args.frame, 0, args.threads))
     c_off, d_off = z.seek_table_of(img)
     nfr = len(c_off) - 1
     batch = z.frame_batch(c_off, d_off, 0, nfr)
@@ -89,7 +94,10 @@ def main():
     torch.cuda.synchronize()
 
     def step():
-        z.decode_frames(desc, comp, out, status)
+        if zstd:
+            z.zstd_decode_frames(desc, comp, out, status)
+        else:
+            z.decode_frames(desc, comp, out, status)
 
     for _ in range(args.warmup):
         step()
@@ -160,15 +168,17 @@ def main():
     # one launch = the decode call: its kernels run back to back on the stream
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9
-    kname = z.lib().zsk_lz4_kernel_name(nfr).decode()
+    kname = "zstd_frame_kernel" if zstd else z.lib().zsk_lz4_kernel_name(nfr).decode()
     stages = None
     if n_timed:
-        names = {"plan": "lz4_plan_kernel", "parse": "lz4_scan_kernel", "execute": kname,
-                 "hand-off": "lz4_wave_kernel<4096, 4, true>"}
+        names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel",
+                  "execute": "seq_exec_kernel", "hand-off": "zstd_check_kernel"} if zstd else
+                 {"plan": "lz4_plan_kernel", "parse": "lz4_scan_kernel", "execute": kname,
+                  "hand-off": "lz4_wave_kernel<4096, 4, true>"})
         stages = {k: {"kernel": names[k], "avg_ms": round(v, 4)} for k, v in stage_ms.items()}
     value = dsum * world * args.steps / t_max / 1e9
     line = {
-        "metric": METRIC,
+        "metric": METRIC_ZSTD if zstd else METRIC,
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": world,
@@ -179,9 +189,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (SURVEY §8d generator, compressed with liblz4 1.9.3 as the reference writer does)",
-        "config": {"workload": "config2: LZ4 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
-                               "compressed image resident in HBM",
+        "data": ("synthetic (SURVEY §8d generator, compressed with libzstd 1.4.9 level 3 / strategy 1 "
+                 "as the reference writer does)" if zstd else
+                 "synthetic (SURVEY §8d generator, compressed with liblz4 1.9.3 as the reference writer does)"),
+        "config": {"workload": ("config5: zstd 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
+                                "compressed image resident in HBM" if zstd else
+                                "config2: LZ4 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
+                                "compressed image resident in HBM"),
                    "frame_bytes": args.frame, "frames_per_gpu": nfr,
                    "decoded_bytes_per_gpu": dsum, "compressed_bytes_per_gpu": comp_bytes,
                    "parallelism": f"frames sharded x{world}"},

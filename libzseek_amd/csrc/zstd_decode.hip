@@ -26,6 +26,8 @@
 // reaches the new bytes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "lz4_dev.h"
 #include "zsk_internal.h"
@@ -71,6 +73,7 @@ struct ZLds {
     int16_t norm[256];        // normalized counts
     uint8_t wts[256];         // Huffman weights
     uint32_t cnt[256];        // per-symbol next-state counters
+    uint8_t lbuf[4][256];     // decoded literals of the 4 Huffman streams, staged
     uint32_t rank[16];        // Huffman: first cell of each weight
 };
 
@@ -143,9 +146,12 @@ __device__ __forceinline__ void dma256(const In &I, uint32_t a, uint32_t dst)
     __builtin_amdgcn_global_load_lds((const void *)(I.base4 + x), la<void>(uni(dst)), 4, 0, 0);
 }
 
+// s_waitcnt vmcnt(0) through the builtin, so the compiler's wait-count pass
+// knows the LDS-DMA writes have landed and adds no waits of its own before
+// later LDS reads (expcnt / lgkmcnt fields left at their maximum)
 __device__ __forceinline__ void dma_wait()
 {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
 // forward window: 256 bytes from frame offset p (rounded down to 4); returns
@@ -175,11 +181,16 @@ __device__ __forceinline__ uint32_t win_bits(const ZLds &L, uint32_t bit, uint32
 }
 
 // ---- backward bitstreams through LDS rings ----------------------------------
+// A lane's stream bytes sit in its ring; the bits it reads next sit in a
+// 64-bit register container C, refilled 32 bits at a time: C holds stream
+// bits [pos, pos + nb), the next bit read being bit pos + nb - 1.
 struct Rd {
     uint32_t ring;   // LDS address of this lane's ring
     uint32_t x0;     // coordinate of stream byte 0
     uint32_t rlo;    // the ring holds coordinates [rlo, rlo + kRing) (rlo multiple of kSeg)
-    int32_t pos;     // bits not yet consumed; < 0 once read past the start
+    int32_t pos;     // lowest stream bit in C (< 0: zeros below the stream's start)
+    int32_t nb;      // valid bits in C
+    uint64_t C;
 };
 
 __device__ __forceinline__ uint32_t ring_dw(const Rd &r, uint32_t a)
@@ -187,7 +198,7 @@ __device__ __forceinline__ uint32_t ring_dw(const Rd &r, uint32_t a)
     return *la<uint32_t>(r.ring + (a & (kRing - 1)));
 }
 
-// n (<= 32) bits at bit lo >= 0 of the stream
+// n (1..32) stream bits at bit lo >= 0
 __device__ __forceinline__ uint32_t bits_at(const Rd &r, int32_t lo, uint32_t n)
 {
     const uint32_t b = r.x0 + ((uint32_t)lo >> 3), a = b & ~3u;
@@ -196,21 +207,40 @@ __device__ __forceinline__ uint32_t bits_at(const Rd &r, int32_t lo, uint32_t n)
     return (uint32_t)((q >> sh) & ((1ull << n) - 1));
 }
 
-__device__ __forceinline__ uint32_t rd_peek(const Rd &r, uint32_t n)
+// make C hold >= 32 bits (bits below the stream's start read as 0)
+__device__ __forceinline__ void rd_fill(Rd &r)
 {
-    const int32_t lo = r.pos - (int32_t)n;
-    if (lo >= 0)
-        return bits_at(r, lo, n);
-    if (r.pos <= 0)
-        return 0;
-    return bits_at(r, 0, (uint32_t)r.pos) << (uint32_t)(-lo);
+    if (r.nb < 32) {
+        r.pos -= 32;
+        const uint32_t v = r.pos >= 0 ? bits_at(r, r.pos, 32)
+                         : r.pos > -32 ? bits_at(r, 0, (uint32_t)(32 + r.pos)) << (uint32_t)(-r.pos)
+                                       : 0u;
+        r.C = (r.C << 32) | v;
+        r.nb += 32;
+    }
+}
+
+// the next n (<= nb) bits, not consumed
+__device__ __forceinline__ uint32_t rd_look(const Rd &r, uint32_t n)
+{
+    return (uint32_t)(r.C >> (uint32_t)(r.nb - (int32_t)n)) & (uint32_t)((1ull << n) - 1);
 }
 
 __device__ __forceinline__ uint32_t rd_read(Rd &r, uint32_t n)
 {
-    const uint32_t v = n ? rd_peek(r, n) : 0;
-    r.pos -= (int32_t)n;
+    if (n == 0)
+        return 0;
+    if (r.nb < (int32_t)n)
+        rd_fill(r);
+    const uint32_t v = rd_look(r, n);
+    r.nb -= (int32_t)n;
     return v;
+}
+
+// stream bits not consumed yet (< 0 once read past the start)
+__device__ __forceinline__ int32_t rd_left(const Rd &r)
+{
+    return r.pos + r.nb;
 }
 
 // Start one stream per active lane: [xs, xs + len) (len >= 1).  Wave-wide.
@@ -235,6 +265,8 @@ __device__ __forceinline__ bool rd_init(const In &I, Rd &r, bool act, uint32_t r
         return true;
     const uint32_t last = *la<uint8_t>(ring + ((end - 1) & (kRing - 1)));
     r.pos = last ? (int32_t)(8 * (len - 1)) + hibit(last) : 0;
+    r.nb = 0;
+    r.C = 0;
     return last != 0;
 }
 
@@ -553,6 +585,9 @@ __device__ __forceinline__ bool emit(Sink &S, uint32_t src, uint32_t lit, uint32
 // ---- literals ---------------------------------------------------------------------------
 struct Frame {
     In I;
+    uint32_t codes;    // LDS: literal-length codes [0, 36), match-length codes [36, 89)
+    bool timed;
+    uint64_t tm, t[4]; // section timers (timing builds): literals, tables, sequences, rest
     uint32_t clen;     // compressed entry bytes
     uint8_t *lit;      // literal scratch of this frame (laid out like its output)
     uint32_t cap;      // output capacity (seek-table dSize)
@@ -563,6 +598,15 @@ struct Frame {
     uint32_t tvalid;   // bit t: table t valid
     uint32_t rep0, rep1, rep2;
 };
+
+__device__ __forceinline__ void zmark(Frame &F, int i)
+{
+    if (F.timed) {
+        const uint64_t t = __builtin_readcyclecounter();
+        F.t[i] += t - F.tm;
+        F.tm = t;
+    }
+}
 
 // write bytes [p, p + n) of v (16 bytes) into the literal scratch, clamped at
 // the frame's capacity (corrupt frames may announce more literals)
@@ -599,25 +643,36 @@ __device__ __forceinline__ bool huf_streams(ZLds &L, Frame &F, uint32_t ns, uint
         return false;
     const uint32_t lg = F.huf_log;
     const uint32_t maxc = uni(__builtin_amdgcn_readlane(cnt, 0));   // stream 0 is the longest
-    u32x4 acc = (u32x4){0, 0, 0, 0};
-    for (uint32_t i = 0; i < maxc; i++) {
+    // decoded bytes go to a 256-byte LDS buffer per stream, one ds_write_b8
+    // per symbol; every 256 symbols the wave copies the buffers out (4 bytes
+    // per lane, coalesced)
+    const uint32_t lb = ldsaddr(L.lbuf[lane & 3]);
+    auto flush = [&](uint32_t i0, uint32_t m) {   // symbols [i0, i0 + m) of every stream
+        for (uint32_t k = 0; k < ns; k++) {
+            const uint32_t ck = lane_val(cnt, (int)k), dk = lane_val(dst, (int)k);
+            const uint32_t mk = ck > i0 ? (ck - i0 < m ? ck - i0 : m) : 0;
+            if (4 * lane < mk) {
+                const uint32_t v = *la<uint32_t>(ldsaddr(L.lbuf[k]) + 4 * lane);
+                lit_put(F, dk + i0 + 4 * lane, (u32x4){v, 0, 0, 0}, mk - 4 * lane < 4 ? mk - 4 * lane : 4);
+            }
+        }
+    };
+    uint32_t i = 0;
+    for (; i < maxc; i++) {
         if ((i & 63) == 0)
             rd_refill(F.I, r, act);
         if (act && i < cnt) {
-            const uint32_t e = L.huf[rd_peek(r, lg)];
-            r.pos -= (int32_t)(e >> 8);
-            const uint32_t sym = e & 0xFF, d = (i >> 2) & 3, sh = (i & 3) * 8;
-            acc.x |= d == 0 ? sym << sh : 0;
-            acc.y |= d == 1 ? sym << sh : 0;
-            acc.z |= d == 2 ? sym << sh : 0;
-            acc.w |= d == 3 ? sym << sh : 0;
-            if ((i & 15) == 15 || i + 1 == cnt) {
-                lit_put(F, dst + (i & ~15u), acc, (i & 15) + 1);
-                acc = (u32x4){0, 0, 0, 0};
-            }
+            rd_fill(r);
+            const uint32_t e = L.huf[rd_look(r, lg)];
+            r.nb -= (int32_t)(e >> 8);
+            *la<uint8_t>(lb + (i & 255)) = (uint8_t)e;
         }
+        if ((i & 255) == 255)
+            flush(i - 255, 256);
     }
-    bad = act && r.pos != 0;
+    if (maxc & 255)
+        flush(maxc & ~255u, maxc & 255);
+    bad = act && rd_left(r) != 0;
     return !__ballot(bad);
 }
 
@@ -784,7 +839,9 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p
     if (n >= kZBlockMax)
         return ZE_SRC_WRONG;
     uint32_t lused = 0, litn = 0;
+    zmark(F, 3);
     uint32_t e = literals(L, F, p, n, &lused, &litn);
+    zmark(F, 0);
     if (e)
         return e;
     uint32_t q = p + lused;
@@ -828,6 +885,7 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p
                 return err;
             q += u;
         }
+        zmark(F, 1);
         Rd r;
         const bool ok = rd_init(F.I, r, lane == 0, ldsaddr(L.ring[0]), F.I.s0 + q, qe > q ? qe - q : 1);
         if (!uni(ok && qe > q ? 1u : 0u))
@@ -840,7 +898,8 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p
             sml = rd_read(r, F.tlog[2]);
         }
         for (uint32_t i = 0; i < nseq; i++) {
-            rd_refill(F.I, r, lane == 0);
+            if ((i & 7) == 0)   // <= 8 sequences x 12 bytes < the refill margin
+                rd_refill(F.I, r, lane == 0);
             if (lane == 0 && !err) {
                 const uint32_t cll = *lp<uint32_t>(L.fse[0] + sll), cof = *lp<uint32_t>(L.fse[1] + sof),
                                cml = *lp<uint32_t>(L.fse[2] + sml);
@@ -849,7 +908,8 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p
                     err = ZE_CORRUPT;
                 } else {
                     const uint64_t ofv = (1ull << ofc) + rd_read(r, ofc);
-                    const uint32_t mlcode = c_ml[mlc], llcode = c_ll[llc];
+                    const uint32_t mlcode = *la<uint32_t>(F.codes + 4 * (36 + mlc)),
+                                   llcode = *la<uint32_t>(F.codes + 4 * llc);
                     const uint32_t ml = (mlcode & 0xFFFFFF) + rd_read(r, mlcode >> 24);
                     const uint32_t ll = (llcode & 0xFFFFFF) + rd_read(r, llcode >> 24);
                     uint64_t off;
@@ -890,10 +950,11 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p
             if (uni(err))
                 break;
         }
+        zmark(F, 2);
         err = uni(err);
         if (err)
             return err;
-        if (uni(lane == 0 && r.pos > 0 ? 1u : 0u))
+        if (uni(lane == 0 && rd_left(r) > 0 ? 1u : 0u))
             return ZE_CORRUPT;
         F.rep0 = uni(rep0);
         F.rep1 = uni(rep1);
@@ -1055,14 +1116,12 @@ __device__ __forceinline__ int32_t decode_entry(ZLds &L, Frame &F, Sink &S, uint
 // item bound per frame (lane per frame): 2 items per sequence + padding + 4 per block
 __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restrict__ desc, uint32_t n,
                                                         const uint8_t *__restrict__ comp,
-                                                        uint32_t *__restrict__ bound,
-                                                        unsigned long long *__restrict__ extent)
+                                                        uint32_t *__restrict__ bound)
 {
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
     if (f >= n)
         return;
     const FrameDesc d = desc[f];
-    atomicMax(extent, (unsigned long long)(d.d_off + d.d_size));
     const Span sp = make_span(comp + d.c_off, d.c_size);
     auto B = [&](uint32_t p) -> uint32_t {
         return p < d.c_size ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(sp.r, sp.s0 + p, 0, 0) : 0u;
@@ -1121,21 +1180,34 @@ __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restr
     bound[f] = (uint32_t)((items + 3) & ~3ull);
 }
 
-// exclusive scan of per-frame bounds -> rec_base[0..n] (one workgroup)
-__global__ __launch_bounds__(1024) void zstd_scan_kernel(const uint32_t *__restrict__ bound, uint32_t n,
+// exclusive scan of per-frame bounds -> rec_base[0..n], item total and the
+// output extent max(d_off + d_size) into host-mapped total[0..1] with plain
+// stores (one workgroup; no atomics on host memory)
+__global__ __launch_bounds__(1024) void zstd_scan_kernel(const FrameDesc *__restrict__ desc,
+                                                         const uint32_t *__restrict__ bound, uint32_t n,
                                                          uint64_t *__restrict__ rec_base,
                                                          uint64_t *__restrict__ total)
 {
     __shared__ uint64_t part[1024];
+    __shared__ uint64_t ext[1024];
     const uint32_t t = threadIdx.x;
     const uint32_t chunk = (n + 1023) / 1024;
     const uint32_t i0 = t * chunk < n ? t * chunk : n;
     const uint32_t i1 = i0 + chunk < n ? i0 + chunk : n;
-    uint64_t s = 0;
-    for (uint32_t i = i0; i < i1; i++)
+    uint64_t s = 0, e = 0;
+    for (uint32_t i = i0; i < i1; i++) {
         s += bound[i];
+        const uint64_t x = desc[i].d_off + desc[i].d_size;
+        e = x > e ? x : e;
+    }
     part[t] = s;
+    ext[t] = e;
     __syncthreads();
+    for (uint32_t d = 512; d >= 1; d >>= 1) {
+        if (t < d && ext[t + d] > ext[t])
+            ext[t] = ext[t + d];
+        __syncthreads();
+    }
     for (uint32_t d = 1; d < 1024; d <<= 1) {
         const uint64_t v = t >= d ? part[t - d] : 0;
         __syncthreads();
@@ -1149,10 +1221,14 @@ __global__ __launch_bounds__(1024) void zstd_scan_kernel(const uint32_t *__restr
     }
     if (t == 1023) {
         rec_base[n] = part[t];
-        *total = part[t];
+        total[0] = part[t];
+        total[1] = ext[0];
     }
 }
 
+__device__ unsigned long long g_ztime[4];   // timing builds: cycles per section
+
+template <bool TIMED>
 __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ lit, const uint64_t *__restrict__ rec_base, uint64_t capacity,
@@ -1160,6 +1236,10 @@ __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
     uint64_t *__restrict__ ck)
 {
     __shared__ ZLds lds[kZW];
+    __shared__ uint32_t codes[89];
+    for (uint32_t i = threadIdx.x; i < 89; i += 64 * kZW)
+        codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
+    __syncthreads();
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     const uint32_t f = uni(blockIdx.x * kZW + w);
     if (f >= n)
@@ -1167,6 +1247,10 @@ __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
     ZLds &L = lds[w];
     const FrameDesc d = desc[f];
     Frame F;
+    F.codes = ldsaddr(codes);
+    F.timed = TIMED;
+    F.t[0] = F.t[1] = F.t[2] = F.t[3] = 0;
+    F.tm = TIMED ? __builtin_readcyclecounter() : 0;
     const uintptr_t fa = reinterpret_cast<uintptr_t>(comp + d.c_off);
     F.I.base4 = reinterpret_cast<const uint8_t *>(fa & ~(uintptr_t)3);
     F.I.s0 = (uint32_t)(fa & 3);
@@ -1196,6 +1280,12 @@ __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
         status[f] = st;
         nitems[f] = S.k;
         ck[f] = c;
+    }
+    if (TIMED) {
+        zmark(F, 3);
+        if (lane == 0)
+            for (int i = 0; i < 4; i++)
+                atomicAdd(&g_ztime[i], (unsigned long long)F.t[i]);
     }
 }
 
@@ -1363,11 +1453,10 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         return 0;
     uint64_t *total_dev = nullptr;
     (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
-    s->total[1] = 0;
     hipLaunchKernelGGL(zstd_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
-                       nframes, d_comp, s->bound, (unsigned long long *)(total_dev + 1));
-    hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, s->bound, nframes, s->rec_base,
-                       total_dev);
+                       nframes, d_comp, s->bound);
+    hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, s->bound, nframes,
+                       s->rec_base, total_dev);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1376,15 +1465,31 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL(zstd_frame_kernel, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0, stream,
-                       d_desc, nframes, d_comp, s->lit, s->rec_base, s->items_cap, s->items, s->nitems,
-                       d_status, s->ck);
-    if (launch_seq_exec_lit(d_desc, nframes, s->lit, d_out, s->rec_base, s->items, s->nitems, d_status,
-                            stream) != 0)
-        return -1;
+    static const bool timed = getenv("ZSEEK_ZSTD_TIMING") != nullptr;
+    if (timed) {
+        unsigned long long z[4] = {0, 0, 0, 0};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ztime), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(zstd_frame_kernel<true>, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0,
+                           stream, d_desc, nframes, d_comp, s->lit, s->rec_base, s->items_cap, s->items,
+                           s->nitems, d_status, s->ck);
+        (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_ztime), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        const double t = (double)(z[0] + z[1] + z[2] + z[3]);
+        fprintf(stderr, "zstd frame kernel (wave cycles): literals %.1f%%  tables %.1f%%  sequences %.1f%%  rest %.1f%%  total %.3g\n",
+                100 * z[0] / t, 100 * z[1] / t, 100 * z[2] / t, 100 * z[3] / t, t);
+    } else {
+        hipLaunchKernelGGL(zstd_frame_kernel<false>, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0,
+                           stream, d_desc, nframes, d_comp, s->lit, s->rec_base, s->items_cap, s->items,
+                           s->nitems, d_status, s->ck);
+    }
+    stage_mark(2, stream);
+    const int rc = launch_seq_exec_lit(d_desc, nframes, s->lit, d_out, s->rec_base, s->items,
+                                       s->nitems, d_status, stream);
+    stage_mark(3, stream);
     hipLaunchKernelGGL(zstd_check_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes,
                        d_out, s->ck, d_status);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    stage_mark(4, stream);
+    return rc == 0 && hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // Plan, wait for the item total and output extent (host-mapped), size the
@@ -1397,8 +1502,10 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         return 0;
     if (zstd_scratch_reserve(s, nframes, 0, 0, stream) != 0)
         return -1;
+    stage_mark(0, stream);
     if (launch_zstd_plan(d_desc, nframes, d_comp, s, stream) != 0)
         return -1;
+    stage_mark(1, stream);
     if (hipStreamSynchronize(stream) != hipSuccess)
         return -1;
     if (zstd_scratch_reserve(s, nframes, s->total[1], s->total[0], stream) != 0)

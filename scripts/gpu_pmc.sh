@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 V=${VARIANTS:-0}
-K="python scripts/kbench.py --size 1073741824 --variants $V --rounds 1 --reps 1"
+K=${PMC_CMD:-"python scripts/kbench.py --size 1073741824 --variants $V --rounds 1 --reps 1"}
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
            "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
