@@ -227,7 +227,79 @@ __device__ __forceinline__ int32_t hdr_status(Scan &L)
 // ---- fast path: one whole sequence (the common case) -------------------------
 // Leaves anything it cannot finish (bytes not in the ring yet, longer
 // extensions, errors) in its phase for a later sub-step or the slow step.
+// Branch-free: both halves (token, offset) are evaluated on every lane and
+// committed under predicates — with one wave per SIMD, the exec-mask chains
+// of an if/return version cost more than the selects.
 __device__ __forceinline__ void fast(Scan &L)
+{
+    const bool en = L.k == L.ks && L.ph <= P_OFF;   // queue empty: items go to q0..q2
+    const bool in_tok = L.ph == P_TOKEN;
+    // token: literal length with at most one extension byte
+    const uint32_t ip = L.ip, rem = L.iend - ip;
+    const uint32_t w = r4(L, ip);
+    const uint32_t tok = w & 0xFF, e = (w >> 8) & 0xFF;
+    const bool lext = (tok >> 4) == 15;
+    const uint32_t lit = lext ? 15 + e : tok >> 4;
+    const uint32_t p = ip + (lext ? 2 : 1);
+    const bool tok_ok = ip < L.iend && L.cx0 + ip + (rem < 2 ? 1 : 2) <= L.avail &&
+                        !(lext && (e == 255 || rem - 1 <= 15));
+    // the block's last sequence: literals only, ending the block
+    const bool last = L.op + lit > L.oend - kMfLimit || L.iend - p < lit + 2 + 1 + kLastLiterals;
+    const bool last_ok = en && in_tok && tok_ok && last && L.iend - p == lit && L.op + lit <= L.oend &&
+                         L.op + lit <= L.dlen;
+    const bool t_ok = en && in_tok && tok_ok && !last && L.op + lit <= L.dlen;
+    // offset + match length with at most one extension byte (after the token
+    // just parsed, or the pending one)
+    const uint32_t q = in_tok ? p + lit : ip;
+    const uint32_t ctok = in_tok ? tok : L.tok;
+    const uint32_t clsrc = in_tok ? p : L.lsrc;
+    const uint32_t cnlit = in_tok ? lit : L.nlit;
+    const uint32_t cop = in_tok ? L.op + lit : L.op;
+    const uint32_t o4 = r4(L, q);
+    const uint32_t off = o4 & 0xFFFF, e2 = (o4 >> 16) & 0xFF;
+    const bool mext = (ctok & 15) == 15;
+    const uint32_t p2 = q + (mext ? 3 : 2);
+    const uint32_t ml = (mext ? 15 + e2 : ctok & 15) + kMinMatch;
+    const bool o_ok = (in_tok ? t_ok : en) && L.cx0 + q + 3 <= L.avail &&
+                      !(mext && (q + 2 >= L.iend || e2 == 255 || p2 >= L.iend - (kLastLiterals - 1))) &&
+                      off != 0 && off <= cop - L.floor_ && cop + ml <= L.oend - kLastLiterals &&
+                      cop + ml <= L.dlen;
+    // one sequence to emit (a match, or the literals-only last one)
+    const bool em = o_ok || last_ok;
+    const uint32_t esrc = o_ok ? clsrc : p, elit = o_ok ? cnlit : lit;
+    const uint32_t eoff = o_ok ? off : 0, eml = o_ok ? ml : 0;
+    const bool big = elit > 255 || eml > 258;
+    const uint32_t pad = big && (L.k & 63) == 63 ? 1 : 0;
+    const uint32_t nk = big ? 2 + pad : 1;
+    const bool fits = L.k + nk <= L.cap;
+    const uint32_t xa = esrc | kItemExt;
+    const uint32_t small_b = eoff | (elit << 16) | ((eml ? eml - 3 : 0) << 24);
+    const bool put = em && fits;
+    L.q0a = put ? (big ? (pad ? 0 : xa) : esrc) : L.q0a;
+    L.q0b = put ? (big ? (pad ? 0 : eoff) : small_b) : L.q0b;
+    L.q1a = put ? (pad ? xa : elit) : L.q1a;
+    L.q1b = put ? (pad ? eoff : eml) : L.q1b;
+    L.q2a = put ? elit : L.q2a;
+    L.q2b = put ? eml : L.q2b;
+    L.k = put ? L.k + nk : L.k;
+    // state: offset done > token done (offset waits) > last sequence
+    const uint32_t nip = o_ok ? p2 : (last_ok ? L.iend : (t_ok ? p + lit : L.ip));
+    const uint32_t nop = o_ok ? cop + ml : (last_ok || t_ok ? L.op + lit : L.op);
+    const uint32_t nph = o_ok ? P_TOKEN : (last_ok ? P_BHDR : (t_ok ? P_OFF : L.ph));
+    L.tok = t_ok ? tok : L.tok;
+    L.lsrc = t_ok ? p : L.lsrc;
+    L.nlit = t_ok ? lit : L.nlit;
+    L.ip = nip;
+    L.op = nop;
+    L.ph = nph;
+    if (em && !fits)
+        finish(L, ST_NOT_RUN);
+}
+
+// ---- the if/return form of fast() (A/B builds: scan version 1) ---------------
+// Leaves anything it cannot finish (bytes not in the ring yet, longer
+// extensions, errors) in its phase for a later sub-step or the slow step.
+__device__ __forceinline__ void fast_br(Scan &L)
 {
     if (L.k != L.ks)
         return;
@@ -467,7 +539,7 @@ __device__ __forceinline__ void slow(Scan &L)
 // One sub-step with pipeline slot S: retire S into the ring, parse, store one
 // queued item, issue S's next load.  Returns true when the stream jumped (the
 // caller drops the other slots' loads).
-template <bool SLOW>
+template <bool SLOW, bool BR>
 __device__ __forceinline__ bool sub(Scan &L, Fill &S)
 {
     if (S.x != kOff) {
@@ -476,8 +548,12 @@ __device__ __forceinline__ bool sub(Scan &L, Fill &S)
         lds_w128(raddr(L, S.x + 16), S.b);
         L.avail = S.x + 32;
     }
-    if (L.ph <= P_OFF)
+    if (BR) {
+        if (L.ph <= P_OFF)
+            fast_br(L);
+    } else {
         fast(L);
+    }
     if (SLOW && L.ph != P_DONE)
         slow(L);
     // one item store
@@ -519,6 +595,7 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v)
     return ((uint64_t)hi << 32) | lo;
 }
 
+template <bool BR>
 __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))) void lz4_scan_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
@@ -592,7 +669,7 @@ __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))
     for (;;) {
 #pragma unroll
         for (int i = 0; i < (int)kD; i++) {
-            const bool jumped = i == 0 ? sub<true>(L, sl[i]) : sub<false>(L, sl[i]);
+            const bool jumped = i == 0 ? sub<true, BR>(L, sl[i]) : sub<false, BR>(L, sl[i]);
             // a jump restarted the stream: drop the other slots' loads
             if (jumped) {
 #pragma unroll
@@ -620,13 +697,18 @@ __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))
 
 int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items,
-                    uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
+                    uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
+                    int version)
 {
     if (nframes == 0)
         return 0;
     const uint32_t per = 64 * kSW;
-    hipLaunchKernelGGL(lz4_scan_kernel, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                       nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at);
+    if (version == 1)
+        hipLaunchKernelGGL(lz4_scan_kernel<true>, dim3((nframes + per - 1) / per), dim3(per), 0, stream,
+                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at);
+    else
+        hipLaunchKernelGGL(lz4_scan_kernel<false>, dim3((nframes + per - 1) / per), dim3(per), 0, stream,
+                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -821,19 +821,20 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     stage_mark(1, stream);
     // diag (tuning builds): 0x800 = the first-generation parse kernel,
     // 0x1000 = the first-generation execute kernel (low bits: its variants),
-    // 0x200/0x201 = LDS-ring staged execute v1/v2, 0x203..0x208 = seq_exec
+    // 0x400 = the scan's if/return fast path,
+    // 0x200/0x201 = LDS-ring staged execute v1/v2, 0x203..0x20A = seq_exec
     // versions; 0 = the production pair lz4_scan_kernel + seq_exec v4
     const bool old_parse = (diag & 0x800) != 0, old_exec = (diag & 0x1000) != 0;
     const int xd = diag & 0x3FF;
     if ((stages & 2) && !old_parse)
         launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                        s->nitems, d_status, d_fail_at, stream);
+                        s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0);
     else if (stages & 2)
         hipLaunchKernelGGL(lz4_parse_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                            s->nitems, d_status, d_fail_at);
     stage_mark(2, stream);
-    if ((stages & 4) && !old_exec && xd >= 0x203 && xd <= 0x208) {
+    if ((stages & 4) && !old_exec && xd >= 0x203 && xd <= 0x20A) {
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
                         stream, xd & 0xF);
     } else if ((stages & 4) && !old_exec && (xd == 0x200 || xd == 0x201)) {

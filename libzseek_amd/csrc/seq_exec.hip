@@ -44,10 +44,11 @@ using namespace lz4d;
 constexpr uint32_t kItemExt = 0x80000000u;
 constexpr uint32_t kItemPos = 0x3FFFFFFFu;
 constexpr uint32_t kXW = 4;                 // waves (frames) per workgroup
-constexpr uint32_t kXOut = 4096;            // output bytes staged per batch at most
-constexpr uint32_t kXBuf = kXOut + 80;      // stage bytes per wave (2 kept chunks + read slack)
-constexpr uint32_t kXPieces = kXOut / 16 + 2 * 64;   // pieces of a batch at most
-constexpr uint32_t kXWave = kXBuf + 8 * kXPieces;    // stage + piece descriptors
+// per wave, for OUTB output bytes staged per batch at most: the stage (2 kept
+// chunks + read slack) and the piece descriptors (one per 16-byte piece)
+constexpr uint32_t x_buf(uint32_t outb) { return outb + 80; }
+constexpr uint32_t x_pieces(uint32_t outb) { return outb / 16 + 2 * 64; }
+constexpr uint32_t x_wave(uint32_t outb) { return x_buf(outb) + 8 * x_pieces(outb); }
 constexpr uint32_t kBad = 0x80000000u;      // buffer offset past any range: load returns 0
 
 typedef u32x4 u32x4_l __attribute__((aligned(1)));
@@ -347,14 +348,14 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 }
 
 // DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores
-template <bool DIST, int DIAG>
+template <bool DIST, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     const int32_t *__restrict__ status, const uint8_t *__restrict__ lit)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * kXWave];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * x_wave(OUTB)];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t f = uni(blockIdx.x * kXW + w);
@@ -374,8 +375,8 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const Span lsp = lit ? make_span(lit + d.d_off, (uint64_t)d.d_size + 16)
                          : make_span(comp + d.c_off, d.c_size);
     Stage S;
-    S.base = (uint32_t)(uintptr_t)(lds + w * kXWave);
-    const uint32_t descs = S.base + kXBuf;
+    S.base = (uint32_t)(uintptr_t)(lds + w * x_wave(OUTB));
+    const uint32_t descs = S.base + x_buf(OUTB);
     S.a0 = (uint32_t)(reinterpret_cast<uintptr_t>(O.o) & 15);
     S.cb = 0xFFFFFFFFu;      // chunk -1 at index 0: chunk 0 starts at index 16
     uint32_t produced = 0;   // frame bytes decoded
@@ -411,11 +412,11 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
                 ml = mc ? mc + 3 : 0;
             }
         }
-        // batch = the lanes before the first whose output would pass kXOut;
+        // batch = the lanes before the first whose output would pass OUTB;
         // an extended item keeps its second half
         const uint32_t len = lit + ml;
         const uint32_t inc = wave_incl_add(len);
-        const uint64_t over = __ballot(act0 && inc > kXOut);
+        const uint64_t over = __ballot(act0 && inc > OUTB);
         uint32_t nb = over ? (uint32_t)__builtin_ctzll(over) : 64;
         if (nb == 64 && (lane_val(w0, 63) & kItemExt))
             nb = 63;
@@ -564,14 +565,17 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     if (nframes == 0)
         return 0;
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
-#define ZSK_X(D, G)                                                                            \
-    hipLaunchKernelGGL((seq_exec_kernel<D, G>), grid, block, 0, stream, d_desc, nframes, d_comp, \
+#define ZSK_X(D, G)   ZSK_XB(D, G, 4096)
+#define ZSK_XB(D, G, B)                                                                        \
+    hipLaunchKernelGGL((seq_exec_kernel<D, G, B>), grid, block, 0, stream, d_desc, nframes, d_comp, \
                        d_out, rec_base, items, nitems, d_status, nullptr)
     switch (version) {
     case 3: ZSK_X(false, 0); break;
     case 5: ZSK_X(true, 1); break;
     case 6: ZSK_X(true, 2); break;
     case 7: ZSK_X(true, 3); break;
+    case 9: ZSK_XB(true, 0, 3072); break;
+    case 10: ZSK_XB(true, 0, 2048); break;
     case 8: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
@@ -589,6 +593,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     default: ZSK_X(true, 0); break;
     }
 #undef ZSK_X
+#undef ZSK_XB
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -598,7 +603,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<true, 0>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<true, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -144,7 +144,8 @@ struct ZstdScratch {
     uint64_t *ck = nullptr;        // per-frame checksum request
     uint8_t *lit = nullptr;        // literal scratch (output-sized + 64)
     uint64_t *items = nullptr;
-    uint64_t *total = nullptr;     // host-mapped: [0] item total, [1] output extent of the last plan
+    uint64_t *d_total = nullptr;   // [0] item total, [1] output extent of the last plan
+    uint64_t *total = nullptr;     // pinned host copy of d_total
     uint32_t frames_cap = 0;
     uint64_t lit_cap = 0, items_cap = 0;
 };
@@ -160,10 +161,11 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream);
 
 // Parse phase, streaming lane-per-frame (lz4_scan.hip): same outputs as
-// lz4_parse_kernel.
+// lz4_parse_kernel.  version 1 = the if/return fast path (A/B builds).
 int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items,
-                    uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream);
+                    uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
+                    int version = 0);
 
 // Lane-per-frame decoder (lz4_lane.hip) + hand-offs to the wave kernel.
 int launch_lz4_lane(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,

@@ -1181,8 +1181,8 @@ __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restr
 }
 
 // exclusive scan of per-frame bounds -> rec_base[0..n], item total and the
-// output extent max(d_off + d_size) into host-mapped total[0..1] with plain
-// stores (one workgroup; no atomics on host memory)
+// output extent max(d_off + d_size) into total[0..1] (device memory, copied
+// to the host by the launcher; one workgroup)
 __global__ __launch_bounds__(1024) void zstd_scan_kernel(const FrameDesc *__restrict__ desc,
                                                          const uint32_t *__restrict__ bound, uint32_t n,
                                                          uint64_t *__restrict__ rec_base,
@@ -1231,9 +1231,9 @@ __device__ unsigned long long g_ztime[4];   // timing builds: cycles per section
 template <bool TIMED>
 __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
-    uint8_t *__restrict__ lit, const uint64_t *__restrict__ rec_base, uint64_t capacity,
-    uint64_t *__restrict__ items, uint32_t *__restrict__ nitems, int32_t *__restrict__ status,
-    uint64_t *__restrict__ ck)
+    uint8_t *__restrict__ lit, uint64_t lit_cap, const uint64_t *__restrict__ rec_base,
+    uint64_t capacity, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
+    int32_t *__restrict__ status, uint64_t *__restrict__ ck)
 {
     __shared__ ZLds lds[kZW];
     __shared__ uint32_t codes[89];
@@ -1272,7 +1272,10 @@ __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
     S.cap = (uint32_t)(rec_base[f + 1] - rb);
     uint64_t c = 0;
     int32_t st;
-    if (rec_base[f + 1] > capacity || d.c_size >= 0x7FFFFF00u)
+    // scratch sized by the plan: a frame that would not fit is refused, never
+    // written out of bounds
+    if (rec_base[f + 1] > capacity || d.c_size >= 0x7FFFFF00u ||
+        d.d_off + (uint64_t)d.d_size + 16 > lit_cap)
         st = zerr(ZE_GENERIC);
     else
         st = decode_entry(L, F, S, d.c_size, &c);
@@ -1399,7 +1402,8 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
             hipMalloc((void **)&s->rec_base, sizeof(uint64_t) * (cap + 1)) != hipSuccess ||
             hipMalloc((void **)&s->nitems, sizeof(uint32_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->ck, sizeof(uint64_t) * cap) != hipSuccess ||
-            hipHostMalloc((void **)&s->total, 2 * sizeof(uint64_t), hipHostMallocMapped) != hipSuccess)
+            hipMalloc((void **)&s->d_total, 2 * sizeof(uint64_t)) != hipSuccess ||
+            hipHostMalloc((void **)&s->total, 2 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
             return -1;
         s->total[0] = s->total[1] = 0;
         s->frames_cap = cap;
@@ -1439,25 +1443,30 @@ void zstd_scratch_free(ZstdScratch *s)
         (void)hipFree(s->lit);
     if (s->items)
         (void)hipFree(s->items);
+    if (s->d_total)
+        (void)hipFree(s->d_total);
     if (s->total)
         (void)hipHostFree(s->total);
     *s = ZstdScratch();
 }
 
-// Plan only: bounds + offsets; *s->total (host-mapped) holds the item total
-// once the stream reaches it.
+// Plan only: bounds + offsets, then the item total and output extent copied
+// into s->total (pinned host memory), valid once the stream reaches it.
 int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      ZstdScratch *s, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
-    uint64_t *total_dev = nullptr;
-    (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
     hipLaunchKernelGGL(zstd_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
                        nframes, d_comp, s->bound);
     hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, s->bound, nframes,
-                       s->rec_base, total_dev);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+                       s->rec_base, s->d_total);
+    if (hipGetLastError() != hipSuccess)
+        return -1;
+    return hipMemcpyAsync(s->total, s->d_total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) ==
+                   hipSuccess
+               ? 0
+               : -1;
 }
 
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
@@ -1470,7 +1479,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         unsigned long long z[4] = {0, 0, 0, 0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ztime), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
         hipLaunchKernelGGL(zstd_frame_kernel<true>, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0,
-                           stream, d_desc, nframes, d_comp, s->lit, s->rec_base, s->items_cap, s->items,
+                           stream, d_desc, nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->items,
                            s->nitems, d_status, s->ck);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_ztime), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
@@ -1479,7 +1488,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                 100 * z[0] / t, 100 * z[1] / t, 100 * z[2] / t, 100 * z[3] / t, t);
     } else {
         hipLaunchKernelGGL(zstd_frame_kernel<false>, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0,
-                           stream, d_desc, nframes, d_comp, s->lit, s->rec_base, s->items_cap, s->items,
+                           stream, d_desc, nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->items,
                            s->nitems, d_status, s->ck);
     }
     stage_mark(2, stream);
@@ -1492,7 +1501,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     return rc == 0 && hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Plan, wait for the item total and output extent (host-mapped), size the
+// Plan, wait for the item total and output extent, size the
 // scratch, decode.  The one synchronization point of the zstd path: the item
 // slots of a frame are only known once its sequence counts are read.
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
