@@ -133,6 +133,29 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t v)
     return x;
 }
 
+// Order LDS writes of some lanes before LDS reads of others in the same
+// wave.  The hardware already does (a wave's DS ops execute in order; no
+// instruction is emitted), but the compiler treats lanes as threads: without
+// a fence it may forward a lane's own earlier store to a load of a location
+// another lane wrote meanwhile.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+
+// inclusive prefix max over the wave (0 is the identity)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
+{
+    uint32_t x = v;
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return x;
+}
+
 __device__ __forceinline__ uint32_t lane_val(uint32_t v, int l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);

@@ -834,7 +834,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                            d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                            s->nitems, d_status, d_fail_at);
     stage_mark(2, stream);
-    if ((stages & 4) && !old_exec && xd >= 0x203 && xd <= 0x20A) {
+    if ((stages & 4) && !old_exec && xd >= 0x203 && xd <= 0x20B) {
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
                         stream, xd & 0xF);
     } else if ((stages & 4) && !old_exec && (xd == 0x200 || xd == 0x201)) {

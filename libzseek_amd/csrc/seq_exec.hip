@@ -48,7 +48,15 @@ constexpr uint32_t kXW = 4;                 // waves (frames) per workgroup
 // chunks + read slack) and the piece descriptors (one per 16-byte piece)
 constexpr uint32_t x_buf(uint32_t outb) { return outb + 80; }
 constexpr uint32_t x_pieces(uint32_t outb) { return outb / 16 + 2 * 64; }
-constexpr uint32_t x_wave(uint32_t outb) { return x_buf(outb) + 8 * x_pieces(outb); }
+// after the stage: piece descriptors (copy_desc, 8 B per piece) or the run
+// table + piece owners (copy_scan, 32 B per lane + 4 B per piece)
+constexpr uint32_t kXOwn = 6;   // piece owners per lane in the blocked scan
+constexpr uint32_t x_wave(uint32_t outb)
+{
+    return x_buf(outb) + (8 * x_pieces(outb) > 32 * 64 + 4 * 64 * kXOwn ? 8 * x_pieces(outb)
+                                                                        : 32 * 64 + 4 * 64 * kXOwn);
+}
+static_assert(x_pieces(4096) <= 64 * kXOwn, "piece owners");
 constexpr uint32_t kBad = 0x80000000u;      // buffer offset past any range: load returns 0
 
 typedef u32x4 u32x4_l __attribute__((aligned(1)));
@@ -209,6 +217,7 @@ __device__ __forceinline__ void copy_desc(const Stage &S, const Out &O, const Sp
                 ((uint64_t)(da | (n < 16 ? n : 16) << 16 | kind << 24) << 32) | sx;
         }
     }
+    wave_lds_sync();
     for (uint32_t t0 = 0; t0 < T; t0 += 256) {
         u32x4 vl[4], vm[4];
         uint32_t dw[4], sx[4];
@@ -233,6 +242,84 @@ __device__ __forceinline__ void copy_desc(const Stage &S, const Out &O, const Sp
                 if ((dw[j] >> 24) == K_STAGE)
                     v = lds16(saddr(S, sx[j]));
                 lds_put(S.base + (dw[j] & 0xFFFF), v, n);
+            }
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+    }
+}
+
+// copy_desc with piece-parallel descriptors: instead of each lane looping
+// over its own pieces (as many steps as the batch's longest run), each lane
+// writes its two runs to a table, marks its first piece in an owner array,
+// and one blocked prefix max over the array gives every piece slot its
+// owning lane; a slot then reads its run from the table.  Same loads, same
+// writes, same order as copy_desc.
+template <int DIAG>
+__device__ __forceinline__ void copy_scan(const Stage &S, const Out &O, const Span &lsp,
+                                          uint32_t tab, uint32_t flushed, uint32_t lane,
+                                          uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
+                                          uint32_t mb, uint32_t mn)
+{
+    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
+    const uint32_t inc = wave_incl_add(np);
+    const uint32_t T = lane_val(inc, 63);
+    if (T == 0)
+        return;
+    const uint32_t x = inc - np;
+    const uint32_t own = tab + 32 * 64;   // owner + 1 of piece t at own + 4 t
+    *lp<u32x4>(tab + 32 * lane) = (u32x4){src, op, lit, x};
+    *lp<u32x4>(tab + 32 * lane + 16) = (u32x4){msrc, mb, mn, lpn};
+    const uint32_t ob = own + 4 * kXOwn * lane;   // this lane's block of owners
+    // one access type for the owner array (uint32_t): a mixed-width
+    // access would let the compiler forward the cleared value past the marks
+#pragma unroll
+    for (uint32_t k = 0; k < kXOwn; k++)
+        *lp<uint32_t>(ob + 4 * k) = 0;
+    if (np)
+        *lp<uint32_t>(own + 4 * x) = lane + 1;
+    wave_lds_sync();
+    uint32_t o[kXOwn];
+#pragma unroll
+    for (uint32_t k = 0; k < kXOwn; k++)
+        o[k] = *lp<uint32_t>(ob + 4 * k);
+#pragma unroll
+    for (uint32_t k = 1; k < kXOwn; k++)
+        o[k] = max(o[k], o[k - 1]);
+    const uint32_t carry = dpp_prev(wave_incl_max(o[kXOwn - 1]), 0);
+#pragma unroll
+    for (uint32_t k = 0; k < kXOwn; k++)
+        *lp<uint32_t>(ob + 4 * k) = max(o[k], carry);
+    wave_lds_sync();
+    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
+        u32x4 vl[4], vm[4];
+        uint32_t da[4], sx[4], nn[4], kd[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t t = t0 + 64 * j + lane;
+            const bool on = t < T;
+            const uint32_t r = on ? *lp<uint32_t>(own + 4 * t) - 1 : 0;
+            const u32x4 e0 = *lp<u32x4>(tab + 32 * r), e1 = *lp<u32x4>(tab + 32 * r + 16);
+            const uint32_t i = t - e0.w;
+            const bool isl = i < e1.w;
+            const uint32_t n = isl ? e0.z : e1.z;
+            const uint32_t po = piece_off(n, isl ? i : i - e1.w);
+            sx[j] = (isl ? e0.x : e1.x) + po;
+            da[j] = saddr(S, (isl ? e0.y : e1.y) + po);
+            nn[j] = on ? (n < 16 ? n : 16) : 0;
+            kd[j] = isl ? K_LIT : (sx[j] + 16 <= flushed ? K_HBM : K_STAGE);
+            vl[j] = bload16(lsp.r, on && kd[j] == K_LIT && !(DIAG & 1) ? lsp.s0 + sx[j] : kBad);
+            vm[j] = bload16(O.sp.r, on && kd[j] == K_HBM && !(DIAG & 1) ? O.sp.s0 + sx[j] : kBad);
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (nn[j]) {
+                u32x4 v = vl[j] | vm[j];   // the disabled load returned zeros
+                if (kd[j] == K_STAGE)
+                    v = lds16(saddr(S, sx[j]));
+                lds_put(da[j], v, nn[j]);
             }
             if (t0 + 64 * j + 64 >= T)
                 break;
@@ -348,7 +435,10 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 }
 
 // DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores
-template <bool DIST, int DIAG, uint32_t OUTB>
+// MODE: 0 = lane-owned copies and frontier readiness (v3), 1 = piece
+// descriptors (v4), 2 = piece-parallel descriptors (v5); 1 and 2 use exact
+// readiness
+template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
@@ -477,10 +567,13 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if (DIST)
+        if (MODE == 2)
+            copy_scan<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
+        else if (MODE == 1)
             copy_desc<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
         else
             copy_own(S, O, lsp, flushed, src, op, lit, msrc, mb, early ? ml : 0);
+        wave_lds_sync();   // stage bytes of other lanes from here on
         ZSK_T(1)
         // rounds: matches reading bytes of this batch
         uint64_t pending = __ballot(ml != 0 && !early);
@@ -495,7 +588,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         while (pending) {
             const bool mine = (pending >> lane) & 1;
             bool ready;
-            if (DIST) {
+            if (MODE != 0) {
                 // blocked while the source meets a lower pending match's destination
                 bool blocked = false;
                 uint64_t pj = pending;
@@ -515,11 +608,12 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
             }
             if (ready && overlap)
                 copy_overlap(S, O, flushed, mb, off, ml);
-            if (DIST)
+            if (MODE != 0)
                 copy_round(S, O, flushed, msrc, mb, ready && !overlap ? ml : 0);
             else
                 copy_own(S, O, lsp, flushed, 0, 0, 0, msrc, mb, ready && !overlap ? ml : 0);
             pending &= ~__ballot(ready);
+            wave_lds_sync();
             if (DIAG & 16)
                 cnt[5] += 1;
         }
@@ -532,6 +626,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
                 flush_chunk(S, O, c);
         fc = end_c;
         // keep chunks fc-1 (flushed) and fc (partial) at stage index 0
+        wave_lds_sync();
         if (!last && fc - 1 != S.cb) {
             u32x4 v;
             if (lane < 2)
@@ -540,6 +635,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
                 *lp<u32x4>(S.base + 16 * lane) = v;
             S.cb = fc - 1;
         }
+        wave_lds_sync();
         b += nb;
         const uint64_t a = __shfl_down(cur, nb & 63, 64);
         const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
@@ -570,16 +666,17 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     hipLaunchKernelGGL((seq_exec_kernel<D, G, B>), grid, block, 0, stream, d_desc, nframes, d_comp, \
                        d_out, rec_base, items, nitems, d_status, nullptr)
     switch (version) {
-    case 3: ZSK_X(false, 0); break;
-    case 5: ZSK_X(true, 1); break;
-    case 6: ZSK_X(true, 2); break;
-    case 7: ZSK_X(true, 3); break;
-    case 9: ZSK_XB(true, 0, 3072); break;
-    case 10: ZSK_XB(true, 0, 2048); break;
+    case 3: ZSK_X(0, 0); break;
+    case 5: ZSK_X(1, 1); break;
+    case 6: ZSK_X(1, 2); break;
+    case 7: ZSK_X(1, 3); break;
+    case 9: ZSK_XB(1, 0, 3072); break;
+    case 10: ZSK_XB(1, 0, 2048); break;
+    case 11: ZSK_X(2, 0); break;
     case 8: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
-        ZSK_X(true, 16);
+        ZSK_X(1, 16);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_xstats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
         const double t = (double)(z[0] + z[1] + z[2] + z[3]);
@@ -590,7 +687,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                 z[8] / nb, z[5] / nb, z[6] / nb, z[7] / nb, z[9] / nb);
         break;
     }
-    default: ZSK_X(true, 0); break;
+    default: ZSK_X(1, 0); break;
     }
 #undef ZSK_X
 #undef ZSK_XB
@@ -603,7 +700,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<true, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<1, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

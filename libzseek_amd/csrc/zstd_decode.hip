@@ -152,6 +152,7 @@ __device__ __forceinline__ void dma256(const In &I, uint32_t a, uint32_t dst)
 __device__ __forceinline__ void dma_wait()
 {
     __builtin_amdgcn_s_waitcnt(0x0F70);
+    wave_lds_sync();
 }
 
 // forward window: 256 bytes from frame offset p (rounded down to 4); returns
@@ -374,6 +375,7 @@ __device__ __forceinline__ void fse_build(ZLds &L, uint32_t *tab, uint32_t nsym,
 {
     const uint32_t lane = lane_id();
     const uint32_t size = 1u << tl, mask = size - 1;
+    wave_lds_sync();   // norm[] from lane 0
     if (lane == 0) {
         uint32_t high = size - 1;
         for (uint32_t s = 0; s < nsym; s++)
@@ -392,6 +394,7 @@ __device__ __forceinline__ void fse_build(ZLds &L, uint32_t *tab, uint32_t nsym,
     }
     for (uint32_t s = lane; s < nsym; s += 64)
         L.cnt[s] = L.norm[s] == -1 ? 1u : (uint32_t)L.norm[s];
+    wave_lds_sync();
     for (uint32_t u0 = 0; u0 < size; u0 += 64) {
         const uint32_t u = u0 + lane;
         const bool act = u < size;
@@ -408,6 +411,7 @@ __device__ __forceinline__ void fse_build(ZLds &L, uint32_t *tab, uint32_t nsym,
             }
             if (lane == 0)
                 L.cnt[sj] = base + (uint32_t)__builtin_popcountll(m);
+            wave_lds_sync();
             rem &= ~m;
         }
     }
@@ -523,6 +527,7 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
     const uint32_t lastw = (uint32_t)hibit(rest) + 1;
     if (lane == 0)
         L.wts[nw] = (uint8_t)lastw;
+    wave_lds_sync();
     r1 += lastw == 1;
     if (r1 < 2 || (r1 & 1))
         return 0;
@@ -540,6 +545,7 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
             acc += cntw[k] << (k - 1);
         }
     }
+    wave_lds_sync();
     // cells: symbols in order, each takes 2^(w-1) cells of its class
     for (uint32_t s = 0; s < nw; s++) {
         const uint32_t w = uni(L.wts[s]);
@@ -552,6 +558,7 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
             L.huf[c0 + c] = e;
         if (lane == 0)
             L.rank[w] = c0 + len;
+        wave_lds_sync();
     }
     *log = lg;
     return used;
@@ -648,6 +655,7 @@ __device__ __forceinline__ bool huf_streams(ZLds &L, Frame &F, uint32_t ns, uint
     // per lane, coalesced)
     const uint32_t lb = ldsaddr(L.lbuf[lane & 3]);
     auto flush = [&](uint32_t i0, uint32_t m) {   // symbols [i0, i0 + m) of every stream
+        wave_lds_sync();   // lbuf[k] written by lane k, read by all
         for (uint32_t k = 0; k < ns; k++) {
             const uint32_t ck = lane_val(cnt, (int)k), dk = lane_val(dst, (int)k);
             const uint32_t mk = ck > i0 ? (ck - i0 < m ? ck - i0 : m) : 0;
@@ -656,6 +664,7 @@ __device__ __forceinline__ bool huf_streams(ZLds &L, Frame &F, uint32_t ns, uint
                 lit_put(F, dk + i0 + 4 * lane, (u32x4){v, 0, 0, 0}, mk - 4 * lane < 4 ? mk - 4 * lane : 4);
             }
         }
+        wave_lds_sync();   // before lane k writes lbuf[k] again
     };
     uint32_t i = 0;
     for (; i < maxc; i++) {
