@@ -139,18 +139,24 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 // decode (frame kernel -> items + literal scratch, execute, checksums).
 struct ZstdScratch {
     uint32_t *bound = nullptr;     // per-frame item bound
-    uint64_t *rec_base = nullptr;  // n + 1 slot offsets
+    uint32_t *bblk = nullptr;      // per-frame block count (plan)
+    uint64_t *rec_base = nullptr;  // n + 1 item slot offsets
+    uint64_t *blk_base = nullptr;  // n + 1 block slot offsets
     uint32_t *nitems = nullptr;
     uint64_t *ck = nullptr;        // per-frame checksum request
     uint8_t *lit = nullptr;        // literal scratch (output-sized + 64)
     uint64_t *items = nullptr;
-    uint64_t *d_total = nullptr;   // [0] item total, [1] output extent of the last plan
+    uint8_t *ops = nullptr;        // per-frame op lists (4 per block + 4), 32 B each
+    uint8_t *hjobs = nullptr;      // Huffman stream jobs, 4 per block, 32 B each
+    uint8_t *slots = nullptr;      // per-block decoding tables (kZSlot bytes each)
+    uint8_t *hbad = nullptr;       // per Huffman stream: 1 = corrupt
+    uint64_t *d_total = nullptr;   // [0] item total, [1] output extent, [2] blocks
     uint64_t *total = nullptr;     // pinned host copy of d_total
     uint32_t frames_cap = 0;
-    uint64_t lit_cap = 0, items_cap = 0;
+    uint64_t lit_cap = 0, items_cap = 0, blocks_cap = 0, ops_cap = 0;
 };
 int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, uint64_t items,
-                         hipStream_t stream);
+                         uint64_t blocks, hipStream_t stream);
 void zstd_scratch_free(ZstdScratch *s);
 int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      ZstdScratch *s, hipStream_t stream);

@@ -2,28 +2,29 @@
 // ZSTD_decompressDCtx / ZSTD_decompressStream call (decompress.c:434-538;
 // libzstd 1.4.9, restated in oracle/zstd_oracle.c).
 //
-// Three launches per batch, then the LZ4 path's execute kernel:
+// A zstd frame is serial twice over (Huffman literal streams, FSE sequence
+// states), but each serial chain is short and there are many of them, so each
+// gets its own lane.  Per batch, after the plan:
 //
-//   zstd_plan_kernel   one LANE per frame: walks frame and block headers and
-//                      each block's sequence count -> an exact bound on the
-//                      frame's 8-byte sequence items; zstd_scan_kernel turns
-//                      the bounds into slot offsets;
-//   zstd_frame_kernel  one WAVE per frame: headers (wave-uniform, read from
-//                      256-byte windows staged in LDS), Huffman tables and the
-//                      three FSE tables (built in LDS, rank assignment
-//                      wave-parallel by ballots), Huffman literals (one lane
-//                      per stream) into a literal scratch laid out like the
-//                      output, and the sequences (lane 0) -> items: literal
-//                      source, lengths and the resolved offset (repeat offsets
-//                      applied), with every libzstd validation; raw / RLE
-//                      blocks become literal runs;
+//   zstd_plan_kernel   lane per frame: walks frame and block headers and each
+//   zstd_scan_kernel   block's sequence count -> item bound and block count
+//                      per frame -> slot offsets (one workgroup);
+//   zstd_frame_kernel  wave per frame: headers (wave-uniform, 256-byte LDS
+//                      windows), raw / RLE literals into the literal scratch,
+//                      Huffman and FSE tables built in LDS (rank assignment
+//                      by ballots) and stored to the block's slot in HBM, one
+//                      Huffman job per stream, and the frame's op list;
+//   zstd_huf_kernel    lane per Huffman stream (16 blocks per wave, their
+//                      tables staged in LDS) -> literal scratch, laid out like
+//                      the output;
+//   zstd_seq_kernel    lane per frame: replays the op list — FSE states,
+//                      repeat offsets, every libzstd check in libzstd's order
+//                      -> 8-byte items (LZ4 item format, full offset);
 //   seq_exec_kernel    (seq_exec.hip) copies literal runs and matches;
 //   zstd_check_kernel  XXH64 content checksums, for frames that carry one.
 //
-// Every backward bitstream is read by one lane through a 2 KiB LDS ring that
-// the wave refills 512 bytes at a time with global_load_lds (no VGPRs held
-// while the bytes are in flight; the ring is refilled long before the reader
-// reaches the new bytes).
+// Backward bitstreams are read straight from HBM: a lane holds the 16-byte
+// chunk it is consuming and has the next one in flight.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -41,8 +42,6 @@ using namespace lz4d;
 constexpr uint32_t kZMagic = 0xFD2FB528u;
 constexpr uint32_t kZBlockMax = 128u << 10;
 constexpr uint32_t kZW = 2;          // waves (frames) per workgroup
-constexpr uint32_t kRing = 2048;     // bitstream ring bytes per reader
-constexpr uint32_t kSeg = 512;       // refill unit
 constexpr uint32_t kItemExt = 0x80000000u;
 
 enum : uint32_t {
@@ -63,17 +62,15 @@ __device__ __forceinline__ int32_t zerr(uint32_t e)
     return (int32_t)(ST_ZSTD_FLAG | e);
 }
 
-// LDS per wave
+// LDS per wave of the frame kernel
 struct ZLds {
     uint16_t huf[4096];       // Huffman X1 cells: symbol | nbits << 8
     uint32_t fse[3][512];     // LL / OF / ML cells: symbol | nbits << 8 | base << 16
-    uint8_t ring[4][kRing];   // backward bitstream rings, one per reader lane
     uint8_t win[256];         // forward window: headers, table descriptions
     uint32_t wfse[64];        // FSE table of compressed Huffman weights
     int16_t norm[256];        // normalized counts
     uint8_t wts[256];         // Huffman weights
     uint32_t cnt[256];        // per-symbol next-state counters
-    uint8_t lbuf[4][256];     // decoded literals of the 4 Huffman streams, staged
     uint32_t rank[16];        // Huffman: first cell of each weight
 };
 
@@ -179,119 +176,6 @@ __device__ __forceinline__ uint32_t win_bits(const ZLds &L, uint32_t bit, uint32
     for (int i = 0; i < 4; i++)
         v |= (b + i < 256 ? (uint32_t)*lp<uint8_t>(L.win + b + i) : 0u) << (8 * i);
     return (v >> (bit & 7)) & ((1u << n) - 1);
-}
-
-// ---- backward bitstreams through LDS rings ----------------------------------
-// A lane's stream bytes sit in its ring; the bits it reads next sit in a
-// 64-bit register container C, refilled 32 bits at a time: C holds stream
-// bits [pos, pos + nb), the next bit read being bit pos + nb - 1.
-struct Rd {
-    uint32_t ring;   // LDS address of this lane's ring
-    uint32_t x0;     // coordinate of stream byte 0
-    uint32_t rlo;    // the ring holds coordinates [rlo, rlo + kRing) (rlo multiple of kSeg)
-    int32_t pos;     // lowest stream bit in C (< 0: zeros below the stream's start)
-    int32_t nb;      // valid bits in C
-    uint64_t C;
-};
-
-__device__ __forceinline__ uint32_t ring_dw(const Rd &r, uint32_t a)
-{
-    return *la<uint32_t>(r.ring + (a & (kRing - 1)));
-}
-
-// n (1..32) stream bits at bit lo >= 0
-__device__ __forceinline__ uint32_t bits_at(const Rd &r, int32_t lo, uint32_t n)
-{
-    const uint32_t b = r.x0 + ((uint32_t)lo >> 3), a = b & ~3u;
-    const uint64_t q = (uint64_t)ring_dw(r, a) | ((uint64_t)ring_dw(r, a + 4) << 32);
-    const uint32_t sh = (b & 3) * 8 + ((uint32_t)lo & 7);
-    return (uint32_t)((q >> sh) & ((1ull << n) - 1));
-}
-
-// make C hold >= 32 bits (bits below the stream's start read as 0)
-__device__ __forceinline__ void rd_fill(Rd &r)
-{
-    if (r.nb < 32) {
-        r.pos -= 32;
-        const uint32_t v = r.pos >= 0 ? bits_at(r, r.pos, 32)
-                         : r.pos > -32 ? bits_at(r, 0, (uint32_t)(32 + r.pos)) << (uint32_t)(-r.pos)
-                                       : 0u;
-        r.C = (r.C << 32) | v;
-        r.nb += 32;
-    }
-}
-
-// the next n (<= nb) bits, not consumed
-__device__ __forceinline__ uint32_t rd_look(const Rd &r, uint32_t n)
-{
-    return (uint32_t)(r.C >> (uint32_t)(r.nb - (int32_t)n)) & (uint32_t)((1ull << n) - 1);
-}
-
-__device__ __forceinline__ uint32_t rd_read(Rd &r, uint32_t n)
-{
-    if (n == 0)
-        return 0;
-    if (r.nb < (int32_t)n)
-        rd_fill(r);
-    const uint32_t v = rd_look(r, n);
-    r.nb -= (int32_t)n;
-    return v;
-}
-
-// stream bits not consumed yet (< 0 once read past the start)
-__device__ __forceinline__ int32_t rd_left(const Rd &r)
-{
-    return r.pos + r.nb;
-}
-
-// Start one stream per active lane: [xs, xs + len) (len >= 1).  Wave-wide.
-// Returns false on a lane whose stream has no end mark.
-__device__ __forceinline__ bool rd_init(const In &I, Rd &r, bool act, uint32_t ring, uint32_t xs,
-                                        uint32_t len)
-{
-    r.ring = ring;
-    r.x0 = xs;
-    const uint32_t end = xs + len;
-    r.rlo = ((end - 1) & ~(kSeg - 1)) - (kRing - kSeg);
-    uint64_t m = __ballot(act);
-    while (m) {
-        const int j = __builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t rlo = lane_val(r.rlo, j), rg = lane_val(ring, j);
-        for (uint32_t k = 0; k < kRing; k += 256)
-            dma256(I, rlo + k, rg + ((rlo + k) & (kRing - 1)));
-    }
-    dma_wait();
-    if (!act)
-        return true;
-    const uint32_t last = *la<uint8_t>(ring + ((end - 1) & (kRing - 1)));
-    r.pos = last ? (int32_t)(8 * (len - 1)) + hibit(last) : 0;
-    r.nb = 0;
-    r.C = 0;
-    return last != 0;
-}
-
-// Keep every active lane's ring ahead of its reader: when the reader is
-// within 128 bytes (more than a reader consumes between two calls) of the
-// ring's lowest segment, which may still be in flight, wait for the loads in
-// flight and request the next 512 bytes below.  Wave-wide.
-__device__ __forceinline__ void rd_refill(const In &I, Rd &r, bool act)
-{
-    const int32_t bmin = (int32_t)r.x0 + (r.pos >> 3) - 128;
-    const bool need = act && (int32_t)r.rlo > (int32_t)r.x0 && bmin < (int32_t)(r.rlo + kSeg);
-    uint64_t m = __ballot(need);
-    if (!m)
-        return;
-    dma_wait();
-    while (m) {
-        const int j = __builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t a = lane_val(r.rlo, j) - kSeg, rg = lane_val(r.ring, j);
-        dma256(I, a, rg + (a & (kRing - 1)));
-        dma256(I, a + 256, rg + ((a + 256) & (kRing - 1)));
-    }
-    if (need)
-        r.rlo -= kSeg;
 }
 
 // ---- FSE tables -----------------------------------------------------------------
@@ -589,30 +473,79 @@ __device__ __forceinline__ bool emit(Sink &S, uint32_t src, uint32_t lit, uint32
     return true;
 }
 
-// ---- literals ---------------------------------------------------------------------------
+// ---- phase hand-off records (frame kernel -> Huffman / sequence kernels) --------------
+// Per-block decoding tables, in HBM: the block's Huffman cells and its three
+// FSE tables, so the lane-parallel kernels need no table building of their own.
+constexpr uint32_t kZSlot = 10752;               // bytes per block slot
+constexpr uint32_t kSlotFse = 8192;              // byte offset of the FSE cells (u16)
+constexpr uint32_t kFseOff[3] = {0, 512, 768};   // LL / OF / ML, in u16 cells
+
+// One Huffman stream (4 per block; len == 0: no stream).  32 bytes.
+struct HufJob {
+    uint64_t src;   // comp coordinate of the stream's first byte
+    uint64_t dst;   // literal-scratch coordinate of its first symbol
+    uint32_t len;   // stream bytes
+    uint32_t cnt;   // symbols to decode
+    uint32_t lim;   // symbols that may be stored (the frame's capacity)
+    uint32_t lg;    // table log of the block's Huffman cells
+};
+static_assert(sizeof(HufJob) == 32, "HufJob");
+
+// Per-frame op list, in decode order.  The frame kernel stops at its first
+// error (OP_ERR); the sequence kernel replays the list and reports the first
+// failure in libzstd's order, interleaving the Huffman kernel's stream
+// results (OP_LIT) with the frame kernel's header checks.
+enum : uint32_t {
+    OP_LIT = 1,   // a: block -> the block's Huffman streams must have decoded cleanly
+    OP_SEQ,       // a: nseq, b: stream (frame offset), c: stream bytes, d: literal start,
+                  // e: literal count, f: block, g: table logs LL | OF << 4 | ML << 8
+    OP_RUN,       // a: literal start, b: bytes (raw / RLE block)
+    OP_FBEGIN,    // zstd frame starts: repeat offsets reset
+    OP_FEND,      // a: 1 = content size present, 2 = checksum; b/c: size lo/hi; d: checksum
+    OP_ERR,       // a: status
+    OP_DONE,
+};
+struct ZOp {
+    uint32_t k, a, b, c, d, e, f, g;
+};
+static_assert(sizeof(ZOp) == 32, "ZOp");
+
+__device__ __forceinline__ uint64_t op_base(const uint64_t *blk_base, uint32_t f)
+{
+    return 4 * blk_base[f] + 4ull * f;
+}
+
+// ---- frame kernel state ------------------------------------------------------------------
 struct Frame {
     In I;
-    uint32_t codes;    // LDS: literal-length codes [0, 36), match-length codes [36, 89)
-    bool timed;
-    uint64_t tm, t[4]; // section timers (timing builds): literals, tables, sequences, rest
     uint32_t clen;     // compressed entry bytes
+    uint64_t c_abs;    // comp coordinate of the entry
+    uint64_t d_abs;    // literal-scratch coordinate of the entry
     uint8_t *lit;      // literal scratch of this frame (laid out like its output)
     uint32_t cap;      // output capacity (seek-table dSize)
-    uint32_t lo;       // literal bytes decoded into the scratch
-    uint32_t o;        // output bytes accounted for
+    uint32_t lo;       // literal bytes placed in the scratch
     uint32_t huf_log;  // 0: no Huffman table yet
     uint32_t tlog[3];  // LL / OF / ML table logs (valid flags below)
     uint32_t tvalid;   // bit t: table t valid
-    uint32_t rep0, rep1, rep2;
+    ZOp *ops;          // this frame's op list
+    uint32_t nop, op_cap;
+    uint64_t blk0;     // first block slot of the frame
+    uint32_t nblk, blk_cap;
+    uint8_t *slots;
+    HufJob *jobs;
 };
 
-__device__ __forceinline__ void zmark(Frame &F, int i)
+// append an op (wave-uniform; lane 0 writes).  The last slot is kept for the
+// error that ends a list which would overflow.
+__device__ __forceinline__ bool put_op(Frame &F, uint32_t k, uint32_t a = 0, uint32_t b = 0, uint32_t c = 0,
+                                       uint32_t d = 0, uint32_t e = 0, uint32_t f = 0, uint32_t g = 0)
 {
-    if (F.timed) {
-        const uint64_t t = __builtin_readcyclecounter();
-        F.t[i] += t - F.tm;
-        F.tm = t;
-    }
+    if (F.nop + 1 >= F.op_cap && k != OP_ERR && k != OP_DONE)
+        return false;
+    if (lane_id() == 0)
+        F.ops[F.nop] = ZOp{k, a, b, c, d, e, f, g};
+    F.nop++;
+    return true;
 }
 
 // write bytes [p, p + n) of v (16 bytes) into the literal scratch, clamped at
@@ -626,71 +559,14 @@ __device__ __forceinline__ void lit_put(Frame &F, uint32_t p, u32x4 v, uint32_t 
     store_exact(F.lit + p, v, n);
 }
 
-// Huffman streams: lane l < ns decodes stream l into [dst, dst + cnt)
-__device__ __forceinline__ bool huf_streams(ZLds &L, Frame &F, uint32_t ns, uint32_t x_s, const uint32_t *len,
-                            uint32_t dst0, uint32_t size)
+// Literals section at frame offset p (block bytes [p, p + n)) of the block
+// with slot g; *used, *litn, *huf (Huffman streams queued).  Returns 0 or a
+// zstd error.  Wave-wide.
+__device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint32_t p, uint32_t n,
+                                             uint32_t *used, uint32_t *litn, bool *huf)
 {
     const uint32_t lane = lane_id();
-    const uint32_t seg = ns == 1 ? size : (size + 3) / 4;
-    const bool act = lane < ns;
-    uint32_t xs = x_s, sl = 0, dst = dst0, cnt = 0;
-    for (uint32_t k = 0; k < ns; k++) {
-        if (lane == k) {
-            sl = len[k];
-            dst = dst0 + k * seg;
-            cnt = k + 1 < ns ? seg : size - k * seg;
-        }
-        if (lane > k)
-            xs += len[k];
-    }
-    Rd r;
-    const bool ok = rd_init(F.I, r, act && sl > 0, ldsaddr(L.ring[lane & 3]), xs, sl ? sl : 1);
-    bool bad = act && (sl == 0 || !ok);
-    if (__ballot(bad))
-        return false;
-    const uint32_t lg = F.huf_log;
-    const uint32_t maxc = uni(__builtin_amdgcn_readlane(cnt, 0));   // stream 0 is the longest
-    // decoded bytes go to a 256-byte LDS buffer per stream, one ds_write_b8
-    // per symbol; every 256 symbols the wave copies the buffers out (4 bytes
-    // per lane, coalesced)
-    const uint32_t lb = ldsaddr(L.lbuf[lane & 3]);
-    auto flush = [&](uint32_t i0, uint32_t m) {   // symbols [i0, i0 + m) of every stream
-        wave_lds_sync();   // lbuf[k] written by lane k, read by all
-        for (uint32_t k = 0; k < ns; k++) {
-            const uint32_t ck = lane_val(cnt, (int)k), dk = lane_val(dst, (int)k);
-            const uint32_t mk = ck > i0 ? (ck - i0 < m ? ck - i0 : m) : 0;
-            if (4 * lane < mk) {
-                const uint32_t v = *la<uint32_t>(ldsaddr(L.lbuf[k]) + 4 * lane);
-                lit_put(F, dk + i0 + 4 * lane, (u32x4){v, 0, 0, 0}, mk - 4 * lane < 4 ? mk - 4 * lane : 4);
-            }
-        }
-        wave_lds_sync();   // before lane k writes lbuf[k] again
-    };
-    uint32_t i = 0;
-    for (; i < maxc; i++) {
-        if ((i & 63) == 0)
-            rd_refill(F.I, r, act);
-        if (act && i < cnt) {
-            rd_fill(r);
-            const uint32_t e = L.huf[rd_look(r, lg)];
-            r.nb -= (int32_t)(e >> 8);
-            *la<uint8_t>(lb + (i & 255)) = (uint8_t)e;
-        }
-        if ((i & 255) == 255)
-            flush(i - 255, 256);
-    }
-    if (maxc & 255)
-        flush(maxc & ~255u, maxc & 255);
-    bad = act && rd_left(r) != 0;
-    return !__ballot(bad);
-}
-
-// Literals section at frame offset p (block bytes [p, p + n)); *used, *litn.
-// Returns 0 or a zstd error.  Wave-wide.
-__device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint32_t p, uint32_t n, uint32_t *used,
-                             uint32_t *litn)
-{
-    const uint32_t lane = lane_id();
+    *huf = false;
     if (n < 3)
         return ZE_CORRUPT;
     const uint32_t wx = stage_win(L, F.I, p);
@@ -761,7 +637,7 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint32_t p, uint
     } else if (!F.huf_log) {
         return ZE_DICT_CORRUPT;
     }
-    uint32_t len[4];
+    uint32_t len[4] = {0, 0, 0, 0};
     if (ns == 1) {
         len[0] = qn;
     } else {
@@ -779,8 +655,31 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint32_t p, uint
             return ZE_CORRUPT;
         q += 6;
     }
-    if (!huf_streams(L, F, ns, F.I.s0 + q, len, F.lo, size))
-        return ZE_CORRUPT;
+    for (uint32_t k = 0; k < ns; k++)
+        if (len[k] == 0)
+            return ZE_CORRUPT;   // a stream without its end mark
+    // the block's Huffman cells -> its slot; one job per stream
+    const uint32_t lg = F.huf_log;
+    uint8_t *slot = F.slots + g * kZSlot;
+    const uint32_t chunks = (1u << lg) >= 8 ? (1u << lg) / 8 : 1;
+    for (uint32_t c = lane; c < chunks; c += 64)
+        *reinterpret_cast<u32x4 *>(slot + 16 * c) = *reinterpret_cast<const u32x4 *>(&L.huf[8 * c]);
+    if (lane < ns) {
+        const uint32_t seg = ns == 1 ? size : (size + 3) / 4;
+        const uint32_t off = q + (lane > 0 ? len[0] : 0) + (lane > 1 ? len[1] : 0) + (lane > 2 ? len[2] : 0);
+        const uint32_t dst = F.lo + lane * seg;
+        const uint32_t cnt = lane + 1 < ns ? seg : size - lane * seg;
+        const uint32_t room = dst < F.cap ? F.cap - dst : 0;
+        HufJob J;
+        J.src = F.c_abs + off;
+        J.dst = F.d_abs + dst;
+        J.len = lane == 0 ? len[0] : lane == 1 ? len[1] : lane == 2 ? len[2] : len[3];
+        J.cnt = cnt;
+        J.lim = cnt < room ? cnt : room;
+        J.lg = lg;
+        F.jobs[4 * g + lane] = J;
+    }
+    *huf = true;
     *used = lh + csize;
     *litn = size;
     return 0;
@@ -841,18 +740,24 @@ __device__ __forceinline__ uint32_t seq_table(ZLds &L, Frame &F, uint32_t t, uin
     return 0;
 }
 
-// One compressed block [p, p + n) -> items.  Returns 0 or a zstd error.
-__device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p, uint32_t n)
+// One compressed block [p, p + n): literals, then the sequence section's
+// header and tables -> the block's slot and ops.  Returns 0 or a zstd error.
+// Wave-wide.
+__device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_t n)
 {
     const uint32_t lane = lane_id();
     if (n >= kZBlockMax)
         return ZE_SRC_WRONG;
+    if (F.nblk >= F.blk_cap)
+        return ZE_GENERIC;
+    const uint64_t g = F.blk0 + F.nblk++;
     uint32_t lused = 0, litn = 0;
-    zmark(F, 3);
-    uint32_t e = literals(L, F, p, n, &lused, &litn);
-    zmark(F, 0);
+    bool huf = false;
+    uint32_t e = literals(L, F, g, p, n, &lused, &litn, &huf);
     if (e)
         return e;
+    if (huf && !put_op(F, OP_LIT, (uint32_t)g))
+        return ZE_GENERIC;
     uint32_t q = p + lused;
     const uint32_t qe = p + n;
     if (q >= qe)
@@ -877,9 +782,7 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p
     } else {
         q += 1;
     }
-    uint32_t o = F.o, lp_ = F.lo;
-    const uint32_t le = F.lo + litn;
-    bool full = false;
+    uint32_t tl = 0;
     if (nseq) {
         if (q + 1 > qe)
             return ZE_SRC_WRONG;
@@ -894,150 +797,68 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, Sink &S, uint32_t p
                 return err;
             q += u;
         }
-        zmark(F, 1);
-        Rd r;
-        const bool ok = rd_init(F.I, r, lane == 0, ldsaddr(L.ring[0]), F.I.s0 + q, qe > q ? qe - q : 1);
-        if (!uni(ok && qe > q ? 1u : 0u))
-            return ZE_CORRUPT;
-        uint32_t sll = 0, sof = 0, sml = 0, err = 0;
-        uint32_t rep0 = F.rep0, rep1 = F.rep1, rep2 = F.rep2;
-        if (lane == 0) {
-            sll = rd_read(r, F.tlog[0]);
-            sof = rd_read(r, F.tlog[1]);
-            sml = rd_read(r, F.tlog[2]);
-        }
-        for (uint32_t i = 0; i < nseq; i++) {
-            if ((i & 7) == 0)   // <= 8 sequences x 12 bytes < the refill margin
-                rd_refill(F.I, r, lane == 0);
-            if (lane == 0 && !err) {
-                const uint32_t cll = *lp<uint32_t>(L.fse[0] + sll), cof = *lp<uint32_t>(L.fse[1] + sof),
-                               cml = *lp<uint32_t>(L.fse[2] + sml);
-                const uint32_t llc = cll & 0xFF, ofc = cof & 0xFF, mlc = cml & 0xFF;
-                if (llc > 35 || ofc > 31 || mlc > 52) {
-                    err = ZE_CORRUPT;
-                } else {
-                    const uint64_t ofv = (1ull << ofc) + rd_read(r, ofc);
-                    const uint32_t mlcode = *la<uint32_t>(F.codes + 4 * (36 + mlc)),
-                                   llcode = *la<uint32_t>(F.codes + 4 * llc);
-                    const uint32_t ml = (mlcode & 0xFFFFFF) + rd_read(r, mlcode >> 24);
-                    const uint32_t ll = (llcode & 0xFFFFFF) + rd_read(r, llcode >> 24);
-                    uint64_t off;
-                    if (ofv > 3) {
-                        off = ofv - 3;
-                        rep2 = rep1;
-                        rep1 = rep0;
-                        rep0 = (uint32_t)off;
-                    } else {
-                        const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0);
-                        if (idx == 0) {
-                            off = rep0;
-                        } else {
-                            off = idx == 1 ? rep1 : idx == 2 ? rep2 : rep0 - 1;
-                            if (off == 0)
-                                off = 1;
-                            if (idx != 1)
-                                rep2 = rep1;
-                            rep1 = rep0;
-                            rep0 = (uint32_t)off;
-                        }
-                    }
-                    sll = (cll >> 16) + rd_read(r, (cll >> 8) & 0xFF);
-                    sml = (cml >> 16) + rd_read(r, (cml >> 8) & 0xFF);
-                    sof = (cof >> 16) + rd_read(r, (cof >> 8) & 0xFF);
-                    if ((uint64_t)o + ll + ml > F.cap)
-                        err = ZE_DST_SMALL;
-                    else if (le - lp_ < ll)
-                        err = ZE_CORRUPT;
-                    else if (off > (uint64_t)o + ll)
-                        err = ZE_CORRUPT;
-                    else if (!emit(S, lp_, ll, (uint32_t)off, ml))
-                        full = true, err = ZE_GENERIC;
-                    lp_ += ll;
-                    o += ll + ml;
-                }
+        // the three tables -> the block's slot as u16 cells: symbol | next-state
+        // rank ns << 6 (nbits and base follow from ns and the table log)
+        uint16_t *dst = reinterpret_cast<uint16_t *>(F.slots + g * kZSlot + kSlotFse);
+        wave_lds_sync();
+#pragma unroll
+        for (uint32_t t = 0; t < 3; t++) {
+            const uint32_t size = 1u << F.tlog[t];
+            for (uint32_t u = lane; u < size; u += 64) {
+                const uint32_t c = *lp<uint32_t>(&L.fse[t][u]);
+                const uint32_t ns = ((c >> 16) + size) >> ((c >> 8) & 0xFF);
+                dst[kFseOff[t] + u] = (uint16_t)((c & 0xFF) | ns << 6);
             }
-            if (uni(err))
-                break;
         }
-        zmark(F, 2);
-        err = uni(err);
-        if (err)
-            return err;
-        if (uni(lane == 0 && rd_left(r) > 0 ? 1u : 0u))
-            return ZE_CORRUPT;
-        F.rep0 = uni(rep0);
-        F.rep1 = uni(rep1);
-        F.rep2 = uni(rep2);
-        o = uni(o);
-        lp_ = uni(lp_);
+        tl = F.tlog[0] | F.tlog[1] << 4 | F.tlog[2] << 8;
     }
-    const uint32_t last = le - lp_;
-    if (o + last > F.cap)
-        return ZE_DST_SMALL;
-    if (last) {
-        uint32_t ok = 1;
-        if (lane == 0)
-            ok = emit(S, lp_, last, 0, 0);
-        if (!uni(ok))
-            return ZE_GENERIC;
-    }
-    (void)full;
-    S.k = uni(S.k);
-    F.o = o + last;
-    F.lo = le;
+    if (!put_op(F, OP_SEQ, nseq, q, qe > q ? qe - q : 0, F.lo, litn, (uint32_t)g, tl))
+        return ZE_GENERIC;
+    F.lo += litn;
     return 0;
 }
 
-// literal-only item for a raw / RLE block already in the scratch at F.lo
-__device__ __forceinline__ bool run_item(Sink &S, uint32_t src, uint32_t n)
-{
-    uint32_t ok = 1;
-    if (lane_id() == 0 && n)
-        ok = emit(S, src, n, 0, 0);
-    S.k = uni(S.k);
-    return uni(ok) != 0;
-}
-
-// One seek-table entry: every zstd frame in it (ZSTD_decompressDCtx).
-__device__ __forceinline__ int32_t decode_entry(ZLds &L, Frame &F, Sink &S, uint32_t clen, uint64_t *ck)
+// One seek-table entry: every zstd frame in it (ZSTD_decompressDCtx) -> ops.
+// Returns 0, or the zstd error at which the op list ends.
+__device__ __forceinline__ uint32_t decode_entry(ZLds &L, Frame &F, uint32_t clen)
 {
     const uint32_t lane = lane_id();
     uint32_t ip = 0, frames = 0;
     bool summed = false;   // a checksummed frame was decoded: it must be the entry's last
     while (clen - ip >= 5) {
         if (summed)
-            return zerr(ZE_GENERIC);
+            return ZE_GENERIC;
         uint32_t wx = stage_win(L, F.I, ip);
         auto B = [&](uint32_t i) { return uni(wb(L, wx, F.I, ip + i)); };
         const uint32_t magic = B(0) | B(1) << 8 | B(2) << 16 | B(3) << 24;
         if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
             if (clen - ip < 8)
-                return zerr(ZE_SRC_WRONG);
+                return ZE_SRC_WRONG;
             const uint64_t sk = 8 + (uint64_t)(B(4) | B(5) << 8 | B(6) << 16 | B(7) << 24);
             if (sk > clen - ip)
-                return zerr(ZE_SRC_WRONG);
+                return ZE_SRC_WRONG;
             ip += (uint32_t)sk;
             continue;
         }
         if (magic != kZMagic)
-            return zerr(frames ? ZE_SRC_WRONG : ZE_PREFIX);
+            return frames ? ZE_SRC_WRONG : ZE_PREFIX;
         frames++;
         const uint32_t n = clen - ip;
         if (n < 9)
-            return zerr(ZE_SRC_WRONG);
+            return ZE_SRC_WRONG;
         const uint32_t fhd = B(4);
         const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, csum = (fhd >> 2) & 1,
                        did = fhd & 3;
         const uint32_t dsz = did == 3 ? 4 : did;
         const uint32_t hsize = 5 + !single + dsz + (fcs_flag == 0 ? single : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8);
         if (n < hsize + 3)
-            return zerr(ZE_SRC_WRONG);
+            return ZE_SRC_WRONG;
         if (fhd & 0x08)
-            return zerr(ZE_FRAMEPARAM);
+            return ZE_FRAMEPARAM;
         uint32_t h = 5;
         if (!single) {
             if ((B(h) >> 3) + 10 > 31)
-                return zerr(ZE_WINDOW);
+                return ZE_WINDOW;
             h++;
         }
         uint32_t dict = 0;
@@ -1055,30 +876,28 @@ __device__ __forceinline__ int32_t decode_entry(ZLds &L, Frame &F, Sink &S, uint
             fcs = (uint64_t)(B(h) | B(h + 1) << 8 | B(h + 2) << 16 | B(h + 3) << 24) |
                   ((uint64_t)(B(h + 4) | B(h + 5) << 8 | B(h + 6) << 16 | B(h + 7) << 24) << 32);
         if (dict)
-            return zerr(ZE_DICT_WRONG);
+            return ZE_DICT_WRONG;
         ip += hsize;
         // frame state
         F.huf_log = 0;
         F.tvalid = 0;
-        F.rep0 = 1;
-        F.rep1 = 4;
-        F.rep2 = 8;
-        const uint32_t o0 = F.o;
+        if (!put_op(F, OP_FBEGIN))
+            return ZE_GENERIC;
         for (;;) {
             if (clen - ip < 3)
-                return zerr(ZE_SRC_WRONG);
+                return ZE_SRC_WRONG;
             wx = stage_win(L, F.I, ip);
             const uint32_t bh = B(0) | B(1) << 8 | B(2) << 16;
             const uint32_t lastb = bh & 1, type = (bh >> 1) & 3, bsize = bh >> 3;
             const uint32_t csz = type == 1 ? 1 : bsize;
             if (type == 3)
-                return zerr(ZE_CORRUPT);
+                return ZE_CORRUPT;
             ip += 3;
             if (csz > clen - ip)
-                return zerr(ZE_SRC_WRONG);
+                return ZE_SRC_WRONG;
             if (type == 0 || type == 1) {
-                if (bsize > F.cap - F.o)
-                    return zerr(ZE_DST_SMALL);
+                // into the scratch (clamped at the capacity); the sequence
+                // kernel checks the output room in order
                 if (type == 0) {
                     const Span sp = make_span(F.I.base4 + F.I.s0, F.clen);
                     for (uint32_t k = 16 * lane; k < bsize; k += 1024) {
@@ -1090,42 +909,50 @@ __device__ __forceinline__ int32_t decode_entry(ZLds &L, Frame &F, Sink &S, uint
                     for (uint32_t k = 16 * lane; k < bsize; k += 1024)
                         lit_put(F, F.lo + k, (u32x4){bv, bv, bv, bv}, bsize - k < 16 ? bsize - k : 16);
                 }
-                if (!run_item(S, F.lo, bsize))
-                    return zerr(ZE_GENERIC);
+                if (!put_op(F, OP_RUN, F.lo, bsize))
+                    return ZE_GENERIC;
                 F.lo += bsize;
-                F.o += bsize;
             } else {
-                const uint32_t e = block(L, F, S, ip, bsize);
+                const uint32_t e = block(L, F, ip, bsize);
                 if (e)
-                    return zerr(e);
+                    return e;
             }
             ip += csz;
             if (lastb)
                 break;
         }
-        if (fcs != ~0ull && F.o - o0 != fcs)
-            return zerr(ZE_CORRUPT);
+        uint32_t fl = fcs != ~0ull ? 1u : 0u, want = 0;
+        bool trunc = false;
         if (csum) {
-            if (clen - ip < 4)
-                return zerr(ZE_CHECKSUM);
-            wx = stage_win(L, F.I, ip);
-            const uint32_t want = B(0) | B(1) << 8 | B(2) << 16 | B(3) << 24;
-            *ck = (1ull << 63) | ((uint64_t)o0 << 32) | want;   // covers [o0, dSize)
-            summed = true;
-            ip += 4;
+            if (clen - ip < 4) {
+                trunc = true;
+            } else {
+                wx = stage_win(L, F.I, ip);
+                want = B(0) | B(1) << 8 | B(2) << 16 | B(3) << 24;
+                fl |= 2;
+                summed = true;
+                ip += 4;
+            }
         }
+        if (!put_op(F, OP_FEND, fl, (uint32_t)fcs, (uint32_t)(fcs >> 32), want))
+            return ZE_GENERIC;
+        if (trunc)
+            return ZE_CHECKSUM;
     }
     if (clen != ip)
-        return zerr(ZE_SRC_WRONG);
-    return F.o == F.cap ? ST_OK : ST_SHORT_FRAME;
+        return ZE_SRC_WRONG;
+    return 0;
 }
+
 
 // ---- kernels -------------------------------------------------------------------------------
 
-// item bound per frame (lane per frame): 2 items per sequence + padding + 4 per block
+// item bound per frame (lane per frame): 2 items per sequence + padding + 4 per
+// block; and the frame's block count (its table slots and op list)
 __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restrict__ desc, uint32_t n,
                                                         const uint8_t *__restrict__ comp,
-                                                        uint32_t *__restrict__ bound)
+                                                        uint32_t *__restrict__ bound,
+                                                        uint32_t *__restrict__ bblk)
 {
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
     if (f >= n)
@@ -1137,7 +964,7 @@ __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restr
     };
     const uint32_t clen = d.c_size;
     uint64_t items = 8;
-    uint32_t ip = 0;
+    uint32_t ip = 0, blocks = 0;
     while (clen - ip >= 9 && items < (1u << 30)) {
         const uint32_t magic = B(ip) | B(ip + 1) << 8 | B(ip + 2) << 16 | B(ip + 3) << 24;
         if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
@@ -1156,6 +983,7 @@ __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restr
             const uint32_t type = (bh >> 1) & 3, bsize = bh >> 3;
             ip += 3;
             items += 4;
+            blocks++;
             if (type == 2 && bsize >= 3) {
                 const uint32_t b0 = B(ip), lt = b0 & 3, sf = (b0 >> 2) & 3;
                 uint32_t sec;
@@ -1187,29 +1015,36 @@ __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restr
             ip += 4;
     }
     bound[f] = (uint32_t)((items + 3) & ~3ull);
+    bblk[f] = blocks;
 }
 
-// exclusive scan of per-frame bounds -> rec_base[0..n], item total and the
-// output extent max(d_off + d_size) into total[0..1] (device memory, copied
-// to the host by the launcher; one workgroup)
+// exclusive scans of the per-frame item bounds and block counts ->
+// rec_base[0..n], blk_base[0..n]; item total, output extent max(d_off +
+// d_size) and block total into total[0..2] (device memory, copied to the host
+// by the launcher; one workgroup)
 __global__ __launch_bounds__(1024) void zstd_scan_kernel(const FrameDesc *__restrict__ desc,
-                                                         const uint32_t *__restrict__ bound, uint32_t n,
+                                                         const uint32_t *__restrict__ bound,
+                                                         const uint32_t *__restrict__ bblk, uint32_t n,
                                                          uint64_t *__restrict__ rec_base,
+                                                         uint64_t *__restrict__ blk_base,
                                                          uint64_t *__restrict__ total)
 {
     __shared__ uint64_t part[1024];
+    __shared__ uint64_t partb[1024];
     __shared__ uint64_t ext[1024];
     const uint32_t t = threadIdx.x;
     const uint32_t chunk = (n + 1023) / 1024;
     const uint32_t i0 = t * chunk < n ? t * chunk : n;
     const uint32_t i1 = i0 + chunk < n ? i0 + chunk : n;
-    uint64_t s = 0, e = 0;
+    uint64_t s = 0, sb = 0, e = 0;
     for (uint32_t i = i0; i < i1; i++) {
         s += bound[i];
+        sb += bblk[i];
         const uint64_t x = desc[i].d_off + desc[i].d_size;
         e = x > e ? x : e;
     }
     part[t] = s;
+    partb[t] = sb;
     ext[t] = e;
     __syncthreads();
     for (uint32_t d = 512; d >= 1; d >>= 1) {
@@ -1219,86 +1054,430 @@ __global__ __launch_bounds__(1024) void zstd_scan_kernel(const FrameDesc *__rest
     }
     for (uint32_t d = 1; d < 1024; d <<= 1) {
         const uint64_t v = t >= d ? part[t - d] : 0;
+        const uint64_t vb = t >= d ? partb[t - d] : 0;
         __syncthreads();
         part[t] += v;
+        partb[t] += vb;
         __syncthreads();
     }
-    uint64_t run = part[t] - s;
+    uint64_t run = part[t] - s, runb = partb[t] - sb;
     for (uint32_t i = i0; i < i1; i++) {
         rec_base[i] = run;
+        blk_base[i] = runb;
         run += bound[i];
+        runb += bblk[i];
     }
     if (t == 1023) {
         rec_base[n] = part[t];
+        blk_base[n] = partb[t];
         total[0] = part[t];
         total[1] = ext[0];
+        total[2] = partb[t];
     }
 }
 
-__device__ unsigned long long g_ztime[4];   // timing builds: cycles per section
-
-template <bool TIMED>
+// Frame kernel: one wave per seek-table entry.  Headers, literal sections
+// (raw / RLE literals straight into the scratch), Huffman and FSE tables
+// (built in LDS, stored to the block's slot), Huffman stream jobs and the op
+// list the sequence kernel replays.
 __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ lit, uint64_t lit_cap, const uint64_t *__restrict__ rec_base,
-    uint64_t capacity, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
-    int32_t *__restrict__ status, uint64_t *__restrict__ ck)
+    uint64_t capacity, const uint64_t *__restrict__ blk_base, uint8_t *__restrict__ ops,
+    uint8_t *__restrict__ slots, uint8_t *__restrict__ jobs)
 {
     __shared__ ZLds lds[kZW];
-    __shared__ uint32_t codes[89];
-    for (uint32_t i = threadIdx.x; i < 89; i += 64 * kZW)
-        codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
-    __syncthreads();
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t w = threadIdx.x >> 6;
     const uint32_t f = uni(blockIdx.x * kZW + w);
     if (f >= n)
         return;
     ZLds &L = lds[w];
     const FrameDesc d = desc[f];
     Frame F;
-    F.codes = ldsaddr(codes);
-    F.timed = TIMED;
-    F.t[0] = F.t[1] = F.t[2] = F.t[3] = 0;
-    F.tm = TIMED ? __builtin_readcyclecounter() : 0;
     const uintptr_t fa = reinterpret_cast<uintptr_t>(comp + d.c_off);
     F.I.base4 = reinterpret_cast<const uint8_t *>(fa & ~(uintptr_t)3);
     F.I.s0 = (uint32_t)(fa & 3);
     F.I.amax = d.c_size ? (F.I.s0 + d.c_size - 1) & ~3u : 0;
+    F.c_abs = d.c_off;
+    F.d_abs = d.d_off;
     F.lit = lit + d.d_off;
     F.clen = d.c_size;
     F.cap = d.d_size;
-    F.lo = F.o = 0;
+    F.lo = 0;
     F.huf_log = 0;
     F.tvalid = 0;
-    F.rep0 = 1;
-    F.rep1 = 4;
-    F.rep2 = 8;
     F.tlog[0] = F.tlog[1] = F.tlog[2] = 0;
+    const uint64_t ob = op_base(blk_base, f);
+    F.ops = reinterpret_cast<ZOp *>(ops) + ob;
+    F.nop = 0;
+    F.op_cap = (uint32_t)(op_base(blk_base, f + 1) - ob);
+    F.blk0 = blk_base[f];
+    F.nblk = 0;
+    F.blk_cap = (uint32_t)(blk_base[f + 1] - F.blk0);
+    F.slots = slots;
+    F.jobs = reinterpret_cast<HufJob *>(jobs);
+    uint32_t e;
+    // scratch sized by the plan: a frame that would not fit is refused, never
+    // written out of bounds
+    if (rec_base[f + 1] > capacity || d.c_size >= 0x7FFFFF00u ||
+        d.d_off + (uint64_t)d.d_size + 16 > lit_cap)
+        e = ZE_GENERIC;
+    else
+        e = decode_entry(L, F, d.c_size);
+    if (e)
+        put_op(F, OP_ERR, (uint32_t)zerr(e));
+    else
+        put_op(F, OP_DONE);
+}
+
+// ---- backward bitstreams, lane per stream -------------------------------------------
+// Bits of the stream [src, src + len) of comp, read from its end: C holds
+// stream bits [pos, pos + nb) (coordinates in bits from the 16-aligned chunk
+// base; bits below the stream's first byte read as 0).  Refills take 32 bits
+// from the register chunk `cur`; the next lower chunk is always in flight in
+// `nxt`, so no read waits on memory.
+struct BRd {
+    __amdgpu_buffer_rsrc_t r;
+    u32x4 cur, nxt;
+    uint64_t C;
+    int32_t nb, pos, xs, q, rem;
+};
+
+constexpr uint32_t kOOR = 0x80000000u;   // out-of-range buffer offset: loads 0
+
+__device__ __forceinline__ u32x4 chunk16(__amdgpu_buffer_rsrc_t r, int32_t q)
+{
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, q >= 0 ? 16u * (uint32_t)q : kOOR, 0, 0));
+}
+
+// mask of the bits of the dword at bit coordinate p that lie at or above xs
+__device__ __forceinline__ uint32_t above(int32_t xs, int32_t p)
+{
+    const int32_t sh = xs - p;
+    return sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
+}
+
+// len >= 1.  False when the stream's last byte (its end mark) is 0.
+__device__ __forceinline__ bool br_init(BRd &b, const uint8_t *comp, uint64_t src, uint32_t len)
+{
+    const uint64_t base = src & ~15ull;
+    const uint32_t rel = (uint32_t)(src - base) + len;   // bytes from base to the stream's end
+    b.r = __builtin_amdgcn_make_buffer_rsrc((void *)(comp + base), 0, (int)((rel + 3) & ~3u), kRsrcDw3);
+    b.xs = 8 * (int32_t)(src - base);
+    const uint32_t last = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(b.r, rel - 1, 0, 0);
+    const int32_t xm = 8 * (int32_t)(rel - 1) + (last ? 31 - __builtin_clz(last) : 0);
+    const int32_t D = xm >> 5, i = D & 3;
+    b.q = D >> 2;
+    const u32x4 c = chunk16(b.r, b.q);
+    b.nxt = chunk16(b.r, b.q - 1);
+    // the dword holding the end mark to .w, the ones below it after it
+    u32x4 a;
+    a.w = i == 3 ? c.w : i == 2 ? c.z : i == 1 ? c.y : c.x;
+    a.z = i == 3 ? c.z : i == 2 ? c.y : c.x;
+    a.y = i == 3 ? c.y : c.x;
+    a.x = c.x;
+    b.pos = 32 * D;
+    const uint32_t v = a.w & ((1u << (xm & 31)) - 1) & above(b.xs, b.pos);
+    b.C = v;
+    b.nb = xm & 31;
+    b.cur = (u32x4){a.x, a.x, a.y, a.z};
+    b.rem = i;
+    return last != 0;
+}
+
+// 32 more bits (nb < 32 on entry)
+__device__ __forceinline__ void br_refill(BRd &b)
+{
+    if (b.rem == 0) {
+        b.cur = b.nxt;
+        b.rem = 4;
+        b.q -= 1;
+        b.nxt = chunk16(b.r, b.q - 1);
+    }
+    b.pos -= 32;
+    b.C = (b.C << 32) | (b.cur.w & above(b.xs, b.pos));
+    b.nb += 32;
+    b.cur.w = b.cur.z;
+    b.cur.z = b.cur.y;
+    b.cur.y = b.cur.x;
+    b.rem -= 1;
+}
+
+// n (<= 31) bits, consumed
+__device__ __forceinline__ uint32_t br_read(BRd &b, uint32_t n)
+{
+    if (b.nb < (int32_t)n)
+        br_refill(b);
+    const uint32_t v = (uint32_t)(b.C >> (uint32_t)(b.nb - (int32_t)n)) & ((1u << n) - 1);
+    b.nb -= (int32_t)n;
+    return v;
+}
+
+// stream bits not consumed yet (< 0 once read past the start)
+__device__ __forceinline__ int32_t br_left(const BRd &b)
+{
+    return b.pos + b.nb - b.xs;
+}
+
+// ---- Huffman literals: one lane per stream -------------------------------------------
+// 16 blocks (64 streams) per wave; their tables packed into 16 KiB of LDS when
+// they fit (else read from the slots).  A lane refills its bit container every
+// G symbols (G * lg <= 32) and stores 16 decoded bytes at a time, aligned.
+constexpr uint32_t kHufLdsCells = 8192;
+
+template <int G, typename Tab>
+__device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *out, uint64_t dst, uint32_t cnt,
+                                           uint32_t lim)
+{
+    const uint32_t mask = (1u << lg) - 1;
+    auto one = [&]() -> uint32_t {
+        const uint32_t e = T((uint32_t)(b.C >> (uint32_t)(b.nb - (int32_t)lg)) & mask);
+        b.nb -= (int32_t)(e >> 8);
+        return e & 0xFF;
+    };
+    uint32_t i = 0;
+    while (i < cnt && ((dst + i) & 15)) {
+        if (b.nb < 32)
+            br_refill(b);
+        const uint32_t s = one();
+        if (i < lim)
+            out[i] = (uint8_t)s;
+        i++;
+    }
+    while (i + 16 <= lim) {
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (k % G == 0 && b.nb < 32)
+                br_refill(b);
+            const uint32_t s = one();
+            if ((k & 3) == 0)
+                acc[k >> 2] = s;
+            else
+                acc[k >> 2] |= s << (8 * (k & 3));
+        }
+        *reinterpret_cast<u32x4 *>(out + i) = acc;
+        i += 16;
+    }
+    while (i < cnt) {
+        if (b.nb < 32)
+            br_refill(b);
+        const uint32_t s = one();
+        if (i < lim)
+            out[i] = (uint8_t)s;
+        i++;
+    }
+}
+
+__global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
+                                                      const uint8_t *__restrict__ comp,
+                                                      const uint8_t *__restrict__ slots,
+                                                      uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t tabs[kHufLdsCells];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t j = blockIdx.x * 64 + lane;
+    HufJob J = {0, 0, 0, 0, 0, 0};
+    if (j < nj)
+        J = reinterpret_cast<const HufJob *>(jobs)[j];
+    const bool act = J.len != 0;
+    const uint32_t lgmax = lane_val(wave_incl_max(act ? J.lg : 0u), 63);
+    // cells of each block's table (stream 0's lane), packed in block order
+    const uint32_t cells = (lane & 3) == 0 && act ? ((1u << J.lg) < 8 ? 8u : 1u << J.lg) : 0u;
+    const uint32_t incl = wave_incl_add(cells);
+    const uint32_t first = (uint32_t)__shfl((int)(incl - cells), (int)(lane & ~3u), 64);
+    const bool in_lds = lane_val(incl, 63) <= kHufLdsCells;
+    if (in_lds) {
+        for (uint32_t b = 0; b < 16; b++) {
+            const uint32_t nc = lane_val(cells, 4 * b);
+            if (!nc)
+                continue;
+            const uint32_t c0 = lane_val(incl, 4 * b) - nc;
+            const uint8_t *src = slots + (uint64_t)(blockIdx.x * 16 + b) * kZSlot;
+            for (uint32_t c = lane; c < nc / 8; c += 64)
+                *lp<u32x4>(&tabs[c0 + 8 * c]) = *reinterpret_cast<const u32x4 *>(src + 16 * c);
+        }
+        __syncthreads();
+    }
+    if (j >= nj)
+        return;
+    bool bad = false;
+    if (act) {
+        BRd b;
+        bad = !br_init(b, comp, J.src, J.len);
+        uint8_t *out = lit + J.dst;
+        if (in_lds) {
+            const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(&tabs[first]);
+            auto T = [&](uint32_t i) -> uint32_t { return *la<uint16_t>(tb + 2 * i); };
+            if (lgmax <= 8)
+                huf_stream<4>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+            else if (lgmax <= 10)
+                huf_stream<3>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+            else
+                huf_stream<2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+        } else {
+            const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)(j >> 2) * kZSlot);
+            auto T = [&](uint32_t i) -> uint32_t { return gt[i]; };
+            if (lgmax <= 10)
+                huf_stream<3>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+            else
+                huf_stream<2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+        }
+        bad = bad || br_left(b) != 0;
+    }
+    hbad[j] = bad ? 1 : 0;
+}
+
+// ---- sequences: one lane per seek-table entry ------------------------------------------
+// Replays the frame's op list: FSE states (tables from the block slots),
+// repeat offsets, every libzstd check, items in the LZ4 item format with the
+// full offset; then the final status, item count and checksum request.
+__device__ __forceinline__ uint32_t fse_next(BRd &b, uint32_t e, uint32_t tl)
+{
+    const uint32_t ns = e >> 6;
+    const uint32_t nbits = tl + (uint32_t)__builtin_clz(ns) - 31;
+    return ((ns << nbits) - (1u << tl)) + br_read(b, nbits);
+}
+
+__global__ __launch_bounds__(256) void zstd_seq_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
+    const uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
+    const uint8_t *__restrict__ slots, const uint8_t *__restrict__ hbad,
+    const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
+    int32_t *__restrict__ status, uint64_t *__restrict__ ck)
+{
+    __shared__ uint32_t codes[89];
+    for (uint32_t i = threadIdx.x; i < 89; i += 256)
+        codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
+    __syncthreads();
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= n)
+        return;
+    const FrameDesc d = desc[f];
+    const uint64_t ob = op_base(blk_base, f);
+    const uint32_t opn = (uint32_t)(op_base(blk_base, f + 1) - ob);
+    const ZOp *op = reinterpret_cast<const ZOp *>(ops) + ob;
     Sink S;
     const uint64_t rb = rec_base[f];
     S.base = items + rb;
     S.k = 0;
     S.cap = (uint32_t)(rec_base[f + 1] - rb);
+    const uint32_t cap = d.d_size;
+    uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
     uint64_t c = 0;
-    int32_t st;
-    // scratch sized by the plan: a frame that would not fit is refused, never
-    // written out of bounds
-    if (rec_base[f + 1] > capacity || d.c_size >= 0x7FFFFF00u ||
-        d.d_off + (uint64_t)d.d_size + 16 > lit_cap)
-        st = zerr(ZE_GENERIC);
-    else
-        st = decode_entry(L, F, S, d.c_size, &c);
-    if (lane == 0) {
-        status[f] = st;
-        nitems[f] = S.k;
-        ck[f] = c;
+    int32_t st = zerr(ZE_GENERIC);
+    for (uint32_t k = 0; k < opn; k++) {
+        const ZOp P = op[k];
+        uint32_t err = 0;
+        if (P.k == OP_LIT) {
+            const uint32_t h = *reinterpret_cast<const uint32_t *>(hbad + 4ull * P.a);
+            if (h)
+                err = ZE_CORRUPT;
+        } else if (P.k == OP_SEQ) {
+            const uint32_t nseq = P.a;
+            uint32_t lp_ = P.d;
+            const uint32_t le = P.d + P.e;
+            if (nseq) {
+                BRd b;
+                if (P.c == 0 || !br_init(b, comp, d.c_off + P.b, P.c)) {
+                    err = ZE_CORRUPT;
+                } else {
+                    const uint32_t tll = P.g & 15, tof = (P.g >> 4) & 15, tml = (P.g >> 8) & 15;
+                    const uint16_t *T = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
+                    uint32_t sll = br_read(b, tll), sof = br_read(b, tof), sml = br_read(b, tml);
+                    for (uint32_t i = 0; i < nseq; i++) {
+                        const uint32_t ell = T[kFseOff[0] + sll], eof = T[kFseOff[1] + sof],
+                                       eml = T[kFseOff[2] + sml];
+                        const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
+                        if (llc > 35 || ofc > 31 || mlc > 52) {
+                            err = ZE_CORRUPT;
+                            break;
+                        }
+                        const uint64_t ofv = (1ull << ofc) + br_read(b, ofc);
+                        const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
+                        const uint32_t ml = (mlcode & 0xFFFFFF) + br_read(b, mlcode >> 24);
+                        const uint32_t ll = (llcode & 0xFFFFFF) + br_read(b, llcode >> 24);
+                        uint64_t off;
+                        if (ofv > 3) {
+                            off = ofv - 3;
+                            rep2 = rep1;
+                            rep1 = rep0;
+                            rep0 = (uint32_t)off;
+                        } else {
+                            const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0);
+                            if (idx == 0) {
+                                off = rep0;
+                            } else {
+                                off = idx == 1 ? rep1 : idx == 2 ? rep2 : rep0 - 1;
+                                if (off == 0)
+                                    off = 1;
+                                if (idx != 1)
+                                    rep2 = rep1;
+                                rep1 = rep0;
+                                rep0 = (uint32_t)off;
+                            }
+                        }
+                        sll = fse_next(b, ell, tll);
+                        sml = fse_next(b, eml, tml);
+                        sof = fse_next(b, eof, tof);
+                        if ((uint64_t)o + ll + ml > cap)
+                            err = ZE_DST_SMALL;
+                        else if (le - lp_ < ll)
+                            err = ZE_CORRUPT;
+                        else if (off > (uint64_t)o + ll)
+                            err = ZE_CORRUPT;
+                        else if (!emit(S, lp_, ll, (uint32_t)off, ml))
+                            err = ZE_GENERIC;
+                        if (err)
+                            break;
+                        lp_ += ll;
+                        o += ll + ml;
+                    }
+                    if (!err && br_left(b) > 0)
+                        err = ZE_CORRUPT;
+                }
+            }
+            if (!err) {
+                const uint32_t last = le - lp_;
+                if (o + last > cap)
+                    err = ZE_DST_SMALL;
+                else if (last && !emit(S, lp_, last, 0, 0))
+                    err = ZE_GENERIC;
+                else
+                    o += last;
+            }
+        } else if (P.k == OP_RUN) {
+            if (P.b > cap - o)
+                err = ZE_DST_SMALL;
+            else if (P.b && !emit(S, P.a, P.b, 0, 0))
+                err = ZE_GENERIC;
+            else
+                o += P.b;
+        } else if (P.k == OP_FBEGIN) {
+            rep0 = 1;
+            rep1 = 4;
+            rep2 = 8;
+            o0 = o;
+        } else if (P.k == OP_FEND) {
+            if ((P.a & 1) && (uint64_t)(o - o0) != ((uint64_t)P.c << 32 | P.b))
+                err = ZE_CORRUPT;
+            else if (P.a & 2)
+                c = (1ull << 63) | ((uint64_t)o0 << 32) | P.d;
+        } else if (P.k == OP_ERR) {
+            st = (int32_t)P.a;
+            break;
+        } else {   // OP_DONE (anything else: a list the frame kernel never wrote)
+            st = P.k == OP_DONE ? (o == cap ? ST_OK : ST_SHORT_FRAME) : zerr(ZE_GENERIC);
+            break;
+        }
+        if (err) {
+            st = zerr(err);
+            break;
+        }
     }
-    if (TIMED) {
-        zmark(F, 3);
-        if (lane == 0)
-            for (int i = 0; i < 4; i++)
-                atomicAdd(&g_ztime[i], (unsigned long long)F.t[i]);
-    }
+    status[f] = st;
+    nitems[f] = S.k;
+    ck[f] = c;
 }
 
 // XXH64 of [o0, cap) of a frame's output for frames flagged by the frame
@@ -1400,106 +1579,117 @@ __global__ __launch_bounds__(256) void zstd_check_kernel(const FrameDesc *__rest
 
 // ---- host side -----------------------------------------------------------------------------------
 
+namespace {
+template <typename T>
+int grow(T **p, uint64_t &cap, uint64_t want, uint64_t unit)
+{
+    if (want <= cap)
+        return 0;
+    if (*p)
+        (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (hipMalloc((void **)p, want * unit) != hipSuccess)
+        return -1;
+    cap = want;
+    return 0;
+}
+}   // namespace
+
 int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, uint64_t items,
-                         hipStream_t stream)
+                         uint64_t blocks, hipStream_t stream)
 {
     (void)stream;
     if (frames + 1 > s->frames_cap) {
         const uint32_t cap = frames + 1 < 4096 ? 4096 : frames + 1;
-        zstd_scratch_free(s);
+        for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
+                        (void *)s->nitems, (void *)s->ck, (void *)s->d_total})
+            if (p)
+                (void)hipFree(p);
+        if (s->total)
+            (void)hipHostFree(s->total);
+        s->bound = s->bblk = s->nitems = nullptr;
+        s->rec_base = s->blk_base = s->ck = s->d_total = s->total = nullptr;
+        s->frames_cap = 0;
         if (hipMalloc((void **)&s->bound, sizeof(uint32_t) * cap) != hipSuccess ||
+            hipMalloc((void **)&s->bblk, sizeof(uint32_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->rec_base, sizeof(uint64_t) * (cap + 1)) != hipSuccess ||
+            hipMalloc((void **)&s->blk_base, sizeof(uint64_t) * (cap + 1)) != hipSuccess ||
             hipMalloc((void **)&s->nitems, sizeof(uint32_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->ck, sizeof(uint64_t) * cap) != hipSuccess ||
-            hipMalloc((void **)&s->d_total, 2 * sizeof(uint64_t)) != hipSuccess ||
-            hipHostMalloc((void **)&s->total, 2 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
+            hipMalloc((void **)&s->d_total, 4 * sizeof(uint64_t)) != hipSuccess ||
+            hipHostMalloc((void **)&s->total, 4 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
             return -1;
-        s->total[0] = s->total[1] = 0;
+        s->total[0] = s->total[1] = s->total[2] = 0;
         s->frames_cap = cap;
     }
-    if (out_bytes + 64 > s->lit_cap) {
-        if (s->lit)
-            (void)hipFree(s->lit);
-        s->lit = nullptr;
-        s->lit_cap = 0;
-        if (hipMalloc((void **)&s->lit, out_bytes + 64) != hipSuccess)
+    if (grow(&s->lit, s->lit_cap, out_bytes + 64, 1) != 0 || grow(&s->items, s->items_cap, items, 8) != 0)
+        return -1;
+    if (blocks > s->blocks_cap) {
+        uint64_t c0 = s->blocks_cap, c1 = s->blocks_cap, c2 = s->blocks_cap;
+        if (grow(&s->hjobs, c0, blocks, 4 * sizeof(HufJob)) != 0 ||
+            grow(&s->hbad, c1, blocks, 4) != 0 || grow(&s->slots, c2, blocks, kZSlot) != 0)
             return -1;
-        s->lit_cap = out_bytes + 64;
+        s->blocks_cap = blocks;
     }
-    if (items > s->items_cap) {
-        if (s->items)
-            (void)hipFree(s->items);
-        s->items = nullptr;
-        s->items_cap = 0;
-        if (hipMalloc((void **)&s->items, items * sizeof(uint64_t)) != hipSuccess)
-            return -1;
-        s->items_cap = items;
-    }
-    return 0;
+    // op lists: 4 per block + 4 per frame
+    return grow(&s->ops, s->ops_cap, blocks + frames, 4 * sizeof(ZOp));
 }
 
 void zstd_scratch_free(ZstdScratch *s)
 {
-    if (s->bound)
-        (void)hipFree(s->bound);
-    if (s->rec_base)
-        (void)hipFree(s->rec_base);
-    if (s->nitems)
-        (void)hipFree(s->nitems);
-    if (s->ck)
-        (void)hipFree(s->ck);
-    if (s->lit)
-        (void)hipFree(s->lit);
-    if (s->items)
-        (void)hipFree(s->items);
-    if (s->d_total)
-        (void)hipFree(s->d_total);
+    for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
+                    (void *)s->nitems, (void *)s->ck, (void *)s->lit, (void *)s->items, (void *)s->ops,
+                    (void *)s->hjobs, (void *)s->slots, (void *)s->hbad, (void *)s->d_total})
+        if (p)
+            (void)hipFree(p);
     if (s->total)
         (void)hipHostFree(s->total);
     *s = ZstdScratch();
 }
 
-// Plan only: bounds + offsets, then the item total and output extent copied
-// into s->total (pinned host memory), valid once the stream reaches it.
+// Plan only: bounds + offsets, then the item total, output extent and block
+// total copied into s->total (pinned host memory), valid once the stream
+// reaches it.
 int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      ZstdScratch *s, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
     hipLaunchKernelGGL(zstd_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
-                       nframes, d_comp, s->bound);
-    hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, s->bound, nframes,
-                       s->rec_base, s->d_total);
+                       nframes, d_comp, s->bound, s->bblk);
+    hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, s->bound, s->bblk, nframes,
+                       s->rec_base, s->blk_base, s->d_total);
     if (hipGetLastError() != hipSuccess)
         return -1;
-    return hipMemcpyAsync(s->total, s->d_total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) ==
+    return hipMemcpyAsync(s->total, s->d_total, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) ==
                    hipSuccess
                ? 0
                : -1;
 }
 
+// Frame kernel -> Huffman kernel -> sequence kernel -> execute -> checksums,
+// back to back on the stream.  s must hold the last plan of these frames.
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
-    static const bool timed = getenv("ZSEEK_ZSTD_TIMING") != nullptr;
-    if (timed) {
-        unsigned long long z[4] = {0, 0, 0, 0};
-        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ztime), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
-        hipLaunchKernelGGL(zstd_frame_kernel<true>, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0,
-                           stream, d_desc, nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->items,
-                           s->nitems, d_status, s->ck);
-        (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_ztime), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
-        (void)hipStreamSynchronize(stream);
-        const double t = (double)(z[0] + z[1] + z[2] + z[3]);
-        fprintf(stderr, "zstd frame kernel (wave cycles): literals %.1f%%  tables %.1f%%  sequences %.1f%%  rest %.1f%%  total %.3g\n",
-                100 * z[0] / t, 100 * z[1] / t, 100 * z[2] / t, 100 * z[3] / t, t);
-    } else {
-        hipLaunchKernelGGL(zstd_frame_kernel<false>, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0,
-                           stream, d_desc, nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->items,
-                           s->nitems, d_status, s->ck);
-    }
+    const uint64_t blocks = s->total[2];
+    if (blocks > s->blocks_cap)
+        return -1;
+    const uint32_t nj = (uint32_t)(4 * blocks);
+    if (nj && hipMemsetAsync(s->hjobs, 0, (size_t)nj * sizeof(HufJob), stream) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(zstd_frame_kernel, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc,
+                       nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops,
+                       s->slots, s->hjobs);
+    if (nj)
+        hipLaunchKernelGGL(zstd_huf_kernel, dim3((nj + 63) / 64), dim3(64), 0, stream, s->hjobs, nj, d_comp,
+                           s->slots, s->lit, s->hbad);
+    hipLaunchKernelGGL(zstd_seq_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc, nframes,
+                       d_comp, s->ops, s->blk_base, s->slots, s->hbad, s->rec_base, s->items, s->nitems,
+                       d_status, s->ck);
     stage_mark(2, stream);
     const int rc = launch_seq_exec_lit(d_desc, nframes, s->lit, d_out, s->rec_base, s->items,
                                        s->nitems, d_status, stream);
@@ -1510,15 +1700,15 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     return rc == 0 && hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Plan, wait for the item total and output extent, size the
-// scratch, decode.  The one synchronization point of the zstd path: the item
-// slots of a frame are only known once its sequence counts are read.
+// Plan, wait for the totals, size the scratch, decode.  The one
+// synchronization point of the zstd path: the item slots and table slots of a
+// frame are only known once its block headers and sequence counts are read.
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
-    if (zstd_scratch_reserve(s, nframes, 0, 0, stream) != 0)
+    if (zstd_scratch_reserve(s, nframes, 0, 0, 0, stream) != 0)
         return -1;
     stage_mark(0, stream);
     if (launch_zstd_plan(d_desc, nframes, d_comp, s, stream) != 0)
@@ -1526,7 +1716,7 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     stage_mark(1, stream);
     if (hipStreamSynchronize(stream) != hipSuccess)
         return -1;
-    if (zstd_scratch_reserve(s, nframes, s->total[1], s->total[0], stream) != 0)
+    if (zstd_scratch_reserve(s, nframes, s->total[1], s->total[0], s->total[2], stream) != 0)
         return -1;
     return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream);
 }
