@@ -161,6 +161,13 @@ __device__ __forceinline__ uint32_t lane_val(uint32_t v, int l)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v)
 {
     for (int m = 32; m >= 1; m >>= 1) {

@@ -588,13 +588,6 @@ __device__ __forceinline__ bool sub(Scan &L, Fill &S)
     return jump;
 }
 
-__device__ __forceinline__ uint64_t uni64(uint64_t v)
-{
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-
 template <bool BR>
 __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))) void lz4_scan_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,

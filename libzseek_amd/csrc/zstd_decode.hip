@@ -448,31 +448,6 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
     return used;
 }
 
-// ---- items (format: lz4_split.hip Sink; full offset in extended items) ------------
-struct Sink {
-    uint64_t *base;
-    uint32_t k, cap;
-};
-
-// lane 0 only
-__device__ __forceinline__ bool emit(Sink &S, uint32_t src, uint32_t lit, uint32_t off, uint32_t ml)
-{
-    if (lit > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF) {
-        const uint32_t pad = (S.k & 63) == 63 ? 1 : 0;
-        if (S.k + pad + 2 > S.cap)
-            return false;
-        if (pad)
-            S.base[S.k++] = 0;
-        S.base[S.k++] = ((uint64_t)off << 32) | src | kItemExt;
-        S.base[S.k++] = ((uint64_t)ml << 32) | lit;
-        return true;
-    }
-    if (S.k + 1 > S.cap)
-        return false;
-    S.base[S.k++] = ((uint64_t)(off | lit << 16 | (ml ? ml - 3 : 0) << 24) << 32) | src;
-    return true;
-}
-
 // ---- phase hand-off records (frame kernel -> Huffman / sequence kernels) --------------
 // Per-block decoding tables, in HBM: the block's Huffman cells and its three
 // FSE tables, so the lane-parallel kernels need no table building of their own.
@@ -1131,23 +1106,52 @@ __global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
 }
 
 // ---- backward bitstreams, lane per stream -------------------------------------------
-// Bits of the stream [src, src + len) of comp, read from its end: C holds
-// stream bits [pos, pos + nb) (coordinates in bits from the 16-aligned chunk
-// base; bits below the stream's first byte read as 0).  Refills take 32 bits
-// from the register chunk `cur`; the next lower chunk is always in flight in
-// `nxt`, so no read waits on memory.
+// Bits of one stream of comp, read from its end: C holds stream bits
+// [pos, pos + nb) (coordinates in bits from the stream's 16-aligned chunk
+// base x0; bits below the stream's first byte read as 0).  The lane's stream
+// bytes pass through a ring of kRS 16-byte slots in LDS (dword k of slot s of
+// lane l at ring base + s * 1024 + k * 256 + 4 * l: a wave's ring reads hit 64
+// different banks whatever dword each lane reads): br_step, once per decode step at a fixed
+// place in the loop, commits the chunk loaded one step earlier and issues the
+// next load — unconditionally, re-fetching the last chunk when the ring is
+// full — so no load result is ever waited for in the step that issued it and
+// no load sits in a divergent branch.  br_fill refills C from the ring.  The
+// buffer resource is wave-uniform (a span of comp covering the wave's
+// streams); x0 is the lane's offset in it.
+constexpr int32_t kRS = 4;
+
 struct BRd {
     __amdgpu_buffer_rsrc_t r;
-    u32x4 cur, nxt;
     uint64_t C;
-    int32_t nb, pos, xs, q, rem;
+    u32x4 P, P2;     // chunks `pend`, `pend2`, committed to the ring at the next step
+    uint32_t x0;
+    uint32_t ring;   // LDS address of this lane's dword 0 of slot 0
+    int32_t nb, pos, xs;
+    int32_t pq;      // next chunk to fetch (decreasing; < 0 reads zeros)
+    int32_t pend, pend2;
 };
 
 constexpr uint32_t kOOR = 0x80000000u;   // out-of-range buffer offset: loads 0
+constexpr uint64_t kMaxSpan = 0x7FFFFF00ull;   // largest span one resource covers
 
-__device__ __forceinline__ u32x4 chunk16(__amdgpu_buffer_rsrc_t r, int32_t q)
+__device__ __forceinline__ u32x4 chunk16(const BRd &b, int32_t q)
 {
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, q >= 0 ? 16u * (uint32_t)q : kOOR, 0, 0));
+    return __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(b.r, q >= 0 ? b.x0 + 16u * (uint32_t)q : kOOR, 0, 0));
+}
+
+__device__ __forceinline__ uint32_t slot_addr(const BRd &b, int32_t q)
+{
+    return b.ring + (uint32_t)(q & (kRS - 1)) * 1024u;
+}
+
+__device__ __forceinline__ void slot_put(const BRd &b, int32_t q, u32x4 v)
+{
+    const uint32_t a = slot_addr(b, q);
+    *la<uint32_t>(a) = v.x;
+    *la<uint32_t>(a + 256) = v.y;
+    *la<uint32_t>(a + 512) = v.z;
+    *la<uint32_t>(a + 768) = v.w;
 }
 
 // mask of the bits of the dword at bit coordinate p that lie at or above xs
@@ -1157,57 +1161,83 @@ __device__ __forceinline__ uint32_t above(int32_t xs, int32_t p)
     return sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
 }
 
-// len >= 1.  False when the stream's last byte (its end mark) is 0.
-__device__ __forceinline__ bool br_init(BRd &b, const uint8_t *comp, uint64_t src, uint32_t len)
+// A span [base, base + len) of comp as a buffer resource (len < 2^31 - 256;
+// rounded up to whole dwords: the hardware range-checks each dword).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const uint8_t *comp, uint64_t base, uint64_t len)
 {
-    const uint64_t base = src & ~15ull;
-    const uint32_t rel = (uint32_t)(src - base) + len;   // bytes from base to the stream's end
-    b.r = __builtin_amdgcn_make_buffer_rsrc((void *)(comp + base), 0, (int)((rel + 3) & ~3u), kRsrcDw3);
-    b.xs = 8 * (int32_t)(src - base);
-    const uint32_t last = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(b.r, rel - 1, 0, 0);
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(comp + base), 0, (int)(uint32_t)((len + 3) & ~3ull),
+                                             kRsrcDw3);
+}
+
+// The stream at offset x (len >= 1 bytes) of resource r, ring at LDS address
+// ring.  False when its last byte (the end mark) is 0.
+__device__ __forceinline__ bool br_init(BRd &b, __amdgpu_buffer_rsrc_t r, uint32_t x, uint32_t len, uint32_t ring)
+{
+    b.r = r;
+    b.ring = ring;
+    b.x0 = x & ~15u;
+    const uint32_t rel = (x & 15u) + len;   // bytes from x0 to the stream's end
+    b.xs = 8 * (int32_t)(x & 15u);
+    const uint32_t last = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, b.x0 + rel - 1, 0, 0);
     const int32_t xm = 8 * (int32_t)(rel - 1) + (last ? 31 - __builtin_clz(last) : 0);
-    const int32_t D = xm >> 5, i = D & 3;
-    b.q = D >> 2;
-    const u32x4 c = chunk16(b.r, b.q);
-    b.nxt = chunk16(b.r, b.q - 1);
-    // the dword holding the end mark to .w, the ones below it after it
-    u32x4 a;
-    a.w = i == 3 ? c.w : i == 2 ? c.z : i == 1 ? c.y : c.x;
-    a.z = i == 3 ? c.z : i == 2 ? c.y : c.x;
-    a.y = i == 3 ? c.y : c.x;
-    a.x = c.x;
+    const int32_t D = xm >> 5, i = D & 3, q = D >> 2;
+    u32x4 c[kRS - 1];
+#pragma unroll
+    for (int k = 0; k < kRS - 1; k++)
+        c[k] = chunk16(b, q - k);
+#pragma unroll
+    for (int k = 0; k < kRS - 1; k++)
+        slot_put(b, q - k, c[k]);
+    b.pq = q - (kRS - 1);
+    b.P = chunk16(b, b.pq);
+    b.P2 = b.P;
+    b.pend = b.pend2 = b.pq;
+    b.pq--;
+    const uint32_t top = i == 3 ? c[0].w : i == 2 ? c[0].z : i == 1 ? c[0].y : c[0].x;
     b.pos = 32 * D;
-    const uint32_t v = a.w & ((1u << (xm & 31)) - 1) & above(b.xs, b.pos);
-    b.C = v;
+    b.C = top & ((1u << (xm & 31)) - 1) & above(b.xs, b.pos);
     b.nb = xm & 31;
-    b.cur = (u32x4){a.x, a.x, a.y, a.z};
-    b.rem = i;
     return last != 0;
 }
 
-// 32 more bits (nb < 32 on entry)
-__device__ __forceinline__ void br_refill(BRd &b)
+// Once per decode step: commit the pending chunk(s), fetch the next one(s)
+// (F = 1 or 2 chunks per step).
+template <int F = 1>
+__device__ __forceinline__ void br_step(BRd &b)
 {
-    if (b.rem == 0) {
-        b.cur = b.nxt;
-        b.rem = 4;
-        b.q -= 1;
-        b.nxt = chunk16(b.r, b.q - 1);
+    slot_put(b, b.pend, b.P);
+    if (F == 2)
+        slot_put(b, b.pend2, b.P2);
+    const int32_t qcur = (b.pos - 32) >> 7;   // chunk of the next dword to absorb
+    bool room = b.pq >= qcur - (kRS - 1);
+    int32_t t = room ? b.pq : b.pq + 1;
+    b.P = chunk16(b, t);
+    b.pend = t;
+    b.pq = room ? b.pq - 1 : b.pq;
+    if (F == 2) {
+        room = b.pq >= qcur - (kRS - 1);
+        t = room ? b.pq : b.pq + 1;
+        b.P2 = chunk16(b, t);
+        b.pend2 = t;
+        b.pq = room ? b.pq - 1 : b.pq;
     }
-    b.pos -= 32;
-    b.C = (b.C << 32) | (b.cur.w & above(b.xs, b.pos));
-    b.nb += 32;
-    b.cur.w = b.cur.z;
-    b.cur.z = b.cur.y;
-    b.cur.y = b.cur.x;
-    b.rem -= 1;
+}
+
+// refill C to >= 32 bits when below (branch-free)
+__device__ __forceinline__ void br_fill(BRd &b)
+{
+    const int32_t p2 = b.pos - 32, dw = p2 >> 5;
+    const uint32_t v = *la<uint32_t>(slot_addr(b, dw >> 2) + 256u * (uint32_t)(dw & 3)) & above(b.xs, p2);
+    const bool need = b.nb < 32;
+    b.C = need ? (b.C << 32) | v : b.C;
+    b.nb = need ? b.nb + 32 : b.nb;
+    b.pos = need ? p2 : b.pos;
 }
 
 // n (<= 31) bits, consumed
 __device__ __forceinline__ uint32_t br_read(BRd &b, uint32_t n)
 {
-    if (b.nb < (int32_t)n)
-        br_refill(b);
+    br_fill(b);
     const uint32_t v = (uint32_t)(b.C >> (uint32_t)(b.nb - (int32_t)n)) & ((1u << n) - 1);
     b.nb -= (int32_t)n;
     return v;
@@ -1223,9 +1253,9 @@ __device__ __forceinline__ int32_t br_left(const BRd &b)
 // 16 blocks (64 streams) per wave; their tables packed into 16 KiB of LDS when
 // they fit (else read from the slots).  A lane refills its bit container every
 // G symbols (G * lg <= 32) and stores 16 decoded bytes at a time, aligned.
-constexpr uint32_t kHufLdsCells = 8192;
+constexpr uint32_t kHufLdsCells = 2048;
 
-template <int G, typename Tab>
+template <int G, int F, typename Tab>
 __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *out, uint64_t dst, uint32_t cnt,
                                            uint32_t lim)
 {
@@ -1236,32 +1266,42 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
         return e & 0xFF;
     };
     uint32_t i = 0;
+    // head (< 16 symbols, <= 180 bits): the ring holds kRS - 1 chunks after br_init
     while (i < cnt && ((dst + i) & 15)) {
-        if (b.nb < 32)
-            br_refill(b);
+        br_fill(b);
         const uint32_t s = one();
         if (i < lim)
             out[i] = (uint8_t)s;
         i++;
     }
+    // 16 symbols per step; each step's 16 bytes are stored after the next
+    // step's loads are issued, so the wait that commits a chunk never waits
+    // on a store issued just before it
+    u32x4 prev = {0, 0, 0, 0};
+    const uint32_t i0 = i;
     while (i + 16 <= lim) {
+        br_step<F>(b);
+        if (i != i0)
+            *reinterpret_cast<u32x4 *>(out + i - 16) = prev;
         u32x4 acc = {0, 0, 0, 0};
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            if (k % G == 0 && b.nb < 32)
-                br_refill(b);
+            if (k % G == 0)
+                br_fill(b);
             const uint32_t s = one();
             if ((k & 3) == 0)
                 acc[k >> 2] = s;
             else
                 acc[k >> 2] |= s << (8 * (k & 3));
         }
-        *reinterpret_cast<u32x4 *>(out + i) = acc;
+        prev = acc;
         i += 16;
     }
+    if (i != i0)
+        *reinterpret_cast<u32x4 *>(out + i - 16) = prev;
     while (i < cnt) {
-        if (b.nb < 32)
-            br_refill(b);
+        br_step<F>(b);
+        br_fill(b);
         const uint32_t s = one();
         if (i < lim)
             out[i] = (uint8_t)s;
@@ -1275,6 +1315,7 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
                                                       uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
 {
     __shared__ __attribute__((aligned(16))) uint16_t tabs[kHufLdsCells];
+    __shared__ __attribute__((aligned(16))) uint8_t rings[kRS * 1024];
     const uint32_t lane = threadIdx.x;
     const uint32_t j = blockIdx.x * 64 + lane;
     HufJob J = {0, 0, 0, 0, 0, 0};
@@ -1299,31 +1340,41 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
         }
         __syncthreads();
     }
+    // one resource over the wave's streams (else lane by lane, each its own)
+    const uint64_t lo = uni64(wave_min64(act ? J.src : ~0ull)) & ~15ull;
+    const uint64_t hi = uni64(wave_max64(act ? J.src + J.len : 0ull));
     if (j >= nj)
         return;
     bool bad = false;
-    if (act) {
+    auto run = [&](__amdgpu_buffer_rsrc_t r, uint64_t base) {
         BRd b;
-        bad = !br_init(b, comp, J.src, J.len);
+        bad = !br_init(b, r, (uint32_t)(J.src - base), J.len, (uint32_t)(uintptr_t)lp<uint8_t>(rings) + 4 * lane);
         uint8_t *out = lit + J.dst;
         if (in_lds) {
             const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(&tabs[first]);
             auto T = [&](uint32_t i) -> uint32_t { return *la<uint16_t>(tb + 2 * i); };
             if (lgmax <= 8)
-                huf_stream<4>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
-            else if (lgmax <= 10)
-                huf_stream<3>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+                huf_stream<4, 1>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
             else
-                huf_stream<2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+                huf_stream<2, 2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
         } else {
             const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)(j >> 2) * kZSlot);
             auto T = [&](uint32_t i) -> uint32_t { return gt[i]; };
-            if (lgmax <= 10)
-                huf_stream<3>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
-            else
-                huf_stream<2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+            huf_stream<2, 2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
         }
         bad = bad || br_left(b) != 0;
+    };
+    if (hi > lo && hi - lo < kMaxSpan) {
+        if (act)
+            run(span_rsrc(comp, lo, hi - lo), lo);
+    } else {
+        for (uint64_t m = __ballot(act); m; m &= m - 1) {
+            const int l = __builtin_ctzll(m);
+            const uint64_t s0 = uni64(__shfl(J.src, l, 64)) & ~15ull;
+            const uint64_t s1 = uni64(__shfl(J.src + J.len, l, 64));
+            if ((int)lane == l)
+                run(span_rsrc(comp, s0, s1 - s0), s0);
+        }
     }
     hbad[j] = bad ? 1 : 0;
 }
@@ -1332,6 +1383,54 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
 // Replays the frame's op list: FSE states (tables from the block slots),
 // repeat offsets, every libzstd check, items in the LZ4 item format with the
 // full offset; then the final status, item count and checksum request.
+// Items of one lane, staged in LDS (16 per lane, item j of lane l at
+// stage + (j & 15) * 512 + 8 * l) and flushed to the frame's slots 8 or more
+// at a time: no item store is pending at the next ring commit's wait.
+struct LSink {
+    uint64_t *base;
+    uint32_t k, f, cap;
+    uint32_t stage;
+};
+
+__device__ __forceinline__ void lput(LSink &S, uint64_t v)
+{
+    *la<uint64_t>(S.stage + (S.k & 15) * 512) = v;
+    S.k++;
+}
+
+// the 8-byte item format of lz4_split.hip (Sink), with the full offset in
+// extended items
+__device__ __forceinline__ bool lemit(LSink &S, uint32_t src, uint32_t lit, uint32_t off, uint32_t ml)
+{
+    if (lit > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF) {
+        const uint32_t pad = (S.k & 63) == 63 ? 1 : 0;
+        if (S.k + pad + 2 > S.cap)
+            return false;
+        if (pad)
+            lput(S, 0);
+        lput(S, ((uint64_t)off << 32) | src | kItemExt);
+        lput(S, ((uint64_t)ml << 32) | lit);
+        return true;
+    }
+    if (S.k + 1 > S.cap)
+        return false;
+    lput(S, ((uint64_t)(off | lit << 16 | (ml ? ml - 3 : 0) << 24) << 32) | src);
+    return true;
+}
+
+__device__ __forceinline__ void lflush(LSink &S)
+{
+    for (uint32_t j = S.f; j < S.k; j++)
+        S.base[j] = *la<uint64_t>(S.stage + (j & 15) * 512);
+    S.f = S.k;
+}
+
+__device__ __forceinline__ void lmaybe(LSink &S)
+{
+    if (S.k - S.f >= 8)
+        lflush(S);
+}
+
 __device__ __forceinline__ uint32_t fse_next(BRd &b, uint32_t e, uint32_t tl)
 {
     const uint32_t ns = e >> 6;
@@ -1347,132 +1446,160 @@ __global__ __launch_bounds__(256) void zstd_seq_kernel(
     int32_t *__restrict__ status, uint64_t *__restrict__ ck)
 {
     __shared__ uint32_t codes[89];
+    __shared__ __attribute__((aligned(16))) uint8_t rings[4][kRS * 1024];
+    __shared__ __attribute__((aligned(16))) uint64_t stage[4][16 * 64];
     for (uint32_t i = threadIdx.x; i < 89; i += 256)
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
     __syncthreads();
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
-    if (f >= n)
+    const bool act = f < n;
+    FrameDesc d = {0, 0, 0, 0};
+    if (act)
+        d = desc[f];
+    // one resource over the wave's frames (else lane by lane, each its own)
+    const uint64_t lo = uni64(wave_min64(act ? d.c_off : ~0ull)) & ~15ull;
+    const uint64_t hi = uni64(wave_max64(act ? d.c_off + d.c_size : 0ull));
+    if (!act)
         return;
-    const FrameDesc d = desc[f];
     const uint64_t ob = op_base(blk_base, f);
     const uint32_t opn = (uint32_t)(op_base(blk_base, f + 1) - ob);
     const ZOp *op = reinterpret_cast<const ZOp *>(ops) + ob;
-    Sink S;
+    LSink S;
     const uint64_t rb = rec_base[f];
     S.base = items + rb;
-    S.k = 0;
+    S.k = S.f = 0;
     S.cap = (uint32_t)(rec_base[f + 1] - rb);
+    S.stage = (uint32_t)(uintptr_t)lp<uint64_t>(&stage[threadIdx.x >> 6][threadIdx.x & 63]);
     const uint32_t cap = d.d_size;
     uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
     uint64_t c = 0;
     int32_t st = zerr(ZE_GENERIC);
-    for (uint32_t k = 0; k < opn; k++) {
-        const ZOp P = op[k];
-        uint32_t err = 0;
-        if (P.k == OP_LIT) {
-            const uint32_t h = *reinterpret_cast<const uint32_t *>(hbad + 4ull * P.a);
-            if (h)
-                err = ZE_CORRUPT;
-        } else if (P.k == OP_SEQ) {
-            const uint32_t nseq = P.a;
-            uint32_t lp_ = P.d;
-            const uint32_t le = P.d + P.e;
-            if (nseq) {
-                BRd b;
-                if (P.c == 0 || !br_init(b, comp, d.c_off + P.b, P.c)) {
+    auto replay = [&](__amdgpu_buffer_rsrc_t r, uint64_t base) {
+        for (uint32_t k = 0; k < opn; k++) {
+            const ZOp P = op[k];
+            uint32_t err = 0;
+            if (P.k == OP_LIT) {
+                const uint32_t h = *reinterpret_cast<const uint32_t *>(hbad + 4ull * P.a);
+                if (h)
                     err = ZE_CORRUPT;
-                } else {
-                    const uint32_t tll = P.g & 15, tof = (P.g >> 4) & 15, tml = (P.g >> 8) & 15;
-                    const uint16_t *T = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
-                    uint32_t sll = br_read(b, tll), sof = br_read(b, tof), sml = br_read(b, tml);
-                    for (uint32_t i = 0; i < nseq; i++) {
-                        const uint32_t ell = T[kFseOff[0] + sll], eof = T[kFseOff[1] + sof],
-                                       eml = T[kFseOff[2] + sml];
-                        const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
-                        if (llc > 35 || ofc > 31 || mlc > 52) {
-                            err = ZE_CORRUPT;
-                            break;
-                        }
-                        const uint64_t ofv = (1ull << ofc) + br_read(b, ofc);
-                        const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
-                        const uint32_t ml = (mlcode & 0xFFFFFF) + br_read(b, mlcode >> 24);
-                        const uint32_t ll = (llcode & 0xFFFFFF) + br_read(b, llcode >> 24);
-                        uint64_t off;
-                        if (ofv > 3) {
-                            off = ofv - 3;
-                            rep2 = rep1;
-                            rep1 = rep0;
-                            rep0 = (uint32_t)off;
-                        } else {
-                            const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0);
-                            if (idx == 0) {
-                                off = rep0;
-                            } else {
-                                off = idx == 1 ? rep1 : idx == 2 ? rep2 : rep0 - 1;
-                                if (off == 0)
-                                    off = 1;
-                                if (idx != 1)
-                                    rep2 = rep1;
+            } else if (P.k == OP_SEQ) {
+                const uint32_t nseq = P.a;
+                uint32_t lp_ = P.d;
+                const uint32_t le = P.d + P.e;
+                if (nseq) {
+                    BRd b;
+                    if (P.c == 0 || !br_init(b, r, (uint32_t)(d.c_off - base) + P.b, P.c,
+                                              (uint32_t)(uintptr_t)lp<uint8_t>(rings[threadIdx.x >> 6]) +
+                                                  4 * (threadIdx.x & 63))) {
+                        err = ZE_CORRUPT;
+                    } else {
+                        const uint32_t tll = P.g & 15, tof = (P.g >> 4) & 15, tml = (P.g >> 8) & 15;
+                        const uint16_t *T = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
+                        uint32_t sll = br_read(b, tll), sof = br_read(b, tof), sml = br_read(b, tml);
+                        for (uint32_t i = 0; i < nseq; i++) {
+                            br_step(b);
+                            const uint32_t ell = T[kFseOff[0] + sll], eof = T[kFseOff[1] + sof],
+                                           eml = T[kFseOff[2] + sml];
+                            const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
+                            if (llc > 35 || ofc > 31 || mlc > 52) {
+                                err = ZE_CORRUPT;
+                                break;
+                            }
+                            const uint64_t ofv = (1ull << ofc) + br_read(b, ofc);
+                            const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
+                            const uint32_t ml = (mlcode & 0xFFFFFF) + br_read(b, mlcode >> 24);
+                            const uint32_t ll = (llcode & 0xFFFFFF) + br_read(b, llcode >> 24);
+                            uint64_t off;
+                            if (ofv > 3) {
+                                off = ofv - 3;
+                                rep2 = rep1;
                                 rep1 = rep0;
                                 rep0 = (uint32_t)off;
+                            } else {
+                                const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0);
+                                if (idx == 0) {
+                                    off = rep0;
+                                } else {
+                                    off = idx == 1 ? rep1 : idx == 2 ? rep2 : rep0 - 1;
+                                    if (off == 0)
+                                        off = 1;
+                                    if (idx != 1)
+                                        rep2 = rep1;
+                                    rep1 = rep0;
+                                    rep0 = (uint32_t)off;
+                                }
                             }
+                            sll = fse_next(b, ell, tll);
+                            sml = fse_next(b, eml, tml);
+                            sof = fse_next(b, eof, tof);
+                            if ((uint64_t)o + ll + ml > cap)
+                                err = ZE_DST_SMALL;
+                            else if (le - lp_ < ll)
+                                err = ZE_CORRUPT;
+                            else if (off > (uint64_t)o + ll)
+                                err = ZE_CORRUPT;
+                            else if (!lemit(S, lp_, ll, (uint32_t)off, ml))
+                                err = ZE_GENERIC;
+                            if (err)
+                                break;
+                            lmaybe(S);
+                            lp_ += ll;
+                            o += ll + ml;
                         }
-                        sll = fse_next(b, ell, tll);
-                        sml = fse_next(b, eml, tml);
-                        sof = fse_next(b, eof, tof);
-                        if ((uint64_t)o + ll + ml > cap)
-                            err = ZE_DST_SMALL;
-                        else if (le - lp_ < ll)
+                        if (!err && br_left(b) > 0)
                             err = ZE_CORRUPT;
-                        else if (off > (uint64_t)o + ll)
-                            err = ZE_CORRUPT;
-                        else if (!emit(S, lp_, ll, (uint32_t)off, ml))
-                            err = ZE_GENERIC;
-                        if (err)
-                            break;
-                        lp_ += ll;
-                        o += ll + ml;
                     }
-                    if (!err && br_left(b) > 0)
-                        err = ZE_CORRUPT;
                 }
-            }
-            if (!err) {
-                const uint32_t last = le - lp_;
-                if (o + last > cap)
+                if (!err) {
+                    const uint32_t last = le - lp_;
+                    if (o + last > cap)
+                        err = ZE_DST_SMALL;
+                    else if (last && !lemit(S, lp_, last, 0, 0))
+                        err = ZE_GENERIC;
+                    else
+                        o += last;
+                }
+            } else if (P.k == OP_RUN) {
+                if (P.b > cap - o)
                     err = ZE_DST_SMALL;
-                else if (last && !emit(S, lp_, last, 0, 0))
+                else if (P.b && !lemit(S, P.a, P.b, 0, 0))
                     err = ZE_GENERIC;
                 else
-                    o += last;
+                    o += P.b;
+            } else if (P.k == OP_FBEGIN) {
+                rep0 = 1;
+                rep1 = 4;
+                rep2 = 8;
+                o0 = o;
+            } else if (P.k == OP_FEND) {
+                if ((P.a & 1) && (uint64_t)(o - o0) != ((uint64_t)P.c << 32 | P.b))
+                    err = ZE_CORRUPT;
+                else if (P.a & 2)
+                    c = (1ull << 63) | ((uint64_t)o0 << 32) | P.d;
+            } else if (P.k == OP_ERR) {
+                st = (int32_t)P.a;
+                break;
+            } else {   // OP_DONE (anything else: a list the frame kernel never wrote)
+                st = P.k == OP_DONE ? (o == cap ? ST_OK : ST_SHORT_FRAME) : zerr(ZE_GENERIC);
+                break;
             }
-        } else if (P.k == OP_RUN) {
-            if (P.b > cap - o)
-                err = ZE_DST_SMALL;
-            else if (P.b && !emit(S, P.a, P.b, 0, 0))
-                err = ZE_GENERIC;
-            else
-                o += P.b;
-        } else if (P.k == OP_FBEGIN) {
-            rep0 = 1;
-            rep1 = 4;
-            rep2 = 8;
-            o0 = o;
-        } else if (P.k == OP_FEND) {
-            if ((P.a & 1) && (uint64_t)(o - o0) != ((uint64_t)P.c << 32 | P.b))
-                err = ZE_CORRUPT;
-            else if (P.a & 2)
-                c = (1ull << 63) | ((uint64_t)o0 << 32) | P.d;
-        } else if (P.k == OP_ERR) {
-            st = (int32_t)P.a;
-            break;
-        } else {   // OP_DONE (anything else: a list the frame kernel never wrote)
-            st = P.k == OP_DONE ? (o == cap ? ST_OK : ST_SHORT_FRAME) : zerr(ZE_GENERIC);
-            break;
+            if (err) {
+                st = zerr(err);
+                break;
+            }
+            lmaybe(S);
         }
-        if (err) {
-            st = zerr(err);
-            break;
+        lflush(S);
+    };
+    if (hi > lo && hi - lo < kMaxSpan) {
+        replay(span_rsrc(comp, lo, hi - lo), lo);
+    } else {
+        for (uint64_t m = __ballot(true); m; m &= m - 1) {
+            const int l = __builtin_ctzll(m);
+            const uint64_t s0 = uni64(__shfl(d.c_off, l, 64)) & ~15ull;
+            const uint64_t s1 = uni64(__shfl(d.c_off + d.c_size, l, 64));
+            if ((int)(threadIdx.x & 63) == l)
+                replay(span_rsrc(comp, s0, s1 - s0), s0);
         }
     }
     status[f] = st;
