@@ -64,14 +64,12 @@ __device__ __forceinline__ int32_t zerr(uint32_t e)
 
 // LDS per wave of the frame kernel
 struct ZLds {
-    uint16_t huf[4096];       // Huffman X1 cells: symbol | nbits << 8
     uint32_t fse[3][512];     // LL / OF / ML cells: symbol | nbits << 8 | base << 16
-    uint8_t win[256];         // forward window: headers, table descriptions
+    __attribute__((aligned(8))) uint8_t win[256];   // forward window: headers, table descriptions
     uint32_t wfse[64];        // FSE table of compressed Huffman weights
     int16_t norm[256];        // normalized counts
     uint8_t wts[256];         // Huffman weights
     uint32_t cnt[256];        // per-symbol next-state counters
-    uint32_t rank[16];        // Huffman: first cell of each weight
 };
 
 // literal / match length codes: base | extra bits << 24 (RFC 8878 §3.1.1.3.2.1)
@@ -167,15 +165,20 @@ __device__ __forceinline__ uint32_t wb(const ZLds &L, uint32_t wx, const In &I, 
     return *lp<uint8_t>(L.win + (I.s0 + p - wx));
 }
 
+// 32 window bits from bit `bit` (LSB first), from two aligned dword reads;
+// bits past the window's 256 bytes read as 0
+__device__ __forceinline__ uint32_t win32(const ZLds &L, uint32_t bit)
+{
+    const uint32_t d = bit >> 5;
+    const uint32_t lo = d < 64 ? *lp<uint32_t>(L.win + 4 * d) : 0u;
+    const uint32_t hi = d + 1 < 64 ? *lp<uint32_t>(L.win + 4 * d + 4) : 0u;
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (bit & 31));
+}
+
 // forward bits [bit, bit + n) (n <= 16) of the window, LSB first
 __device__ __forceinline__ uint32_t win_bits(const ZLds &L, uint32_t bit, uint32_t n)
 {
-    const uint32_t b = bit >> 3;
-    uint32_t v = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-        v |= (b + i < 256 ? (uint32_t)*lp<uint8_t>(L.win + b + i) : 0u) << (8 * i);
-    return (v >> (bit & 7)) & ((1u << n) - 1);
+    return win32(L, bit) & ((1u << n) - 1);
 }
 
 // ---- FSE tables -----------------------------------------------------------------
@@ -303,9 +306,10 @@ __device__ __forceinline__ void fse_build(ZLds &L, uint32_t *tab, uint32_t nsym,
 
 // ---- Huffman tables --------------------------------------------------------------
 // Tree description at frame offset p (window staged at wx); returns its size
-// or 0 on error.  Builds L.huf; *log receives the table log.  Wave-wide.
+// or 0 on error.  Writes the 2^log decoding cells (symbol | nbits << 8) to
+// cells (HBM); *log receives the table log.  Wave-wide.
 __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, uint32_t p, uint32_t avail,
-                             uint32_t *log)
+                                             uint32_t *log, uint16_t *cells)
 {
     const uint32_t lane = lane_id();
     const uint32_t hb = uni(wb(L, wx, I, p));
@@ -332,14 +336,13 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
                 err = 1;
             } else {
                 int32_t pos = (int32_t)(8 * (bn - 1)) + hibit(lastb);
+                // n backward bits ending at pos (bits below the stream read as 0)
                 auto rb = [&](uint32_t n) -> uint32_t {
                     pos -= (int32_t)n;
-                    uint32_t v = 0;
-                    for (uint32_t i = 0; i < n; i++) {
-                        const int32_t bit = pos + (int32_t)i;
-                        if (bit >= 0 && ((*lp<uint8_t>(L.win + b0 + (bit >> 3)) >> (bit & 7)) & 1))
-                            v |= 1u << i;
-                    }
+                    const int32_t x = (int32_t)(8 * b0) + pos;
+                    uint32_t v = (x >= 0 ? win32(L, (uint32_t)x) : win32(L, 0) << (uint32_t)(-x)) & ((1u << n) - 1);
+                    if (pos < 0)
+                        v = -pos >= (int32_t)n ? 0u : v & (~0u << (uint32_t)(-pos));
                     return v;
                 };
                 uint32_t s1 = rb(tl), s2 = rb(tl);
@@ -416,33 +419,34 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
     if (r1 < 2 || (r1 & 1))
         return 0;
     nw++;
-    // first cell of each weight class: classes in increasing weight order
-    if (lane == 0) {
-        uint32_t cntw[13];
-        for (uint32_t k = 0; k <= 12; k++)
-            cntw[k] = 0;
-        for (uint32_t s = 0; s < nw; s++)
-            cntw[L.wts[s]]++;
-        uint32_t acc = 0;
-        for (uint32_t k = 1; k <= lg; k++) {
-            L.rank[k] = acc;
-            acc += cntw[k] << (k - 1);
-        }
+    // canonical cells, straight into the block's slot: class k (weight k,
+    // 2^(k-1) cells per symbol) follows the lower classes, its symbols in
+    // symbol order
+    uint32_t wl[4];
+#pragma unroll
+    for (int ps = 0; ps < 4; ps++) {
+        const uint32_t s = 64 * ps + lane;
+        wl[ps] = s < nw ? (uint32_t)*lp<uint8_t>(&L.wts[s]) : 0u;
     }
-    wave_lds_sync();
-    // cells: symbols in order, each takes 2^(w-1) cells of its class
-    for (uint32_t s = 0; s < nw; s++) {
-        const uint32_t w = uni(L.wts[s]);
-        if (!w)
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t c0 = 0;
+    for (uint32_t k = 1; k <= lg; k++) {
+        uint32_t n = 0;
+#pragma unroll
+        for (int ps = 0; ps < 4; ps++) {
+            const uint64_t m = __ballot(wl[ps] == k);
+            if (wl[ps] == k)
+                *lp<int16_t>(&L.norm[n + (uint32_t)__builtin_popcountll(m & below)]) = (int16_t)(64 * ps + lane);
+            n += (uint32_t)__builtin_popcountll(m);
+        }
+        if (!n)
             continue;
-        const uint32_t len = (1u << w) >> 1;
-        const uint32_t c0 = uni(L.rank[w]);
-        const uint16_t e = (uint16_t)(s | (lg + 1 - w) << 8);
-        for (uint32_t c = lane; c < len; c += 64)
-            L.huf[c0 + c] = e;
-        if (lane == 0)
-            L.rank[w] = c0 + len;
         wave_lds_sync();
+        const uint32_t sh = k - 1, ck = n << sh, nb = (lg + 1 - k) << 8;
+        for (uint32_t u = lane; u < ck; u += 64)
+            cells[c0 + u] = (uint16_t)((uint32_t)*lp<int16_t>(&L.norm[u >> sh]) | nb);
+        c0 += ck;
+        wave_lds_sync();   // before the list is rewritten
     }
     *log = lg;
     return used;
@@ -462,7 +466,7 @@ struct HufJob {
     uint32_t len;   // stream bytes
     uint32_t cnt;   // symbols to decode
     uint32_t lim;   // symbols that may be stored (the frame's capacity)
-    uint32_t lg;    // table log of the block's Huffman cells
+    uint32_t tab;   // slot holding the Huffman cells | table log << 28
 };
 static_assert(sizeof(HufJob) == 32, "HufJob");
 
@@ -500,6 +504,7 @@ struct Frame {
     uint32_t cap;      // output capacity (seek-table dSize)
     uint32_t lo;       // literal bytes placed in the scratch
     uint32_t huf_log;  // 0: no Huffman table yet
+    uint32_t huf_slot; // block slot holding the current Huffman cells
     uint32_t tlog[3];  // LL / OF / ML table logs (valid flags below)
     uint32_t tvalid;   // bit t: table t valid
     ZOp *ops;          // this frame's op list
@@ -603,10 +608,12 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint
     uint32_t q = p + lh, qn = csize;
     if (type == 2) {
         uint32_t lg = 0;
-        const uint32_t hs = huf_read(L, F.I, wx, q, qn, &lg);
+        const uint32_t hs =
+            huf_read(L, F.I, wx, q, qn, &lg, reinterpret_cast<uint16_t *>(F.slots + g * kZSlot));
         if (!hs)
             return ZE_CORRUPT;
         F.huf_log = lg;
+        F.huf_slot = (uint32_t)g;
         q += hs;
         qn -= hs;
     } else if (!F.huf_log) {
@@ -633,12 +640,9 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint
     for (uint32_t k = 0; k < ns; k++)
         if (len[k] == 0)
             return ZE_CORRUPT;   // a stream without its end mark
-    // the block's Huffman cells -> its slot; one job per stream
+    // one job per stream; the cells are in the slot of the block that sent the
+    // table (this one, or an earlier one for a treeless literals section)
     const uint32_t lg = F.huf_log;
-    uint8_t *slot = F.slots + g * kZSlot;
-    const uint32_t chunks = (1u << lg) >= 8 ? (1u << lg) / 8 : 1;
-    for (uint32_t c = lane; c < chunks; c += 64)
-        *reinterpret_cast<u32x4 *>(slot + 16 * c) = *reinterpret_cast<const u32x4 *>(&L.huf[8 * c]);
     if (lane < ns) {
         const uint32_t seg = ns == 1 ? size : (size + 3) / 4;
         const uint32_t off = q + (lane > 0 ? len[0] : 0) + (lane > 1 ? len[1] : 0) + (lane > 2 ? len[2] : 0);
@@ -651,7 +655,7 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint
         J.len = lane == 0 ? len[0] : lane == 1 ? len[1] : lane == 2 ? len[2] : len[3];
         J.cnt = cnt;
         J.lim = cnt < room ? cnt : room;
-        J.lg = lg;
+        J.tab = F.huf_slot | lg << 28;
         F.jobs[4 * g + lane] = J;
     }
     *huf = true;
@@ -1322,9 +1326,10 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
     if (j < nj)
         J = reinterpret_cast<const HufJob *>(jobs)[j];
     const bool act = J.len != 0;
-    const uint32_t lgmax = lane_val(wave_incl_max(act ? J.lg : 0u), 63);
+    const uint32_t jlg = J.tab >> 28, jslot = J.tab & 0x0FFFFFFFu;
+    const uint32_t lgmax = lane_val(wave_incl_max(act ? jlg : 0u), 63);
     // cells of each block's table (stream 0's lane), packed in block order
-    const uint32_t cells = (lane & 3) == 0 && act ? ((1u << J.lg) < 8 ? 8u : 1u << J.lg) : 0u;
+    const uint32_t cells = (lane & 3) == 0 && act ? ((1u << jlg) < 8 ? 8u : 1u << jlg) : 0u;
     const uint32_t incl = wave_incl_add(cells);
     const uint32_t first = (uint32_t)__shfl((int)(incl - cells), (int)(lane & ~3u), 64);
     const bool in_lds = lane_val(incl, 63) <= kHufLdsCells;
@@ -1334,7 +1339,7 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
             if (!nc)
                 continue;
             const uint32_t c0 = lane_val(incl, 4 * b) - nc;
-            const uint8_t *src = slots + (uint64_t)(blockIdx.x * 16 + b) * kZSlot;
+            const uint8_t *src = slots + (uint64_t)lane_val(jslot, 4 * b) * kZSlot;
             for (uint32_t c = lane; c < nc / 8; c += 64)
                 *lp<u32x4>(&tabs[c0 + 8 * c]) = *reinterpret_cast<const u32x4 *>(src + 16 * c);
         }
@@ -1354,13 +1359,13 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
             const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(&tabs[first]);
             auto T = [&](uint32_t i) -> uint32_t { return *la<uint16_t>(tb + 2 * i); };
             if (lgmax <= 8)
-                huf_stream<4, 1>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+                huf_stream<4, 1>(b, T, jlg, out, J.dst, J.cnt, J.lim);
             else
-                huf_stream<2, 2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+                huf_stream<2, 2>(b, T, jlg, out, J.dst, J.cnt, J.lim);
         } else {
-            const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)(j >> 2) * kZSlot);
+            const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)jslot * kZSlot);
             auto T = [&](uint32_t i) -> uint32_t { return gt[i]; };
-            huf_stream<2, 2>(b, T, J.lg, out, J.dst, J.cnt, J.lim);
+            huf_stream<2, 2>(b, T, jlg, out, J.dst, J.cnt, J.lim);
         }
         bad = bad || br_left(b) != 0;
     };
