@@ -68,6 +68,7 @@ struct ZLds {
     __attribute__((aligned(8))) uint8_t win[256];   // forward window: headers, table descriptions
     uint32_t wfse[64];        // FSE table of compressed Huffman weights
     int16_t norm[256];        // normalized counts
+    uint16_t spr[512];        // FSE spread: symbol of each cell in spread order
     uint8_t wts[256];         // Huffman weights
     uint32_t cnt[256];        // per-symbol next-state counters
 };
@@ -175,21 +176,28 @@ __device__ __forceinline__ uint32_t win32(const ZLds &L, uint32_t bit)
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (bit & 31));
 }
 
-// forward bits [bit, bit + n) (n <= 16) of the window, LSB first
-__device__ __forceinline__ uint32_t win_bits(const ZLds &L, uint32_t bit, uint32_t n)
-{
-    return win32(L, bit) & ((1u << n) - 1);
-}
-
 // ---- FSE tables -----------------------------------------------------------------
-// Normalized counts from the window at bit 0 of frame offset p (lane 0),
+// Normalized counts from the window at bit 0 of window offset wofs (lane 0),
 // RFC 8878 §4.1.1 / FSE_readNCount.  Returns bytes used, or 0 on error
-// (*err set).  norm[] receives nsym entries.
+// (*err set).  norm[] receives nsym entries; the caller zeroes norm[0..max_sym]
+// first (zero counts are not written).  The bits are read through a 64-bit
+// register window W = window bits [wp, wp + 64), reloaded every 32 bits.
 __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t avail, uint32_t max_sym,
-                                uint32_t max_log, uint32_t *tlog, uint32_t *nsym, uint32_t *err)
+                                                uint32_t max_log, uint32_t *tlog, uint32_t *nsym, uint32_t *err)
 {
-    uint32_t pos = 8 * wofs;
-    const uint32_t tl = win_bits(L, pos, 4) + 5;
+    uint32_t pos = 8 * wofs, wp = pos + 64;   // forces the first load
+    uint64_t W = 0;
+    auto bits = [&](uint32_t n) -> uint32_t {   // n <= 16 bits at pos, not consumed
+        if (pos - wp >= 32) {
+            wp = pos & ~31u;
+            const uint32_t d = wp >> 5;
+            const uint32_t lo = d < 64 ? *lp<uint32_t>(L.win + 4 * d) : 0u;
+            const uint32_t hi = d + 1 < 64 ? *lp<uint32_t>(L.win + 4 * d + 4) : 0u;
+            W = ((uint64_t)hi << 32) | lo;
+        }
+        return (uint32_t)(W >> (pos - wp)) & ((1u << n) - 1);
+    };
+    const uint32_t tl = bits(4) + 5;
     pos += 4;
     if (tl > max_log) {
         *err = ZE_CORRUPT;
@@ -198,30 +206,27 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
     int32_t remaining = (1 << tl) + 1, threshold = 1 << tl;
     uint32_t nbits = tl + 1, sym = 0;
     bool prev0 = false;
-    for (uint32_t i = 0; i <= max_sym; i++)
-        L.norm[i] = 0;
     while (remaining > 1 && sym <= max_sym) {
         if (prev0) {
             uint32_t n0 = sym;
-            while (win_bits(L, pos, 16) == 0xFFFF) {
+            while (bits(16) == 0xFFFF) {
                 n0 += 24;
                 pos += 16;
             }
-            while (win_bits(L, pos, 2) == 3) {
+            while (bits(2) == 3) {
                 n0 += 3;
                 pos += 2;
             }
-            n0 += win_bits(L, pos, 2);
+            n0 += bits(2);
             pos += 2;
             if (n0 > max_sym) {
                 *err = ZE_CORRUPT;
                 return 0;
             }
-            while (sym < n0)
-                L.norm[sym++] = 0;
+            sym = n0;   // the skipped counts stay 0
         }
         const int32_t mx = 2 * threshold - 1 - remaining;
-        const int32_t v = (int32_t)win_bits(L, pos, nbits);
+        const int32_t v = (int32_t)bits(nbits);
         int32_t count;
         if ((v & (threshold - 1)) < mx) {
             count = v & (threshold - 1);
@@ -234,7 +239,9 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
         }
         count--;
         remaining -= count < 0 ? -count : count;
-        L.norm[sym++] = (int16_t)count;
+        if (count)
+            *lp<int16_t>(&L.norm[sym]) = (int16_t)count;
+        sym++;
         prev0 = count == 0;
         while (remaining < threshold) {
             nbits--;
@@ -255,53 +262,126 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
     return used;
 }
 
-// Decoding table from norm[0..nsym) with accuracy log tl: symbol spread by
-// lane 0, next states assigned wave-parallel (per 64-cell group, one ballot
-// per distinct symbol, cells ranked in position order).  Wave-wide.
+// norm[0..n) = 0, wave-wide (before read_ncount)
+__device__ __forceinline__ void norm_clear(ZLds &L, uint32_t n)
+{
+    for (uint32_t i = lane_id(); i < n; i += 64)
+        *lp<int16_t>(&L.norm[i]) = 0;
+    wave_lds_sync();
+}
+
+// Decoding table from norm[0..nsym) with accuracy log tl (FSE_buildDTable):
+// cell = symbol | nbits << 8 | base << 16.  Wave-wide.  With nsym <= 64 (every
+// table zstd defines: LL 36, OF 32, ML 53, Huffman weights 13 symbols) it is
+// built without serial loops: the spread visits positions (j * step) & mask
+// and the valid ones (<= high) take the cells in symbol order, so a prefix
+// count over j gives each position its cell and a prefix max over the symbol
+// starts gives each cell its symbol; next states are ranked per 64-cell group
+// by ballots, with the per-symbol counters in lane registers.
 __device__ __forceinline__ void fse_build(ZLds &L, uint32_t *tab, uint32_t nsym, uint32_t tl)
 {
     const uint32_t lane = lane_id();
     const uint32_t size = 1u << tl, mask = size - 1;
+    const uint32_t step = (size >> 1) + (size >> 3) + 3;
+    const uint64_t below = (1ull << lane) - 1;
     wave_lds_sync();   // norm[] from lane 0
-    if (lane == 0) {
-        uint32_t high = size - 1;
-        for (uint32_t s = 0; s < nsym; s++)
-            if (L.norm[s] == -1)
-                *lp<uint32_t>(tab + high--) = s;
-        const uint32_t step = (size >> 1) + (size >> 3) + 3;
-        uint32_t pos = 0;
-        for (uint32_t s = 0; s < nsym; s++) {
-            for (int32_t i = 0; i < L.norm[s]; i++) {
-                *lp<uint32_t>(tab + pos) = s;
-                do
-                    pos = (pos + step) & mask;
-                while (pos > high);
+    if (nsym > 64) {
+        if (lane == 0) {
+            uint32_t high = size - 1;
+            for (uint32_t s = 0; s < nsym; s++)
+                if (L.norm[s] == -1)
+                    *lp<uint32_t>(tab + high--) = s;
+            uint32_t pos = 0;
+            for (uint32_t s = 0; s < nsym; s++) {
+                for (int32_t i = 0; i < L.norm[s]; i++) {
+                    *lp<uint32_t>(tab + pos) = s;
+                    do
+                        pos = (pos + step) & mask;
+                    while (pos > high);
+                }
             }
         }
+        for (uint32_t s = lane; s < nsym; s += 64)
+            L.cnt[s] = L.norm[s] == -1 ? 1u : (uint32_t)L.norm[s];
+        wave_lds_sync();
+        for (uint32_t u0 = 0; u0 < size; u0 += 64) {
+            const uint32_t u = u0 + lane;
+            const bool act = u < size;
+            const uint32_t s = act ? (*lp<uint32_t>(tab + u) & 0xFF) : 0xFFFFu;
+            uint64_t rem = __ballot(act);
+            while (rem) {
+                const uint32_t sj = lane_val(s, __builtin_ctzll(rem));
+                const uint64_t m = __ballot(act && s == sj);
+                const uint32_t base = uni(L.cnt[sj]);
+                if ((m >> lane) & 1) {
+                    const uint32_t ns = base + (uint32_t)__builtin_popcountll(m & below);
+                    const uint32_t nb = tl - (uint32_t)hibit(ns);
+                    *lp<uint32_t>(tab + u) = sj | nb << 8 | ((ns << nb) - size) << 16;
+                }
+                if (lane == 0)
+                    L.cnt[sj] = base + (uint32_t)__builtin_popcountll(m);
+                wave_lds_sync();
+                rem &= ~m;
+            }
+        }
+        return;
     }
-    for (uint32_t s = lane; s < nsym; s += 64)
-        L.cnt[s] = L.norm[s] == -1 ? 1u : (uint32_t)L.norm[s];
+    // lane s: symbol s
+    const int32_t nc = lane < nsym ? (int32_t)*lp<int16_t>(&L.norm[lane]) : 0;
+    const uint32_t c = nc > 0 ? (uint32_t)nc : 0u;
+    const bool low = nc == -1;
+    const uint32_t K = wave_incl_add(c) - c;   // the symbol's first cell in spread order
+    const uint64_t lm = __ballot(low);
+    const uint32_t high = size - 1 - (uint32_t)__builtin_popcountll(lm);
+    for (uint32_t u = lane; u < size; u += 64)
+        *lp<uint16_t>(&L.spr[u]) = 0;
     wave_lds_sync();
+    if (c)
+        *lp<uint16_t>(&L.spr[K]) = (uint16_t)(lane + 1);
+    wave_lds_sync();
+    uint32_t carry = 0;
+    for (uint32_t k0 = 0; k0 < size; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const uint32_t v = k < size ? (uint32_t)*lp<uint16_t>(&L.spr[k]) : 0u;
+        const uint32_t pm = max(carry, wave_incl_max(v));
+        if (k < size)
+            *lp<uint16_t>(&L.spr[k]) = (uint16_t)(pm - 1);
+        carry = lane_val(pm, 63);
+    }
+    wave_lds_sync();
+    uint32_t kb = 0;
+    for (uint32_t j0 = 0; j0 < size; j0 += 64) {
+        const uint32_t j = j0 + lane, p = (j * step) & mask;
+        const bool valid = j < size && p <= high;
+        const uint64_t m = __ballot(valid);
+        if (valid)
+            *lp<uint32_t>(tab + p) = *lp<uint16_t>(&L.spr[kb + (uint32_t)__builtin_popcountll(m & below)]);
+        kb += (uint32_t)__builtin_popcountll(m);
+    }
+    if (low)   // low-probability symbols at the top, in symbol order from size - 1 down
+        *lp<uint32_t>(tab + size - 1 - (uint32_t)__builtin_popcountll(lm & below)) = lane;
+    wave_lds_sync();
+    uint32_t cntr = low ? 1u : c;   // lane s: next state of symbol s
     for (uint32_t u0 = 0; u0 < size; u0 += 64) {
         const uint32_t u = u0 + lane;
         const bool act = u < size;
         const uint32_t s = act ? (*lp<uint32_t>(tab + u) & 0xFF) : 0xFFFFu;
         uint64_t rem = __ballot(act);
         while (rem) {
-            const uint32_t sj = lane_val(s, __builtin_ctzll(rem));
+            const uint32_t sj = uni(lane_val(s, __builtin_ctzll(rem)));
             const uint64_t m = __ballot(act && s == sj);
-            const uint32_t base = uni(L.cnt[sj]);
+            const uint32_t base = lane_val(cntr, (int)sj);
             if ((m >> lane) & 1) {
-                const uint32_t ns = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+                const uint32_t ns = base + (uint32_t)__builtin_popcountll(m & below);
                 const uint32_t nb = tl - (uint32_t)hibit(ns);
                 *lp<uint32_t>(tab + u) = sj | nb << 8 | ((ns << nb) - size) << 16;
             }
-            if (lane == 0)
-                L.cnt[sj] = base + (uint32_t)__builtin_popcountll(m);
-            wave_lds_sync();
+            if (lane == sj)
+                cntr += (uint32_t)__builtin_popcountll(m);
             rem &= ~m;
         }
     }
+    wave_lds_sync();
 }
 
 // ---- Huffman tables --------------------------------------------------------------
@@ -320,6 +400,7 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
             return 0;
         uint32_t tl = 0, nsym = 0;
         uint32_t hs = 0;
+        norm_clear(L, 256);
         if (lane == 0)
             hs = read_ncount(L, wofs, hb, 255, 6, &tl, &nsym, &err);
         hs = uni(hs);
@@ -701,6 +782,7 @@ __device__ __forceinline__ uint32_t seq_table(ZLds &L, Frame &F, uint32_t t, uin
     if (mode == 2) {
         const uint32_t wx = stage_win(L, F.I, p);
         uint32_t tl = 0, nsym = 0, e = 0, used = 0;
+        norm_clear(L, max_sym + 1);
         if (lane == 0)
             used = read_ncount(L, F.I.s0 + p - wx, avail, max_sym, max_log, &tl, &nsym, &e);
         if (uni(e) || uni(used) == 0) {
