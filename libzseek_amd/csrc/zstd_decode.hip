@@ -386,7 +386,7 @@ __device__ __forceinline__ void fse_build(ZLds &L, uint32_t *tab, uint32_t nsym,
 
 // ---- Huffman tables --------------------------------------------------------------
 // Tree description at frame offset p (window staged at wx); returns its size
-// or 0 on error.  Writes the 2^log decoding cells (symbol | nbits << 8) to
+// or 0 on error.  Writes the 2^log decoding cells (nbits | symbol << 8) to
 // cells (HBM); *log receives the table log.  Wave-wide.
 __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, uint32_t p, uint32_t avail,
                                              uint32_t *log, uint16_t *cells)
@@ -523,9 +523,9 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
         if (!n)
             continue;
         wave_lds_sync();
-        const uint32_t sh = k - 1, ck = n << sh, nb = (lg + 1 - k) << 8;
+        const uint32_t sh = k - 1, ck = n << sh, nb = lg + 1 - k;
         for (uint32_t u = lane; u < ck; u += 64)
-            cells[c0 + u] = (uint16_t)((uint32_t)*lp<int16_t>(&L.norm[u >> sh]) | nb);
+            cells[c0 + u] = (uint16_t)((uint32_t)*lp<int16_t>(&L.norm[u >> sh]) << 8 | nb);
         c0 += ck;
         wave_lds_sync();   // before the list is rewritten
     }
@@ -1320,15 +1320,6 @@ __device__ __forceinline__ void br_fill(BRd &b)
     b.pos = need ? p2 : b.pos;
 }
 
-// n (<= 31) bits, consumed
-__device__ __forceinline__ uint32_t br_read(BRd &b, uint32_t n)
-{
-    br_fill(b);
-    const uint32_t v = (uint32_t)(b.C >> (uint32_t)(b.nb - (int32_t)n)) & ((1u << n) - 1);
-    b.nb -= (int32_t)n;
-    return v;
-}
-
 // stream bits not consumed yet (< 0 once read past the start)
 __device__ __forceinline__ int32_t br_left(const BRd &b)
 {
@@ -1336,20 +1327,24 @@ __device__ __forceinline__ int32_t br_left(const BRd &b)
 }
 
 // ---- Huffman literals: one lane per stream -------------------------------------------
-// 16 blocks (64 streams) per wave; their tables packed into 16 KiB of LDS when
-// they fit (else read from the slots).  A lane refills its bit container every
-// G symbols (G * lg <= 32) and stores 16 decoded bytes at a time, aligned.
+// 16 blocks (64 streams) per wave; their tables packed into LDS when they fit
+// (else read from the slots).  Cells are nbits | symbol << 8.  In the main
+// loop a lane refills its bit container every G symbols (G * lg <= 32) and
+// decodes those G symbols from a 32-bit MSB-first window w of the
+// container's top bits: index = w >> (32 - lg), consume = w <<= cell (the
+// shift takes the cell's low 5 bits, nbits).  16 decoded bytes are stored at
+// a time, aligned.
 constexpr uint32_t kHufLdsCells = 2048;
 
-template <int G, int F, typename Tab>
+template <int G, int F, int DIAG, typename Tab>
 __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *out, uint64_t dst, uint32_t cnt,
                                            uint32_t lim)
 {
-    const uint32_t mask = (1u << lg) - 1;
+    const uint32_t mask = (1u << lg) - 1, sh = 32 - lg;
     auto one = [&]() -> uint32_t {
         const uint32_t e = T((uint32_t)(b.C >> (uint32_t)(b.nb - (int32_t)lg)) & mask);
-        b.nb -= (int32_t)(e >> 8);
-        return e & 0xFF;
+        b.nb -= (int32_t)(e & 0xFF);
+        return e >> 8;
     };
     uint32_t i = 0;
     // head (< 16 symbols, <= 180 bits): the ring holds kRS - 1 chunks after br_init
@@ -1366,20 +1361,29 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     u32x4 prev = {0, 0, 0, 0};
     const uint32_t i0 = i;
     while (i + 16 <= lim) {
-        br_step<F>(b);
-        if (i != i0)
+        if (!(DIAG & 2))
+            br_step<F>(b);
+        if (i != i0 && !(DIAG & 1))
             *reinterpret_cast<u32x4 *>(out + i - 16) = prev;
         u32x4 acc = {0, 0, 0, 0};
+        uint32_t w = 0, used = 0;
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            if (k % G == 0)
+            if (k % G == 0) {
+                b.nb -= (int32_t)used;
                 br_fill(b);
-            const uint32_t s = one();
+                w = (uint32_t)(b.C >> (uint32_t)(b.nb - 32));
+                used = 0;
+            }
+            const uint32_t e = (DIAG & 4) ? (w >> 26) << 8 | 6u : T(w >> sh);
+            w <<= (e & 31);   // nbits
+            used += e & 0xFF;
             if ((k & 3) == 0)
-                acc[k >> 2] = s;
+                acc[k >> 2] = e >> 8;
             else
-                acc[k >> 2] |= s << (8 * (k & 3));
+                acc[k >> 2] |= (e >> 8) << (8 * (k & 3));
         }
+        b.nb -= (int32_t)used;
         prev = acc;
         i += 16;
     }
@@ -1395,6 +1399,9 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     }
 }
 
+__device__ unsigned int g_hdiag[32];   // diagnostic builds: waves per lgmax, LDS / global path
+
+template <int DIAG>
 __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
                                                       const uint8_t *__restrict__ comp,
                                                       const uint8_t *__restrict__ slots,
@@ -1415,6 +1422,10 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
     const uint32_t incl = wave_incl_add(cells);
     const uint32_t first = (uint32_t)__shfl((int)(incl - cells), (int)(lane & ~3u), 64);
     const bool in_lds = lane_val(incl, 63) <= kHufLdsCells;
+    // the longest streams (a literal-only 64 KiB block: 16 Ki symbols each,
+    // ~2.5x the usual) bound the kernel: their waves issue first
+    if (lane_val(wave_incl_max(act ? J.cnt : 0u), 63) > 12000)
+        __builtin_amdgcn_s_setprio(3);
     if (in_lds) {
         for (uint32_t b = 0; b < 16; b++) {
             const uint32_t nc = lane_val(cells, 4 * b);
@@ -1430,6 +1441,10 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
     // one resource over the wave's streams (else lane by lane, each its own)
     const uint64_t lo = uni64(wave_min64(act ? J.src : ~0ull)) & ~15ull;
     const uint64_t hi = uni64(wave_max64(act ? J.src + J.len : 0ull));
+    if (DIAG && lane == 0) {
+        atomicAdd(&g_hdiag[lgmax & 15], 1u);
+        atomicAdd(&g_hdiag[16 + (in_lds ? 1 : 0)], 1u);
+    }
     if (j >= nj)
         return;
     bool bad = false;
@@ -1441,13 +1456,13 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
             const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(&tabs[first]);
             auto T = [&](uint32_t i) -> uint32_t { return *la<uint16_t>(tb + 2 * i); };
             if (lgmax <= 8)
-                huf_stream<4, 1>(b, T, jlg, out, J.dst, J.cnt, J.lim);
+                huf_stream<4, 1, DIAG>(b, T, jlg, out, J.dst, J.cnt, J.lim);
             else
-                huf_stream<2, 2>(b, T, jlg, out, J.dst, J.cnt, J.lim);
+                huf_stream<2, 2, DIAG>(b, T, jlg, out, J.dst, J.cnt, J.lim);
         } else {
             const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)jslot * kZSlot);
             auto T = [&](uint32_t i) -> uint32_t { return gt[i]; };
-            huf_stream<2, 2>(b, T, jlg, out, J.dst, J.cnt, J.lim);
+            huf_stream<2, 2, DIAG>(b, T, jlg, out, J.dst, J.cnt, J.lim);
         }
         bad = bad || br_left(b) != 0;
     };
@@ -1470,9 +1485,9 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
 // Replays the frame's op list: FSE states (tables from the block slots),
 // repeat offsets, every libzstd check, items in the LZ4 item format with the
 // full offset; then the final status, item count and checksum request.
-// Items of one lane, staged in LDS (16 per lane, item j of lane l at
-// stage + (j & 15) * 512 + 8 * l) and flushed to the frame's slots 8 or more
-// at a time: no item store is pending at the next ring commit's wait.
+// Items of one lane, staged in LDS (8 per lane, item j of lane l at
+// stage + (j & 7) * 256 + 8 * l) and flushed to the frame's slots 4 or more
+// at a time.
 struct LSink {
     uint64_t *base;
     uint32_t k, f, cap;
@@ -1481,7 +1496,7 @@ struct LSink {
 
 __device__ __forceinline__ void lput(LSink &S, uint64_t v)
 {
-    *la<uint64_t>(S.stage + (S.k & 15) * 512) = v;
+    *la<uint64_t>(S.stage + (S.k & 7) * 256) = v;
     S.k++;
 }
 
@@ -1508,24 +1523,115 @@ __device__ __forceinline__ bool lemit(LSink &S, uint32_t src, uint32_t lit, uint
 __device__ __forceinline__ void lflush(LSink &S)
 {
     for (uint32_t j = S.f; j < S.k; j++)
-        S.base[j] = *la<uint64_t>(S.stage + (j & 15) * 512);
+        S.base[j] = *la<uint64_t>(S.stage + (j & 7) * 256);
     S.f = S.k;
 }
 
 __device__ __forceinline__ void lmaybe(LSink &S)
 {
-    if (S.k - S.f >= 8)
+    if (S.k - S.f >= 4)
         lflush(S);
 }
 
-__device__ __forceinline__ uint32_t fse_next(BRd &b, uint32_t e, uint32_t tl)
+// Sequence bitstream reader, no ring: at each sequence the lane loads the 16
+// bytes (4 dwords) just below its cursor together with the sequence's table
+// cells — one wait covers both — and consumes from registers: C = the top
+// two dwords, two reserve dwords shifted in by fills.  A sequence reads at
+// most 89 bits; the window holds at least 97 below the cursor.  Coordinates
+// are bits from the stream's dword-aligned base x0; bits below the stream's
+// first byte (xs) read as 0.
+struct SRd {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t x0;
+    int32_t xs;
+    int32_t cur;        // stream bits below cur are unread
+    uint64_t C;         // bits [base, base + 64)
+    int32_t base, nb;   // nb = cur - base valid bits at the bottom of C
+    uint32_t r1, r0;    // the two dwords below C
+};
+
+// len >= 1.  False when the stream's last byte (its end mark) is 0.
+__device__ __forceinline__ bool sr_init(SRd &b, __amdgpu_buffer_rsrc_t r, uint32_t x, uint32_t len)
+{
+    b.r = r;
+    b.x0 = x & ~3u;
+    b.xs = 8 * (int32_t)(x & 3u);
+    const uint32_t rel = (x & 3u) + len;
+    const uint32_t last = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, b.x0 + rel - 1, 0, 0);
+    b.cur = 8 * (int32_t)(rel - 1) + (last ? 31 - __builtin_clz(last) : 0);
+    return last != 0;
+}
+
+__device__ __forceinline__ uint32_t sr_dw(const SRd &b, int32_t k)
+{
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(b.r, k >= 0 ? b.x0 + 4u * (uint32_t)k : kOOR, 0, 0);
+}
+
+// the window below the cursor (issued with the step's table loads)
+__device__ __forceinline__ void sr_load(SRd &b)
+{
+    const int32_t D = (b.cur + 31) >> 5, k0 = D - 4;   // dwords [k0, D) hold bits [32 k0, 32 D)
+    u32x4 w;
+    if (k0 >= 0) {
+        w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(b.r, b.x0 + 4u * (uint32_t)k0, 0, 0));
+    } else {   // near the stream's base: dwords below it read as 0
+        w.x = sr_dw(b, k0);
+        w.y = sr_dw(b, k0 + 1);
+        w.z = sr_dw(b, k0 + 2);
+        w.w = sr_dw(b, k0 + 3);
+    }
+    if (k0 <= 0) {   // dword 0 holds the stream's first byte: clear the bits below it
+        w.x &= above(b.xs, 32 * k0);
+        w.y &= above(b.xs, 32 * k0 + 32);
+        w.z &= above(b.xs, 32 * k0 + 64);
+        w.w &= above(b.xs, 32 * k0 + 96);
+    }
+    b.C = (uint64_t)w.w << 32 | w.z;
+    b.base = 32 * (D - 2);
+    b.nb = b.cur - b.base;   // 33..64
+    b.r1 = w.y;
+    b.r0 = w.x;
+}
+
+__device__ __forceinline__ void sr_fill(SRd &b)
+{
+    const bool need = b.nb < 32;
+    b.C = need ? (b.C << 32) | b.r1 : b.C;
+    b.r1 = need ? b.r0 : b.r1;
+    b.nb = need ? b.nb + 32 : b.nb;
+    b.base = need ? b.base - 32 : b.base;
+}
+
+// n (<= 32) bits; nb >= n
+__device__ __forceinline__ uint32_t sr_take(SRd &b, uint32_t n)
+{
+    const uint32_t v = (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)n) & 63)) & (uint32_t)((1ull << n) - 1);
+    b.nb -= (int32_t)n;
+    return v;
+}
+
+// close the sequence: the cursor moves past what was consumed
+__device__ __forceinline__ void sr_done(SRd &b)
+{
+    b.cur = b.base + b.nb;
+}
+
+__device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 {
     const uint32_t ns = e >> 6;
     const uint32_t nbits = tl + (uint32_t)__builtin_clz(ns) - 31;
-    return ((ns << nbits) - (1u << tl)) + br_read(b, nbits);
+    return ((ns << nbits) - (1u << tl)) + sr_take(b, nbits);
 }
 
-__global__ __launch_bounds__(256) void zstd_seq_kernel(
+// 32 frames per wave (lanes 32..63 idle), one wave per workgroup: each
+// frame's three FSE tables are copied into 1600 bytes of LDS when they fit
+// (else read from the slot), so the per-sequence lookups stay on chip; with
+// three such workgroups per CU the LDS, not the lanes, sets how many frames
+// are in flight.
+constexpr uint32_t kSeqLanes = 32;
+constexpr uint32_t kSeqCells = 800;   // u16 cells per frame (768 + copy slack)
+
+__global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
     const uint8_t *__restrict__ slots, const uint8_t *__restrict__ hbad,
@@ -1533,13 +1639,14 @@ __global__ __launch_bounds__(256) void zstd_seq_kernel(
     int32_t *__restrict__ status, uint64_t *__restrict__ ck)
 {
     __shared__ uint32_t codes[89];
-    __shared__ __attribute__((aligned(16))) uint8_t rings[4][kRS * 1024];
-    __shared__ __attribute__((aligned(16))) uint64_t stage[4][16 * 64];
-    for (uint32_t i = threadIdx.x; i < 89; i += 256)
+    __shared__ __attribute__((aligned(16))) uint64_t stage[8 * kSeqLanes];
+    __shared__ __attribute__((aligned(16))) uint16_t ftab[kSeqLanes * kSeqCells];
+    for (uint32_t i = threadIdx.x; i < 89; i += 64)
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
     __syncthreads();
-    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
-    const bool act = f < n;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t f = blockIdx.x * kSeqLanes + lane;
+    const bool act = lane < kSeqLanes && f < n;
     FrameDesc d = {0, 0, 0, 0};
     if (act)
         d = desc[f];
@@ -1556,7 +1663,8 @@ __global__ __launch_bounds__(256) void zstd_seq_kernel(
     S.base = items + rb;
     S.k = S.f = 0;
     S.cap = (uint32_t)(rec_base[f + 1] - rb);
-    S.stage = (uint32_t)(uintptr_t)lp<uint64_t>(&stage[threadIdx.x >> 6][threadIdx.x & 63]);
+    S.stage = (uint32_t)(uintptr_t)lp<uint64_t>(&stage[lane]);
+    uint16_t *const mytab = &ftab[lane * kSeqCells];
     const uint32_t cap = d.d_size;
     uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
     uint64_t c = 0;
@@ -1574,28 +1682,48 @@ __global__ __launch_bounds__(256) void zstd_seq_kernel(
                 uint32_t lp_ = P.d;
                 const uint32_t le = P.d + P.e;
                 if (nseq) {
-                    BRd b;
-                    if (P.c == 0 || !br_init(b, r, (uint32_t)(d.c_off - base) + P.b, P.c,
-                                              (uint32_t)(uintptr_t)lp<uint8_t>(rings[threadIdx.x >> 6]) +
-                                                  4 * (threadIdx.x & 63))) {
+                    SRd b;
+                    if (P.c == 0 || !sr_init(b, r, (uint32_t)(d.c_off - base) + P.b, P.c)) {
                         err = ZE_CORRUPT;
                     } else {
                         const uint32_t tll = P.g & 15, tof = (P.g >> 4) & 15, tml = (P.g >> 8) & 15;
-                        const uint16_t *T = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
-                        uint32_t sll = br_read(b, tll), sof = br_read(b, tof), sml = br_read(b, tml);
+                        // the block's tables into this lane's LDS cells when they
+                        // fit: LL, OF, ML back to back (16-byte copies)
+                        const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
+                        const uint32_t nll = 1u << tll, nof = 1u << tof, nml = 1u << tml;
+                        const uint16_t *TL = gt + kFseOff[0], *TO = gt + kFseOff[1], *TM = gt + kFseOff[2];
+                        if (nll + nof + nml <= 768) {
+                            auto cp = [&](const uint16_t *src, uint32_t at, uint32_t cells) {
+                                for (uint32_t c = 0; c < cells; c += 8)
+                                    *reinterpret_cast<u32x4 *>(mytab + at + c) = *reinterpret_cast<const u32x4 *>(src + c);
+                            };
+                            cp(TL, 0, nll);
+                            cp(TO, nll, nof);
+                            cp(TM, nll + nof, nml);
+                            TL = mytab;
+                            TO = mytab + nll;
+                            TM = mytab + nll + nof;
+                        }
+                        sr_load(b);
+
+                        uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
+                        sr_done(b);
                         for (uint32_t i = 0; i < nseq; i++) {
-                            br_step(b);
-                            const uint32_t ell = T[kFseOff[0] + sll], eof = T[kFseOff[1] + sof],
-                                           eml = T[kFseOff[2] + sml];
+                            const uint32_t ell = TL[sll], eof = TO[sof], eml = TM[sml];
+                            sr_load(b);
                             const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
                             if (llc > 35 || ofc > 31 || mlc > 52) {
                                 err = ZE_CORRUPT;
                                 break;
                             }
-                            const uint64_t ofv = (1ull << ofc) + br_read(b, ofc);
+                            // offset bits (<= 31; the window holds >= 33), a fill before
+                            // the ML + LL extra bits (<= 32) and one before the three
+                            // state updates (<= 26)
+                            const uint64_t ofv = (1ull << ofc) + sr_take(b, ofc);
                             const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
-                            const uint32_t ml = (mlcode & 0xFFFFFF) + br_read(b, mlcode >> 24);
-                            const uint32_t ll = (llcode & 0xFFFFFF) + br_read(b, llcode >> 24);
+                            sr_fill(b);
+                            const uint32_t ml = (mlcode & 0xFFFFFF) + sr_take(b, mlcode >> 24);
+                            const uint32_t ll = (llcode & 0xFFFFFF) + sr_take(b, llcode >> 24);
                             uint64_t off;
                             if (ofv > 3) {
                                 off = ofv - 3;
@@ -1616,9 +1744,11 @@ __global__ __launch_bounds__(256) void zstd_seq_kernel(
                                     rep0 = (uint32_t)off;
                                 }
                             }
+                            sr_fill(b);
                             sll = fse_next(b, ell, tll);
                             sml = fse_next(b, eml, tml);
                             sof = fse_next(b, eof, tof);
+                            sr_done(b);
                             if ((uint64_t)o + ll + ml > cap)
                                 err = ZE_DST_SMALL;
                             else if (le - lp_ < ll)
@@ -1633,7 +1763,7 @@ __global__ __launch_bounds__(256) void zstd_seq_kernel(
                             lp_ += ll;
                             o += ll + ml;
                         }
-                        if (!err && br_left(b) > 0)
+                        if (!err && b.cur - b.xs > 0)
                             err = ZE_CORRUPT;
                     }
                 }
@@ -1685,7 +1815,7 @@ __global__ __launch_bounds__(256) void zstd_seq_kernel(
             const int l = __builtin_ctzll(m);
             const uint64_t s0 = uni64(__shfl(d.c_off, l, 64)) & ~15ull;
             const uint64_t s1 = uni64(__shfl(d.c_off + d.c_size, l, 64));
-            if ((int)(threadIdx.x & 63) == l)
+            if ((int)lane == l)
                 replay(span_rsrc(comp, s0, s1 - s0), s0);
         }
     }
@@ -1898,10 +2028,32 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     hipLaunchKernelGGL(zstd_frame_kernel, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc,
                        nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops,
                        s->slots, s->hjobs);
-    if (nj)
-        hipLaunchKernelGGL(zstd_huf_kernel, dim3((nj + 63) / 64), dim3(64), 0, stream, s->hjobs, nj, d_comp,
-                           s->slots, s->lit, s->hbad);
-    hipLaunchKernelGGL(zstd_seq_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc, nframes,
+    if (nj) {
+        static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
+        const dim3 g((nj + 63) / 64), b(64);
+        if (diag) {
+            unsigned int z[32] = {};
+            (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+        }
+        switch (diag) {
+        case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        case 7: hipLaunchKernelGGL(zstd_huf_kernel<7>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        default: hipLaunchKernelGGL(zstd_huf_kernel<8>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        }
+        if (diag) {
+            unsigned int z[32] = {};
+            (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_hdiag), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+            (void)hipStreamSynchronize(stream);
+            fprintf(stderr, "huf diag %d: lgmax", diag);
+            for (int i = 0; i < 16; i++)
+                if (z[i])
+                    fprintf(stderr, " %d:%u", i, z[i]);
+            fprintf(stderr, "  global %u lds %u\n", z[16], z[17]);
+        }
+    }
+    hipLaunchKernelGGL(zstd_seq_kernel, dim3((nframes + kSeqLanes - 1) / kSeqLanes), dim3(64), 0, stream, d_desc, nframes,
                        d_comp, s->ops, s->blk_base, s->slots, s->hbad, s->rec_base, s->items, s->nitems,
                        d_status, s->ck);
     stage_mark(2, stream);
