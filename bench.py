@@ -171,7 +171,7 @@ def main():
     kname = "zstd_frame_kernel" if zstd else z.lib().zsk_lz4_kernel_name(nfr).decode()
     stages = None
     if n_timed:
-        names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel",
+        names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel + zstd_huf_kernel + zstd_seq_kernel",
                   "execute": "seq_exec_kernel", "hand-off": "zstd_check_kernel"} if zstd else
                  {"plan": "lz4_plan_kernel", "parse": "lz4_scan_kernel", "execute": kname,
                   "hand-off": "lz4_wave_kernel<4096, 4, true>"})
@@ -256,15 +256,15 @@ def traffic_from_profile(kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by scripts/round_profiles.py), used
     only when it was recorded for the kernel this build launches."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(p) as f:
-            rec = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if kernel not in rec.get("kernel", ""):
-        return None
-    return rec.get("hbm_bytes_per_launch")
+    for name in ("pmc_traffic.json", "pmc_traffic_zstd.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if kernel in rec.get("kernel", ""):
+            return rec.get("hbm_bytes_per_launch")
+    return None
 
 
 def cpu_baseline(img, size, frame, threads):

@@ -17,6 +17,9 @@
  *                            frame_size_c/d, seek_table.c:204-226.
  *   zsk_pread_device       — zseek_pread (decompress.c:806-824) with the
  *                            decoded bytes left in device memory.
+ *   zsk_verify_frame_checksums — the seek table's per-frame checksum,
+ *                            parsed by seek_table.c:95-97 and never checked
+ *                            there, checked on the GPU.
  */
 #ifndef ZSEEK_HIP_H
 #define ZSEEK_HIP_H
@@ -128,6 +131,30 @@ ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader,
  * env ZSEEK_HIP_BATCH_BYTES overrides at open). */
 ZSEEK_EXPORT bool zsk_reader_set_batch_bytes(zseek_reader_t *reader,
     size_t bytes);
+
+/*
+ * Seek-table frame checksums.  The seekable format's optional per-frame
+ * checksum (descriptor bit 7; 12-byte entries cSize, dSize, checksum,
+ * seek_table.c:95-97 / writer :392-396) is the low 32 bits of XXH64(seed 0)
+ * of the frame's decoded bytes; the reference parses it and never checks it.
+ *
+ * zsk_verify_frame_checksums: for every frame whose d_status is ZSK_OK, hash
+ * d_out[d_off, d_off + d_size) on the GPU and set its status to
+ * ZSK_ERR_SEEK_CHECKSUM when the low 32 bits differ from d_checksums[f]
+ * (device array, one u32 per frame).  Asynchronous on @stream; 0 or -1.
+ */
+#define ZSK_ERR_SEEK_CHECKSUM 104
+ZSEEK_EXPORT int zsk_verify_frame_checksums(const zsk_frame_desc_t *d_desc,
+    uint32_t nframes, const void *d_out, const uint32_t *d_checksums,
+    int32_t *d_status, void *stream);
+
+/* Make a reader check the seek-table checksum of every frame it decodes
+ * (files whose seek table carries them).  Default off, as the reference; env
+ * ZSEEK_VERIFY_CHECKSUMS=1 at open turns it on.  A mismatching frame fails
+ * like a corrupt one: a short read, then -1 and "...: frame checksum
+ * mismatch".  false for a NULL reader. */
+ZSEEK_EXPORT bool zsk_reader_set_verify_checksums(zseek_reader_t *reader,
+    bool on);
 
 #ifdef __cplusplus
 }

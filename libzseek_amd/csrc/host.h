@@ -92,6 +92,8 @@ struct DeviceCtx {
     size_t d_fail_cap = 0;
     uint32_t *h_fail = nullptr;
     size_t h_fail_cap = 0;
+    uint32_t *d_ck = nullptr;     // the batch's seek-table checksums (verification on)
+    size_t d_ck_cap = 0;
     SplitScratch split;            // two-phase decoder scratch (lz4_split.hip)
     ZstdScratch zs;                // zstd decoder scratch (zstd_decode.hip)
     uint64_t batches = 0, frames_decoded = 0, bytes_decoded = 0, bytes_uploaded = 0;

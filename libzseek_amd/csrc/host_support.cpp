@@ -200,6 +200,7 @@ DeviceCtx::~DeviceCtx()
     (void)hipFree(d_desc);
     (void)hipFree(d_status);
     (void)hipFree(d_fail);
+    (void)hipFree(d_ck);
     split_scratch_free(&split);
     zstd_scratch_free(&zs);
     (void)hipHostFree(h_fail);
@@ -276,7 +277,8 @@ bool DeviceCtx::reserve(size_t comp, size_t out, size_t nframes, char *errbuf)
     (void)hipSetDevice(device);
     if (!grow_dev(&d_comp, &d_comp_cap, comp) || !grow_dev(&d_out, &d_out_cap, out) ||
         !grow_dev(&d_desc, &d_desc_cap, nframes) ||
-        !grow_dev(&d_status, &d_status_cap, nframes) || !grow_dev(&d_fail, &d_fail_cap, nframes)) {
+        !grow_dev(&d_status, &d_status_cap, nframes) || !grow_dev(&d_fail, &d_fail_cap, nframes) ||
+        !grow_dev(&d_ck, &d_ck_cap, nframes)) {
         set_error(errbuf, "allocate GPU decode buffers failed");
         return false;
     }
@@ -340,6 +342,8 @@ const char *status_name(int32_t st)
         return "truncated frame";
     case ST_UNSUPPORTED:
         return "unsupported frame";
+    case ST_SEEK_CHECKSUM:
+        return "frame checksum mismatch";
     case ST_NOT_RUN:
         return "decoder did not run";
     default:

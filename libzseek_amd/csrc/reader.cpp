@@ -54,6 +54,7 @@ struct zseek_reader {
     FrameCache *cache = nullptr;   // NULL when cache_size == 0 (ref :219-227)
     size_t pos = 0;                // zseek_read cursor (ref :826-835)
     size_t batch_bytes = kDefaultBatch;
+    bool verify = false;   // check seek-table frame checksums (the reference never does)
     DeviceCtx gpu;
 };
 
@@ -134,6 +135,8 @@ extern "C" ZSEEK_EXPORT zseek_reader_t *zseek_reader_open_full(zseek_read_file_t
         delete r;
         return nullptr;
     }
+    const char *vck = getenv("ZSEEK_VERIFY_CHECKSUMS");
+    r->verify = vck && *vck && strcmp(vck, "0") != 0;
     const char *env = getenv("ZSEEK_HIP_BATCH_BYTES");
     if (env && *env) {
         size_t b = strtoull(env, nullptr, 0);
@@ -240,6 +243,15 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
         launch_lz4_split(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
                          g.stream, &g.split) != 0)
         e = hipErrorLaunchFailure;
+    // seek-table checksums (descriptor bit 7) when asked for: XXH64 low 32
+    // bits of every decoded frame, on the GPU (frame_check.hip)
+    if (e == hipSuccess && r->verify && st.checksum_flag) {
+        e = hipMemcpyAsync(g.d_ck, st.checksum.data() + f0, n * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, g.stream);
+        if (e == hipSuccess &&
+            launch_frame_checksums(g.d_desc, (uint32_t)n, g.d_out, g.d_ck, g.d_status, g.stream) != 0)
+            e = hipErrorLaunchFailure;
+    }
     if (e == hipSuccess)
         e = hipMemcpyAsync(g.h_status, g.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost,
                            g.stream);
@@ -602,5 +614,15 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_set_batch_bytes(zseek_reader_t *reader, 
         return false;
     std::lock_guard<std::mutex> guard(reader->lock);
     reader->batch_bytes = bytes;
+    return true;
+}
+
+// Seek-table checksum verification switch (zseek_hip.h).
+extern "C" ZSEEK_EXPORT bool zsk_reader_set_verify_checksums(zseek_reader_t *reader, bool on)
+{
+    if (!reader)
+        return false;
+    std::lock_guard<std::mutex> guard(reader->lock);
+    reader->verify = on;
     return true;
 }

@@ -42,6 +42,7 @@ enum : int32_t {
     ST_SHORT_FRAME = 101,    // frame decodes to less than its seek-table dSize
     ST_TRUNCATED = 102,      // compressed frame ends mid-block
     ST_UNSUPPORTED = 103,
+    ST_SEEK_CHECKSUM = 104,  // decoded frame's XXH64 low 32 bits != its seek-table checksum
     ST_NOT_RUN = 0x7fff,     // status slot never written (launch failed)
     ST_BLOCK_ERR = 200,      // internal: block-level parse failure
     ST_DIRECT_FLAG = 0x10000,
@@ -194,6 +195,12 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
                               hipStream_t stream);
 
 const char *status_name(int32_t st);
+
+// Seek-table checksums (frame_check.hip): frames whose status is ST_OK and
+// whose decoded bytes' XXH64 low 32 bits differ from d_want[f] get
+// ST_SEEK_CHECKSUM.
+int launch_frame_checksums(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_out,
+                           const uint32_t *d_want, int32_t *d_status, hipStream_t stream);
 
 }   // namespace zsk
 

@@ -23,6 +23,7 @@ TOOLS_PATH = os.path.join(HERE, "lib", "libzseek_tools.so")
 ERRBUF = 80
 ZSEEK_ZSTD, ZSEEK_LZ4 = 0, 1
 ZSK_OK = 0
+ZSK_ERR_SEEK_CHECKSUM = 104
 
 WRITE_FN = C.CFUNCTYPE(C.c_bool, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p)
 PREAD_FN = C.CFUNCTYPE(C.c_ssize_t, C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p)
@@ -91,6 +92,7 @@ EXPORTED = [
     "zsk_lz4_decode_frames", "zsk_status_string", "zsk_lz4_kernel_name", "zsk_reader_frames", "zsk_reader_type",
     "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
     "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
+    "zsk_verify_frame_checksums", "zsk_reader_set_verify_checksums",
 ]
 
 _lib = None
@@ -154,6 +156,11 @@ def lib() -> C.CDLL:
     L.zsk_reader_gpu_stats.argtypes = [C.c_void_p, C.POINTER(GpuStatsC)]
     L.zsk_reader_set_batch_bytes.restype = C.c_bool
     L.zsk_reader_set_batch_bytes.argtypes = [C.c_void_p, C.c_size_t]
+    L.zsk_verify_frame_checksums.restype = C.c_int
+    L.zsk_verify_frame_checksums.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_void_p]
+    L.zsk_reader_set_verify_checksums.restype = C.c_bool
+    L.zsk_reader_set_verify_checksums.argtypes = [C.c_void_p, C.c_bool]
     _lib = L
     return L
 
@@ -375,6 +382,10 @@ class Reader:
     def set_batch_bytes(self, n: int) -> None:
         lib().zsk_reader_set_batch_bytes(self._h, n)
 
+    def set_verify_checksums(self, on: bool = True) -> None:
+        """zsk_reader_set_verify_checksums: check seek-table frame checksums."""
+        lib().zsk_reader_set_verify_checksums(self._h, bool(on))
+
     def close(self) -> None:
         if self._h:
             lib().zseek_reader_close(self._h, None, self._err)
@@ -473,6 +484,45 @@ def zstd_decode_frames(desc, comp, out, status, stream: int | None = None) -> No
                                       status.data_ptr(), stream)
     if rc != 0:
         raise ZseekError("zsk_zstd_decode_frames launch failed")
+
+
+def verify_frame_checksums(desc, out, checksums, status, stream: int | None = None) -> None:
+    """zsk_verify_frame_checksums on torch device tensors (async): checksums
+    holds N expected XXH64-low-32 values (int32/uint32); a frame whose status
+    is ZSK_OK and whose decoded bytes hash differently gets
+    ZSK_ERR_SEEK_CHECKSUM."""
+    import torch
+    n = status.numel()
+    if desc.numel() != n * 24 or checksums.numel() != n:
+        raise ValueError("desc must hold 24 bytes and checksums one value per frame")
+    for t in (desc, out, checksums, status):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("verify_frame_checksums needs contiguous device tensors")
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    if lib().zsk_verify_frame_checksums(desc.data_ptr(), n, out.data_ptr(), checksums.data_ptr(),
+                                        status.data_ptr(), stream) != 0:
+        raise ZseekError("zsk_verify_frame_checksums launch failed")
+
+
+def with_frame_checksums(image, checksums) -> np.ndarray:
+    """Copy of a seekable image whose seek table carries per-frame checksums
+    (descriptor bit 7; 12-byte entries cSize, dSize, checksum - the layout
+    ZSTD_seekable_writeSeekTable writes, /root/reference/src/seek_table.c:365-419).
+    `checksums`: one value per frame (low 32 bits kept)."""
+    import struct
+    img = np.frombuffer(image, np.uint8) if isinstance(image, (bytes, bytearray)) else image
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    c_off, d_off = seek_table_of(img)
+    n = len(c_off) - 1
+    ent = np.empty((n, 3), "<u4")
+    ent[:, 0] = np.diff(c_off)
+    ent[:, 1] = np.diff(d_off)
+    ent[:, 2] = np.asarray(checksums, np.uint64) & 0xFFFFFFFF
+    body = ent.tobytes()
+    foot = (struct.pack("<II", 0x184D2A5E, len(body) + 9) + body +
+            struct.pack("<IBI", n, 0x80, 0x8F92EAB1))
+    return np.concatenate([img[: int(c_off[n])], np.frombuffer(foot, np.uint8)])
 
 
 STAGES = ("plan", "parse", "execute", "hand-off")

@@ -2,6 +2,7 @@
 and derive profiles/pmc_traffic.json for bench.py's roofline.traffic.
 
   python scripts/round_profiles.py r01 [gpurun_out/round]
+  python scripts/round_profiles.py r01_zstd gpurun_out/zround   (config 5)
 
 HBM bytes per decode launch = sum over its kernels of 2 x FETCH_SIZE (gfx950
 reports half the bytes of a wide streaming read, MI355X_MICROARCH.md HBM
@@ -36,6 +37,11 @@ KERNEL = bench["roofline"]["kernel"]   # the dominant kernel bench.py reports
 # runs plan + parse + execute + the (normally empty) hand-off pass
 LAUNCH = ("lz4_plan_kernel", "lz4_scan_kernel", "seq_exec_kernel", "lz4_wave_kernel",
           "lz4_lane_kernel", "lz4_parse_kernel", "lz4_exec_kernel")
+ZSTD = "zstd" in bench["metric"]
+if ZSTD:   # zsk_zstd_decode_frames: plan + scan + frame + literal + sequence + execute + check
+    LAUNCH = ("zstd_plan_kernel", "zstd_scan_kernel", "zstd_frame_kernel", "zstd_huf_kernel",
+              "zstd_seq_kernel", "seq_exec_kernel", "zstd_check_kernel")
+OUT = "pmc_traffic_zstd.json" if ZSTD else "pmc_traffic.json"
 
 
 def part(name):
@@ -82,6 +88,6 @@ out = {
     "algorithmic_bytes_per_launch": alg,
     "traffic_over_algorithmic": (2 * fetch + write) / alg,
 }
-json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(dst, OUT), "w"), indent=1)
 shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
 print(json.dumps(out, indent=1))

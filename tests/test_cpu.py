@@ -151,7 +151,7 @@ def _declared_symbols():
 
 def test_library_exports_every_declared_symbol(zs):
     declared = _declared_symbols()
-    assert len(declared) == 22
+    assert len(declared) == 24
     for n in ("zseek_reader_open_full", "zseek_pread", "zseek_writer_close",
               "zsk_lz4_decode_frames"):
         assert n in declared
@@ -283,3 +283,50 @@ def test_seek_table_with_checksums(zs, oracle):
     with zs.Reader(img2, 0) as r:
         c_off, d_off = r.frames()
         assert (d_off == st["d_off"]).all() and (c_off == st["c_off"]).all()
+
+
+def test_oracle_xxh64_matches_xxhash_package(oracle):
+    """The oracle's XXH64 (the checker of the GPU frame checksums) against the
+    independent xxhash package: every tail length and a few frame sizes."""
+    xxhash = pytest.importorskip("xxhash")
+    rng = np.random.default_rng(5)
+    for n in list(range(0, 80)) + [1000, 4096, 65536, 65537, 100003]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert oracle.xxh64(b) == xxhash.xxh64_intdigest(b, seed=0), n
+
+
+def test_with_frame_checksums_layout(zs, oracle):
+    """zs.with_frame_checksums writes the table the oracle's restatement of
+    seek_table.c:62-176 parses, checksums included, and the library opens."""
+    data = zs.synth_buffer(300000)
+    img = zs.lz4_seekable(data, 65536)
+    st = oracle.seek_table(img.tobytes())
+    cks = [oracle.xxh64(data[int(st["d_off"][i]): int(st["d_off"][i + 1])].tobytes()) & 0xFFFFFFFF
+           for i in range(st["frames"])]
+    img2 = zs.with_frame_checksums(img, cks)
+    st2 = oracle.seek_table(img2.tobytes())
+    assert st2["checksum_flag"] and st2["frames"] == st["frames"]
+    assert (st2["checksum"] == np.array(cks, np.uint32)).all()
+    assert (st2["c_off"] == st["c_off"]).all() and (st2["d_off"] == st["d_off"]).all()
+    with zs.Reader(img2, 0) as r:
+        r.set_verify_checksums(True)
+        c_off, d_off = r.frames()
+        assert (d_off == st["d_off"]).all()
+
+
+def test_checksum_table_read_by_reference(zs, oracle, ref):
+    """The reference itself opens and decodes a with_frame_checksums image
+    (12-byte entries, descriptor 0x80)."""
+    data = zs.synth_buffer(300000)
+    img = zs.lz4_seekable(data, 65536)
+    n = oracle.seek_table(img.tobytes())["frames"]
+    img2 = zs.with_frame_checksums(img, [0x01234567 * (i + 1) for i in range(n)]).tobytes()
+    r = ref.open(img2, 0)
+    try:
+        assert r.h, r.error
+        ok, st = r.stats()
+        assert ok and st["frames"] == n
+        got, b = r.pread(1000, 70000)
+        assert got == 1000 and b == data[70000:71000].tobytes()
+    finally:
+        r.close()
