@@ -173,7 +173,7 @@ def main():
     if n_timed:
         names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel + zstd_huf_kernel + zstd_seq_kernel",
                   "execute": "seq_exec_kernel", "hand-off": "zstd_check_kernel"} if zstd else
-                 {"plan": "lz4_plan_kernel", "parse": "lz4_scan_kernel", "execute": kname,
+                 {"plan": "lz4_plan_direct_kernel", "parse": "lz4_scan_kernel", "execute": kname,
                   "hand-off": "lz4_wave_kernel<4096, 4, true>"})
         stages = {k: {"kernel": names[k], "avg_ms": round(v, 4)} for k, v in stage_ms.items()}
     value = dsum * world * args.steps / t_max / 1e9
@@ -195,6 +195,9 @@ def main():
         "config": {"workload": ("config5: zstd 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
                                 "compressed image resident in HBM" if zstd else
                                 "config2: LZ4 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
+                                "compressed image resident in HBM" if args.frame == 64 << 10 else
+                                f"config3 (frame-size sweep): LZ4 {args.frame >> 10}KiB frames, "
+                                f"{args.size / 2**30:g} GiB synthetic per GPU, full-range decode, "
                                 "compressed image resident in HBM"),
                    "frame_bytes": args.frame, "frames_per_gpu": nfr,
                    "decoded_bytes_per_gpu": dsum, "compressed_bytes_per_gpu": comp_bytes,

@@ -312,11 +312,39 @@ __device__ int32_t parse_frame(LaneIn &in, Sink &sink, uint32_t clen, uint32_t d
 }
 
 // ---- plan: per-frame item slot offsets ------------------------------------
+// Slot offsets without a scan (the usual case): when the frames lie in order
+// in the input (c_off[f+1] >= c_off[f] + c_size[f], as in every batch the
+// reader builds), frame f's slots start at ceil4((c_off[f] - c_off[0]) / 8 +
+// 40 f), and the gap to frame f+1 is >= c_size/8 + 37 > slots_of(c_size).  A
+// frame out of order sets *redo, and lz4_plan_kernel scans instead.
+__global__ __launch_bounds__(256) void lz4_plan_direct_kernel(const FrameDesc *__restrict__ desc,
+                                                               uint32_t n, uint64_t *__restrict__ rec_base,
+                                                               uint64_t *__restrict__ total,
+                                                               uint32_t *__restrict__ redo)
+{
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= n)
+        return;
+    const FrameDesc d = desc[f];
+    const uint64_t c0 = desc[0].c_off;
+    const uint64_t r = (((d.c_off - c0) >> 3) + 40ull * f + 3) & ~3ull;
+    rec_base[f] = r;
+    if (d.c_off < c0 || (f + 1 < n && desc[f + 1].c_off < d.c_off + d.c_size))
+        *redo = 1;
+    if (f + 1 == n)
+        *total = r + slots_of(d.c_size);
+}
+
+// Slot offsets by an exclusive scan of slots_of(c_size), one workgroup; runs
+// only when lz4_plan_direct_kernel flagged the batch (*redo != 0).
 __global__ __launch_bounds__(1024) void lz4_plan_kernel(const FrameDesc *__restrict__ desc,
                                                         uint32_t n, uint64_t *__restrict__ rec_base,
-                                                        uint64_t *__restrict__ total)
+                                                        uint64_t *__restrict__ total,
+                                                        const uint32_t *__restrict__ redo)
 {
     __shared__ uint64_t part[1024];
+    if (*redo == 0)
+        return;
     const uint32_t t = threadIdx.x;
     const uint32_t chunk = (n + 1023) / 1024;
     const uint32_t i0 = t * chunk < n ? t * chunk : n;
@@ -667,6 +695,13 @@ uint64_t split_items_needed(const FrameDesc *h_desc, uint32_t n)
     uint64_t s = 0;
     for (uint32_t i = 0; i < n; i++)
         s += slots_of(h_desc[i].c_size);
+    // where lz4_plan_direct_kernel's layout ends (frames in order)
+    if (n && h_desc[n - 1].c_off >= h_desc[0].c_off) {
+        const uint64_t last = (((h_desc[n - 1].c_off - h_desc[0].c_off) >> 3) + 40ull * (n - 1) + 3) & ~3ull;
+        const uint64_t d = last + slots_of(h_desc[n - 1].c_size);
+        if (d > s)
+            s = d;
+    }
     return s;
 }
 
@@ -680,6 +715,8 @@ void split_scratch_free(SplitScratch *s)
         (void)hipFree(s->items);
     if (s->total)
         (void)hipHostFree(s->total);
+    if (s->redo)
+        (void)hipFree(s->redo);
     *s = SplitScratch();
 }
 
@@ -690,6 +727,8 @@ int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipS
             return -1;
         *s->total = 0;
     }
+    if (!s->redo && hipMalloc((void **)&s->redo, sizeof(uint32_t)) != hipSuccess)
+        return -1;
     if (frames > s->frames_cap) {
         uint32_t cap = frames < 4096 ? 4096 : frames;
         (void)hipStreamSynchronize(stream);
@@ -810,14 +849,18 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 {
     if (nframes == 0)
         return 0;
-    if (s->frames_cap < nframes || !s->rec_base)
+    if (s->frames_cap < nframes || !s->rec_base || !s->redo)
         return -1;
     uint64_t *total_dev = nullptr;
     (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
     stage_mark(0, stream);
-    if (stages & 1)
+    if (stages & 1) {
+        (void)hipMemsetAsync(s->redo, 0, sizeof(uint32_t), stream);
+        hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
+                           d_desc, nframes, s->rec_base, total_dev, s->redo);
         hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
-                           s->rec_base, total_dev);
+                           s->rec_base, total_dev, s->redo);
+    }
     stage_mark(1, stream);
     // diag (tuning builds): 0x800 = the first-generation parse kernel,
     // 0x1000 = the first-generation execute kernel (low bits: its variants),

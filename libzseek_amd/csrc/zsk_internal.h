@@ -74,6 +74,7 @@ struct SplitScratch {
     uint32_t *nitems = nullptr;     // [frames_cap]
     uint64_t *items = nullptr;      // [items_cap], 8-byte items
     uint64_t *total = nullptr;      // host-mapped: item slots the last plan needed
+    uint32_t *redo = nullptr;      // device flag: frames out of order, slots by scan
     uint32_t frames_cap = 0;
     uint64_t items_cap = 0;
 };
