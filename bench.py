@@ -168,7 +168,7 @@ def main():
     # one launch = the decode call: its kernels run back to back on the stream
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9
-    kname = "zstd_frame_kernel" if zstd else z.lib().zsk_lz4_kernel_name(nfr).decode()
+    kname = "zstd_seq_kernel" if zstd else z.lib().zsk_lz4_kernel_name(nfr).decode()
     stages = None
     if n_timed:
         names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel + zstd_huf_kernel + zstd_seq_kernel",

@@ -855,7 +855,9 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
     stage_mark(0, stream);
     if (stages & 1) {
-        (void)hipMemsetAsync(s->redo, 0, sizeof(uint32_t), stream);
+        // env ZSEEK_PLAN_SCAN=1 forces the scan layout (A/B runs)
+        static const int force_scan = getenv("ZSEEK_PLAN_SCAN") ? 1 : 0;
+        (void)hipMemsetAsync(s->redo, force_scan, sizeof(uint32_t), stream);
         hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, s->rec_base, total_dev, s->redo);
         hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
