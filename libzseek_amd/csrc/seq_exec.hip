@@ -249,6 +249,70 @@ __device__ __forceinline__ void copy_desc(const Stage &S, const Out &O, const Sp
     }
 }
 
+// copy_desc with cheaper descriptor generation: one base descriptor per run
+// (literal, match); piece o of a run is base + o * (1 + 2^32) — its source and
+// its stage destination advance together — and a match piece's kind turns
+// from HBM to stage once its source reaches `flushed`.  Same descriptors,
+// same loads and writes as copy_desc.
+template <int DIAG>
+__device__ __forceinline__ void copy_desc2(const Stage &S, const Out &O, const Span &lsp,
+                                           uint32_t descs, uint32_t flushed, uint32_t lane,
+                                           uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
+                                           uint32_t mb, uint32_t mn)
+{
+    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
+    const uint32_t inc = wave_incl_add(np);
+    const uint32_t T = lane_val(inc, 63);
+    if (T == 0)
+        return;
+    const uint32_t x = inc - np;
+    const uint64_t dl = ((uint64_t)((saddr(S, op) - S.base) | (lit < 16 ? lit : 16) << 16 | K_LIT << 24) << 32) | src;
+    const uint64_t dm = ((uint64_t)((saddr(S, mb) - S.base) | (mn < 16 ? mn : 16) << 16 | K_HBM << 24) << 32) | msrc;
+    const uint32_t lm = lit < 16 ? 0 : lit - 16, mm = mn < 16 ? 0 : mn - 16;
+    uint32_t a = descs + 8 * x;
+    for (uint32_t i = 0; __ballot(i < np); i++) {
+        if (i < np) {
+            const bool isl = i < lpn;
+            const uint32_t o = min(16 * (isl ? i : i - lpn), isl ? lm : mm);
+            uint64_t D = (isl ? dl : dm) + (uint64_t)o * 0x100000001ull;
+            if (!isl && msrc + o + 16 > flushed)
+                D += (uint64_t)(K_STAGE - K_HBM) << 56;
+            *lp<uint64_t>(a) = D;
+        }
+        a += 8;
+    }
+    wave_lds_sync();
+    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
+        u32x4 vl[4], vm[4];
+        uint32_t dw[4], sx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t t = t0 + 64 * j + lane;
+            const bool on = t < T;
+            const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
+            sx[j] = (uint32_t)D;
+            dw[j] = on ? (uint32_t)(D >> 32) : 0;
+            const uint32_t kind = dw[j] >> 24;
+            vl[j] = bload16(lsp.r, on && kind == K_LIT && !(DIAG & 1) ? lsp.s0 + sx[j] : kBad);
+            vm[j] = bload16(O.sp.r, on && kind == K_HBM && !(DIAG & 1) ? O.sp.s0 + sx[j] : kBad);
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t n = (dw[j] >> 16) & 0xFF;
+            if (n) {
+                u32x4 v = vl[j] | vm[j];   // the disabled load returned zeros
+                if ((dw[j] >> 24) == K_STAGE)
+                    v = lds16(saddr(S, sx[j]));
+                lds_put(S.base + (dw[j] & 0xFFFF), v, n);
+            }
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+    }
+}
+
 // copy_desc with piece-parallel descriptors: instead of each lane looping
 // over its own pieces (as many steps as the batch's longest run), each lane
 // writes its two runs to a table, marks its first piece in an owner array,
@@ -436,7 +500,8 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 
 // DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores
 // MODE: 0 = lane-owned copies and frontier readiness (v3), 1 = piece
-// descriptors (v4), 2 = piece-parallel descriptors (v5); 1 and 2 use exact
+// descriptors (v4), 2 = piece-parallel descriptors (v5), 3 = descriptors from
+// one base per run (v12, the default); 1, 2 and 3 use exact
 // readiness
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
@@ -567,7 +632,9 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if (MODE == 2)
+        if (MODE == 3)
+            copy_desc2<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
+        else if (MODE == 2)
             copy_scan<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
         else if (MODE == 1)
             copy_desc<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
@@ -673,6 +740,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 9: ZSK_XB(1, 0, 3072); break;
     case 10: ZSK_XB(1, 0, 2048); break;
     case 11: ZSK_X(2, 0); break;
+    case 12: ZSK_X(3, 0); break;
     case 8: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
@@ -700,7 +768,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<1, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<3, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
