@@ -663,6 +663,7 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 75: return launch_lz4_split_stages(15, 0x20B, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 76: return launch_lz4_split_stages(4, 0x20B, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 77: return launch_lz4_split_stages(15, 0x20C, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 79: return launch_lz4_split_stages(15, 0x20D, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 78: return launch_lz4_split_stages(15, 0x204, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 60: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 38: return launch_lz4_split_stages(7, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);

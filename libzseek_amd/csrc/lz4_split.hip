@@ -868,7 +868,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     // 0x1000 = the first-generation execute kernel (low bits: its variants),
     // 0x400 = the scan's if/return fast path,
     // 0x200/0x201 = LDS-ring staged execute v1/v2, 0x203..0x20A = seq_exec
-    // versions; 0 = the production pair lz4_scan_kernel + seq_exec v12
+    // versions; 0 = the production pair lz4_scan_kernel + seq_exec v13
     const bool old_parse = (diag & 0x800) != 0, old_exec = (diag & 0x1000) != 0;
     const int xd = diag & 0x3FF;
     if ((stages & 2) && !old_parse)
@@ -879,7 +879,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                            d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                            s->nitems, d_status, d_fail_at);
     stage_mark(2, stream);
-    if ((stages & 4) && !old_exec && xd >= 0x203 && xd <= 0x20C) {
+    if ((stages & 4) && !old_exec && xd >= 0x203 && xd <= 0x20D) {
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
                         stream, xd & 0xF);
     } else if ((stages & 4) && !old_exec && (xd == 0x200 || xd == 0x201)) {
@@ -887,7 +887,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                               d_status, stream, xd == 0x201 ? 2 : 1);
     } else if ((stages & 4) && !old_exec) {
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                        stream, 12);
+                        stream, 13);
     } else if (stages & 4) {
         const dim3 grid((nframes + kExecWaves - 1) / kExecWaves), block(64 * kExecWaves);
 #define ZSK_EXEC(D, O)                                                                          \

@@ -501,7 +501,8 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores
 // MODE: 0 = lane-owned copies and frontier readiness (v3), 1 = piece
 // descriptors (v4), 2 = piece-parallel descriptors (v5), 3 = descriptors from
-// one base per run (v12, the default); 1, 2 and 3 use exact
+// one base per run (v12), 4 = v12 with the rounds' readiness found by a binary
+// search over the pending destinations in LDS (v13, the default); 1-4 use exact
 // readiness
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
@@ -632,7 +633,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if (MODE == 3)
+        if (MODE == 3 || MODE == 4)
             copy_desc2<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
         else if (MODE == 2)
             copy_scan<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
@@ -655,7 +656,31 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         while (pending) {
             const bool mine = (pending >> lane) & 1;
             bool ready;
-            if (MODE != 0) {
+            if (MODE == 4) {
+                // pending destinations are ascending and disjoint: compact
+                // them (lane order) into the descriptor area, then binary-
+                // search the first one below this lane that ends after msrc;
+                // blocked iff it also starts before need
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(pending >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pending, 0u));
+                if (mine)
+                    *lp<uint64_t>(descs + 8 * below) = ((uint64_t)me << 32) | mb;
+                wave_lds_sync();
+                uint32_t lo = 0, hi = mine ? below : 0;
+                while (__ballot(lo < hi)) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    const uint32_t mem = lo < hi ? (uint32_t)(*lp<uint64_t>(descs + 8 * mid) >> 32) : 0;
+                    if (lo < hi) {
+                        if (mem > msrc)
+                            hi = mid;
+                        else
+                            lo = mid + 1;
+                    }
+                }
+                const uint32_t mbl = (uint32_t)*lp<uint64_t>(descs + 8 * (mine && lo < below ? lo : 0));
+                ready = mine && !(lo < below && mbl < need);
+                wave_lds_sync();
+            } else if (MODE != 0) {
                 // blocked while the source meets a lower pending match's destination
                 bool blocked = false;
                 uint64_t pj = pending;
@@ -741,6 +766,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 10: ZSK_XB(1, 0, 2048); break;
     case 11: ZSK_X(2, 0); break;
     case 12: ZSK_X(3, 0); break;
+    case 13: ZSK_X(4, 0); break;
     case 8: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
@@ -768,7 +794,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<3, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<4, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
