@@ -171,11 +171,18 @@ def main():
     kname = "zstd_seq_kernel" if zstd else z.lib().zsk_lz4_kernel_name(nfr).decode()
     stages = None
     if n_timed:
+        # the parse kernel the library picks for these frames (zsk_internal.h
+        # chunk_parse_min: the chunk parse for big frames and small batches)
+        chunk = comp_bytes / nfr >= (49152 if nfr >= 32768 else 8192)
         names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel + zstd_huf_kernel + zstd_seq_kernel",
                   "execute": "seq_exec_kernel", "hand-off": "zstd_check_kernel"} if zstd else
-                 {"plan": "lz4_plan_direct_kernel", "parse": "lz4_scan_kernel", "execute": kname,
-                  "hand-off": "lz4_wave_kernel<4096, 4, true>"})
+                 {"plan": "lz4_plan_direct_kernel",
+                  "parse": "lz4_chunk_kernel" if chunk else "lz4_scan_kernel",
+                  "execute": "seq_exec_kernel", "hand-off": "lz4_wave_kernel<4096, 4, true>"})
         stages = {k: {"kernel": names[k], "avg_ms": round(v, 4)} for k, v in stage_ms.items()}
+        if not zstd:   # the dominant kernel of the launch
+            kname = max(("parse", "execute"), key=lambda k: stage_ms[k])
+            kname = names[kname]
     value = dsum * world * args.steps / t_max / 1e9
     line = {
         "metric": METRIC_ZSTD if zstd else METRIC,

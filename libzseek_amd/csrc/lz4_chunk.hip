@@ -1,0 +1,543 @@
+// lz4_chunk.hip — parse phase of the two-phase LZ4 decoder, one WAVE per
+// frame, the LZ4 token chain split over the wave's 64 lanes (gfx950).
+//
+// The lane-per-frame parse (lz4_scan.hip) walks each frame's ~1,500-token
+// chain serially: 65,536 frames = one wave per SIMD, every step a dependent
+// LDS round trip.  Here a frame's compressed block is cut into 64 chunks and
+// every lane parses one, so a frame's chain takes ~25 steps instead of
+// ~1,500 and there are as many waves as frames to hide the latency.
+//
+// A chunk's true first token is unknown until the chunk before it is parsed,
+// so each block goes through three passes over the same bytes:
+//
+//   1. speculate: lane j parses from its chunk start s_j as if a token began
+//      there, until it passes its chunk end, marking every token position it
+//      visits in a per-lane bitmap (LDS, the chunk's first kMap bytes).  An LZ4
+//      token chain started at a wrong byte joins the true chain after a few
+//      tokens (it lands on a true token start), and from there on the two are
+//      the same chain.
+//   2. join: lane j continues its own chain past its exit e_j until it lands
+//      on a position another lane visited (bit set) — y_j — or on the block
+//      end.  If lane j's chain is the true one, y_j is a true token and the
+//      lane whose chunk holds y_j (its owner) is true from y_j on.  Walking
+//      owners from lane 0 (whose start is the block start) gives every lane's
+//      true range [entry_j, y_j): usually lane j+1 starts where lane j stops.
+//   3. count, then emit: each true lane re-parses its range counting output
+//      bytes and items; wave prefix sums give its absolute output position and
+//      item slot; a last pass parses the range again with every liblz4 rule
+//      (same checks, same order as lz4_scan.hip's slow step and
+//      oracle/lz4_oracle.c decode_block) and writes the items.
+//
+// Passes 1-2 never validate: a speculative chain is arbitrary bytes.  They
+// follow liblz4's token/offset/length-extension transitions with the
+// input-side end rule only (a literal run reaching within 8 bytes of the block
+// end ends the block), which makes the same moves as liblz4 on every sequence
+// liblz4 accepts; where the two could differ, pass 3 reports the error liblz4
+// reports.  Correctness never depends on the speculation succeeding: a chain
+// that does not join just makes its left neighbour parse further.
+//
+// Output: the items of lz4_scan.hip (8 bytes per sequence, two when a run is
+// longer than the small form holds) at rec_base[f], without the padding item
+// the older execute kernels needed (seq_exec.hip keeps an extended pair
+// together itself), nitems[f], status[f], fail_at[f].
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lz4_dev.h"
+#include "zsk_internal.h"
+
+namespace zsk {
+
+namespace {
+
+using namespace lz4d;
+
+constexpr uint32_t kItemExt = 0x80000000u;
+constexpr uint32_t kItemPos = 0x3FFFFFFFu;
+constexpr uint32_t kCW = 4;                 // waves (frames) per workgroup
+constexpr uint32_t kMap = 512;              // token-map bits per lane (chunk prefix)
+constexpr uint32_t kMapW = kMap / 32;       // dwords per lane
+constexpr uint32_t kMinChunk = 256;         // shortest chunk worth a lane
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// The frame's compressed bytes through a 16-byte register window: frame
+// offset x is resource byte x + s0; the window holds resource bytes
+// [base, base + 16), base 4-aligned (dword range checks: see load16u).
+struct Src {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t s0;
+};
+
+struct Win {
+    u32x4 w;
+    uint32_t base;
+};
+
+__device__ __forceinline__ uint32_t rd4(const Src &S, Win &W, uint32_t x)
+{
+    const uint32_t rx = x + S.s0;
+    if (rx - W.base > 12u) {
+        W.base = rx & ~3u;
+        W.w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(S.r, W.base, 0, 0));
+    }
+    return vword(W.w, rx - W.base);
+}
+
+__device__ __forceinline__ uint32_t rd1(const Src &S, Win &W, uint32_t x)
+{
+    return rd4(S, W, x) & 0xFF;
+}
+
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T *lp(uint32_t a)
+{
+    return (__attribute__((address_space(3))) T *)(uintptr_t)a;
+}
+
+// One sequence of a chain, no validation (passes 1, 2 and the count).
+// Advances p to the next token (the block end after a literals-only last
+// sequence or when the bytes cannot be a sequence) and adds the sequence's
+// output bytes and items.
+__device__ __forceinline__ void skel(const Src &S, Win &W, uint32_t &p, uint32_t iend,
+                                     uint32_t &out, uint32_t &nitem)
+{
+    const uint32_t t4 = rd4(S, W, p);
+    const uint32_t tok = t4 & 0xFF;
+    uint32_t lit = tok >> 4, pp = p + 1;
+    if (lit == 15) {
+        uint32_t e = (t4 >> 8) & 0xFF;
+        pp++;
+        lit += e;
+        while (e == 255 && pp < iend) {
+            e = rd1(S, W, pp);
+            pp++;
+            lit += e;
+        }
+    }
+    // liblz4's input-side end rule (ip + lit > iend - (2 + 1 + LASTLITERALS))
+    if (pp >= iend || iend - pp < lit + 8) {
+        out += lit;
+        nitem += lit > 255 ? 2 : 1;
+        p = iend;
+        return;
+    }
+    uint32_t q = pp + lit;
+    uint32_t ml = tok & 15;
+    if (ml == 15) {
+        uint32_t e = (rd4(S, W, q) >> 16) & 0xFF;
+        q += 3;
+        ml += e;
+        while (e == 255 && q < iend) {
+            e = rd1(S, W, q);
+            q++;
+            ml += e;
+        }
+    } else {
+        q += 2;
+    }
+    ml += kMinMatch;
+    out += lit + ml;
+    nitem += (lit > 255 || ml > 258) ? 2 : 1;
+    p = q < iend ? q : iend;
+}
+
+struct Blk {
+    uint32_t ib, iend;     // compressed block [ib, iend) (frame offsets)
+    uint32_t bop, oend;    // output position of the block, + max block size
+    uint32_t floor_;       // lowest match source (block start if independent)
+    uint32_t dlen;
+};
+
+// the frame's status for a failure inside block B (lz4_scan.hip fail_block)
+__device__ __forceinline__ int32_t block_fail(const Blk &B, uint32_t bsid, uint32_t max_block)
+{
+    const bool direct = (B.dlen - B.bop) >= max_block;
+    const int32_t bits = (int32_t)((bsid - 4) << ST_BSID_SHIFT);
+    return (direct ? (ST_GENERIC | ST_DIRECT_FLAG) : ST_DECOMPRESS_FAILED) | ST_BLOCK_FAIL_FLAG | bits;
+}
+
+__device__ __forceinline__ void put_item(uint64_t *it, uint32_t &k, uint32_t lsrc, uint32_t lit,
+                                         uint32_t off, uint32_t ml)
+{
+    if (lit > 255 || ml > 258) {
+        it[k] = ((uint64_t)off << 32) | (lsrc | kItemExt);
+        it[k + 1] = ((uint64_t)ml << 32) | lit;
+        k += 2;
+    } else {
+        it[k] = ((uint64_t)(off | (lit << 16) | ((ml ? ml - 3 : 0) << 24)) << 32) | lsrc;
+        k += 1;
+    }
+}
+
+// Pass 3: the validated parse of a true range [p, y) from output position op,
+// items from slot k.  Returns -1, or the status of the first failing rule
+// (ST_BLOCK_ERR for a block failure, ST_DST_OVERFLOW).
+__device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B, uint32_t p,
+                                              uint32_t y, uint32_t op, uint64_t *it, uint32_t k)
+{
+    const uint32_t iend = B.iend;
+    while (p < y) {
+        uint32_t lit;
+        uint32_t tok;
+        {
+            const uint32_t t4 = rd4(S, W, p);
+            tok = t4 & 0xFF;
+            p++;
+            lit = tok >> 4;
+            if (lit == 15) {
+                if (iend - p <= 15)
+                    return ST_BLOCK_ERR;
+                uint32_t s = (t4 >> 8) & 0xFF;
+                p++;
+                lit += s;
+                while (s == 255) {
+                    if (p >= iend)
+                        return ST_BLOCK_ERR;
+                    s = rd1(S, W, p);
+                    p++;
+                    lit += s;
+                }
+            }
+        }
+        if (op + lit > B.oend - kMfLimit || iend - p < lit + 2 + 1 + kLastLiterals) {
+            // the block's last sequence: literals only, ending the block
+            if (iend - p != lit || op + lit > B.oend)
+                return ST_BLOCK_ERR;
+            if (op + lit > B.dlen)
+                return ST_DST_OVERFLOW;
+            put_item(it, k, p, lit, 0, 0);
+            return -1;
+        }
+        if (op + lit > B.dlen)
+            return ST_DST_OVERFLOW;
+        const uint32_t lsrc = p;
+        op += lit;
+        p += lit;
+        const uint32_t o4 = rd4(S, W, p);
+        const uint32_t off = o4 & 0xFFFF;
+        p += 2;
+        uint32_t ml = tok & 15;
+        if (ml == 15) {
+            uint32_t s = (o4 >> 16) & 0xFF;
+            bool first = true;
+            do {
+                if (p >= iend)
+                    return ST_BLOCK_ERR;
+                if (!first)
+                    s = rd1(S, W, p);
+                first = false;
+                p++;
+                ml += s;
+                if (p >= iend - (kLastLiterals - 1))
+                    return ST_BLOCK_ERR;
+            } while (s == 255);
+        }
+        ml += kMinMatch;
+        if (off == 0 || off > op - B.floor_)
+            return ST_BLOCK_ERR;
+        if (op + ml > B.oend - kLastLiterals)
+            return ST_BLOCK_ERR;
+        if (op + ml > B.dlen)
+            return ST_DST_OVERFLOW;
+        put_item(it, k, lsrc, lit, off, ml);
+        op += ml;
+    }
+    return -1;
+}
+
+// One compressed block over the wave.  Returns -1 (block done: *op and *k
+// advanced) or a frame status.
+__device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane, uint32_t mapbase,
+                               uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op)
+{
+    const uint32_t bsize = B.iend - B.ib;
+    // chunking: C bytes per lane (>= kMinChunk), nl lanes
+    uint32_t C = (bsize + 63) / 64;
+    C = C < kMinChunk ? kMinChunk : (C + 3) & ~3u;
+    const uint32_t nl = (bsize + C - 1) / C;
+    const uint32_t s = B.ib + lane * C;
+    const uint32_t t = s + C < B.iend ? s + C : B.iend;
+    const bool act = lane < nl;
+    const uint32_t mlen = C < kMap ? C : kMap;
+    const uint32_t mymap = mapbase + lane * (kMapW * 4);
+
+    uint32_t entry = kNone, y = B.iend;
+    if (nl == 1) {
+        entry = lane == 0 ? B.ib : kNone;
+    } else {
+        // pass 1: speculate over the own chunk, marking visited tokens
+#pragma unroll
+        for (uint32_t i = 0; i < kMapW; i += 4)
+            *lp<u32x4>(mymap + 4 * i) = (u32x4){0, 0, 0, 0};
+        wave_lds_sync();
+        uint32_t p = s, dummy0 = 0, dummy1 = 0;
+        if (act) {
+            while (p < t) {
+                const uint32_t r = p - s;
+                if (r < mlen)
+                    __hip_atomic_fetch_or(lp<uint32_t>(mymap + 4 * (r >> 5)), 1u << (r & 31),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                skel(S, W, p, B.iend, dummy0, dummy1);
+            }
+        }
+        wave_lds_sync();
+        // pass 2: continue to the first position another lane visited
+        if (act) {
+            while (p < B.iend) {
+                const uint32_t c = (p - B.ib) / C;
+                const uint32_t r = p - (B.ib + c * C);
+                if (r < mlen && ((*lp<uint32_t>(mapbase + c * (kMapW * 4) + 4 * (r >> 5)) >> (r & 31)) & 1))
+                    break;
+                skel(S, W, p, B.iend, dummy0, dummy1);
+            }
+        }
+        y = p;
+        // owners: lane j's successor is the lane whose chunk holds y_j
+        const uint32_t nxt = act ? (y >= B.iend ? 64u : (y - B.ib) / C) : 64u;
+        const uint64_t ends = __ballot(act && nxt == 64);
+        const uint32_t m = (uint32_t)__builtin_ctzll(ends | (1ull << 63));   // first lane ending the block
+        const uint64_t bad = __ballot(lane < m && nxt != lane + 1);
+        if (bad == 0 && (ends >> m) & 1) {
+            // the usual case: lanes 0..m, each starting where the previous stops
+            const uint32_t yp = dpp_prev(y, B.ib);
+            entry = lane <= m ? (lane == 0 ? B.ib : yp) : kNone;
+        } else {
+            // follow the owner chain from lane 0
+            uint32_t j = 0, x = B.ib;
+            for (;;) {
+                if (lane == j)
+                    entry = x;
+                const uint32_t yj = lane_val(y, (int)j);
+                const uint32_t nj = lane_val(nxt, (int)j);
+                if (nj >= 64)
+                    break;
+                x = yj;
+                j = nj;
+            }
+        }
+    }
+    const bool tru = entry != kNone;
+    // count: output bytes and items of the true range
+    uint32_t out = 0, nit = 0;
+    if (tru) {
+        uint32_t p = entry;
+        while (p < y)
+            skel(S, W, p, B.iend, out, nit);
+    }
+    const uint32_t oinc = wave_incl_add(out), kinc = wave_incl_add(nit);
+    const uint32_t ktot = lane_val(kinc, 63);
+    if (k + ktot > cap)
+        return ST_NOT_RUN;
+    // emit: the validated parse, items in place
+    int32_t st = -1;
+    if (tru)
+        st = emit_range(S, W, B, entry, y, op + oinc - out, it, k + kinc - nit);
+    const uint64_t fails = __ballot(st >= 0);
+    if (fails) {
+        const int32_t fs = (int32_t)lane_val((uint32_t)st, __builtin_ctzll(fails));
+        return fs;
+    }
+    op += lane_val(oinc, 63);
+    k += ktot;
+    return -1;
+}
+
+__device__ __forceinline__ uint32_t hdr_xxh32(const Src &S, Win &W, uint32_t n)
+{
+    // XXH32(frame descriptor bytes [4, 4 + n), seed 0), n < 16
+    uint32_t acc = 0x165667B1u + n;
+    uint32_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+        acc += rd4(S, W, 4 + i) * 0xC2B2AE3Du;
+        acc = ((acc << 17) | (acc >> 15)) * 0x27D4EB2Fu;
+    }
+    for (; i < n; i++) {
+        acc += rd1(S, W, 4 + i) * 0x165667B1u;
+        acc = ((acc << 11) | (acc >> 21)) * 0x9E3779B1u;
+    }
+    acc ^= acc >> 15;
+    acc *= 0x85EBCA77u;
+    acc ^= acc >> 13;
+    acc *= 0xC2B2AE3Du;
+    acc ^= acc >> 16;
+    return acc;
+}
+
+__global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
+    const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
+    uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
+    uint32_t min_csize)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t f = uni(blockIdx.x * kCW + w);
+    if (f >= n)
+        return;
+    const FrameDesc d = desc[f];
+    if (uni(d.c_size) < min_csize)
+        return;   // lz4_scan_kernel's frame
+    const uint64_t rb0 = rec_base[f];
+    const uint32_t cap = slots_of(d.c_size);
+    const uint32_t clen = d.c_size, dlen = d.d_size;
+    const uint32_t mapbase = (uint32_t)(uintptr_t)(maps) + w * (64 * kMapW * 4);
+    uint64_t *it = items + rb0;
+    Src S;
+    {
+        const Span sp = make_span(comp + d.c_off, clen);
+        S.r = sp.r;
+        S.s0 = sp.s0;
+    }
+    Win W;
+    W.base = 0xFFFFFFF0u;
+    W.w = (u32x4){0, 0, 0, 0};
+    uint32_t op = 0, k = 0, fail_op = 0;
+    int32_t st = ST_OK;
+    do {
+        if (rb0 + cap > capacity || clen > kItemPos) {
+            st = ST_NOT_RUN;
+            break;
+        }
+        // frame header (LZ4F_decodeHeader order; lz4_scan.hip hdr_status)
+        if (clen < 7) {
+            st = ST_HDR_INCOMPLETE;
+            break;
+        }
+        const uint32_t magic = rd4(S, W, 0);
+        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
+            st = ST_SHORT_FRAME;
+            break;
+        }
+        if (magic != kLz4Magic) {
+            st = ST_FRAME_TYPE;
+            break;
+        }
+        const uint32_t fb = rd4(S, W, 4);
+        const uint32_t flg = fb & 0xFF, bd = (fb >> 8) & 0xFF;
+        if (flg & 0x14) {   // block / content checksums: the wave kernel verifies them
+            st = ST_NOT_RUN;
+            break;
+        }
+        if ((flg >> 1) & 1) {
+            st = ST_RESERVED;
+            break;
+        }
+        if (((flg >> 6) & 3) != 1) {
+            st = ST_VERSION;
+            break;
+        }
+        const uint32_t csz = (flg >> 3) & 1;
+        const uint32_t hdr = 7 + (csz ? 8 : 0) + ((flg & 1) ? 4 : 0);
+        if (clen < hdr) {
+            st = ST_HDR_INCOMPLETE;
+            break;
+        }
+        const uint32_t bsid = (bd >> 4) & 7;
+        if ((bd >> 7) & 1) {
+            st = ST_RESERVED;
+            break;
+        }
+        if (bsid < 4) {
+            st = ST_MAXBLOCK;
+            break;
+        }
+        if (bd & 15) {
+            st = ST_RESERVED;
+            break;
+        }
+        if (((hdr_xxh32(S, W, hdr - 5) >> 8) & 0xFF) != rd1(S, W, hdr - 1)) {
+            st = ST_HDR_CHECKSUM;
+            break;
+        }
+        const uint32_t indep = (flg >> 5) & 1;
+        const uint64_t csize = csz ? ((uint64_t)rd4(S, W, 6) | ((uint64_t)rd4(S, W, 10) << 32)) : 0;
+        const uint32_t max_block = 1u << (8 + 2 * bsid);
+        uint32_t ip = hdr;
+        st = -1;
+        while (st < 0) {
+            fail_op = op;
+            if (clen - ip < 4) {
+                st = ST_TRUNCATED;
+                break;
+            }
+            const uint32_t bh = rd4(S, W, ip);
+            ip += 4;
+            if (bh == 0) {
+                if (csz && csize != op)
+                    st = ST_FRAME_SIZE;
+                else
+                    st = op != dlen ? ST_SHORT_FRAME : ST_OK;
+                break;
+            }
+            const uint32_t bsize = bh & 0x7FFFFFFFu;
+            if (bsize > max_block) {
+                st = ST_MAXBLOCK;
+                break;
+            }
+            if (clen - ip < bsize) {
+                st = ST_TRUNCATED;
+                break;
+            }
+            Blk B;
+            B.ib = ip;
+            B.iend = ip + bsize;
+            B.bop = op;
+            B.oend = op + max_block;
+            B.floor_ = indep ? op : 0;
+            B.dlen = dlen;
+            if (bh & 0x80000000u) {
+                // stored block: one literal run
+                if (op + bsize > dlen) {
+                    st = ST_DST_OVERFLOW;
+                    break;
+                }
+                const uint32_t nk = bsize > 255 ? 2 : 1;
+                if (k + nk > cap) {
+                    st = ST_NOT_RUN;
+                    break;
+                }
+                if (lane == 0) {
+                    uint32_t kk = k;
+                    put_item(it, kk, ip, bsize, 0, 0);
+                }
+                k += nk;
+                op += bsize;
+                ip += bsize;
+                continue;
+            }
+            if (bsize == 0) {
+                st = block_fail(B, bsid, max_block);
+                break;
+            }
+            const int32_t bs = chunk_block(S, W, B, lane, mapbase, it, k, cap, op);
+            if (bs == ST_BLOCK_ERR)
+                st = block_fail(B, bsid, max_block);
+            else if (bs >= 0)
+                st = bs;
+            ip = B.iend;
+        }
+    } while (false);
+    if (lane == 0) {
+        status[f] = st;
+        nitems[f] = k;
+        if (fail_at)
+            fail_at[f] = fail_op;
+    }
+}
+
+}   // namespace
+
+int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
+                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize)
+{
+    if (nframes == 0)
+        return 0;
+    hipLaunchKernelGGL(lz4_chunk_kernel, dim3((nframes + kCW - 1) / kCW), dim3(64 * kCW), 0, stream,
+                       d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
+                       min_csize);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}   // namespace zsk

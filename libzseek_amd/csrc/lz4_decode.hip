@@ -666,6 +666,12 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 79: return launch_lz4_split_stages(15, 0x20D, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 78: return launch_lz4_split_stages(15, 0x204, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 60: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    // parse A/B: 80/81 = split decoder with the chunk / scan parse for every
+    // frame, 82/83 = plan + that parse only
+    case 80: return launch_lz4_split_stages(15, 0x4000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 81: return launch_lz4_split_stages(15, 0x2000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 82: return launch_lz4_split_stages(3, 0x4000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 83: return launch_lz4_split_stages(3, 0x2000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 38: return launch_lz4_split_stages(7, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0xA00, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 40: return launch_lz4_split_stages(7, 0x1801, d_desc, nframes, d_comp, d_out, d_status, stream);

@@ -592,16 +592,19 @@ template <bool BR>
 __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))) void lz4_scan_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
-    uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at)
+    uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
+    uint32_t max_csize)
 {
     __shared__ __attribute__((aligned(16))) uint8_t rings[kSW * 64 * kStride];
     const uint32_t f = blockIdx.x * (64 * kSW) + threadIdx.x;
-    const bool act = f < n;
     FrameDesc d = {0, 0, 0, 0};
+    if (f < n)
+        d = desc[f];
+    // frames of max_csize bytes and more belong to lz4_chunk_kernel
+    const bool act = f < n && d.c_size < max_csize;
     uint64_t rb0 = 0;
     uint32_t cap = 0;
     if (act) {
-        d = desc[f];
         rb0 = rec_base[f];
         cap = slots_of(d.c_size);
     }
@@ -691,17 +694,19 @@ __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))
 int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items,
                     uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
-                    int version)
+                    int version, uint32_t max_csize)
 {
     if (nframes == 0)
         return 0;
     const uint32_t per = 64 * kSW;
     if (version == 1)
         hipLaunchKernelGGL(lz4_scan_kernel<true>, dim3((nframes + per - 1) / per), dim3(per), 0, stream,
-                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at);
+                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
+                           max_csize);
     else
         hipLaunchKernelGGL(lz4_scan_kernel<false>, dim3((nframes + per - 1) / per), dim3(per), 0, stream,
-                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at);
+                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
+                           max_csize);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -869,12 +869,23 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     // 0x400 = the scan's if/return fast path,
     // 0x200/0x201 = LDS-ring staged execute v1/v2, 0x203..0x20A = seq_exec
     // versions; 0 = the production pair lz4_scan_kernel + seq_exec v13
+    // 0x2000 = every frame to lz4_scan_kernel, 0x4000 = every frame to
+    // lz4_chunk_kernel; default: frames of >= kChunkParseMin compressed bytes
+    // to the chunk parse, the rest to the scan.  The first-generation execute
+    // steps 64 items at a time and needs the scan's padding items.
     const bool old_parse = (diag & 0x800) != 0, old_exec = (diag & 0x1000) != 0;
     const int xd = diag & 0x3FF;
-    if ((stages & 2) && !old_parse)
-        launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                        s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0);
-    else if (stages & 2)
+    const uint32_t cmin = ((diag & 0x2000) || old_exec) ? 0xFFFFFFFFu
+                          : (diag & 0x4000)              ? 0u
+                                                         : chunk_parse_min(nframes);
+    if ((stages & 2) && !old_parse) {
+        if (cmin != 0)
+            launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
+                            s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0, cmin);
+        if (cmin != 0xFFFFFFFFu)
+            launch_lz4_chunk(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
+                             s->nitems, d_status, d_fail_at, stream, cmin);
+    } else if (stages & 2)
         hipLaunchKernelGGL(lz4_parse_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                            s->nitems, d_status, d_fail_at);
@@ -948,15 +959,32 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
     return launch_lz4_split(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream, &s);
 }
 
-// Automatic choice: the lane-per-frame kernel needs about one
-// frame per lane of the chip to hide its per-frame latency (>= 32768 frames);
-// smaller batches go to the wave-per-frame kernel.
+// Automatic choice: the two-phase decoder (its parse per frame
+// size and batch size, chunk_parse_min) from 64 frames on; a handful of frames
+// go to the wave-per-frame kernel in one launch.
 int lz4_pick_engine(uint32_t nframes)
 {
     const int e = lz4_engine();
     if (e != ENGINE_AUTO)
         return e;
-    return nframes >= 32768 ? ENGINE_SPLIT : ENGINE_WAVE;
+    return nframes >= 64 ? ENGINE_SPLIT : ENGINE_WAVE;
+}
+
+uint32_t chunk_parse_min(uint32_t nframes)
+{
+    static const int forced = [] {
+        const char *v = getenv("ZSEEK_PARSE");
+        if (v && !strcmp(v, "scan"))
+            return 1;
+        if (v && !strcmp(v, "chunk"))
+            return 2;
+        return 0;
+    }();
+    if (forced == 1)
+        return 0xFFFFFFFFu;
+    if (forced == 2)
+        return 0;
+    return nframes >= 32768 ? 49152u : 8192u;
 }
 
 int lz4_engine()
@@ -1016,7 +1044,7 @@ const char *lz4_kernel_name(uint32_t nframes)
 {
     switch (lz4_pick_engine(nframes)) {
     case ENGINE_LANE: return "lz4_lane_kernel";
-    case ENGINE_SPLIT: return "seq_exec_kernel";
+    case ENGINE_SPLIT: return nframes >= 32768 ? "seq_exec_kernel" : "lz4_chunk_kernel";
     default: return "lz4_wave_kernel<4096, 4>";
     }
 }

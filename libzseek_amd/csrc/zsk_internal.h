@@ -173,7 +173,21 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items,
                     uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
-                    int version = 0);
+                    int version = 0, uint32_t max_csize = 0xFFFFFFFFu);
+
+// Parse phase, one wave per frame, chunk-parallel (lz4_chunk.hip): the same
+// outputs as launch_lz4_scan for the frames of min_csize compressed bytes and
+// more (other frames are left to lz4_scan_kernel), items without padding.
+int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
+                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize);
+// Frames of at least chunk_parse_min(nframes) compressed bytes go to the
+// chunk parse: with >= 32768 frames the lane-per-frame scan has a lane for
+// every frame it needs and wins on 64 KiB frames (2.07 vs 4.18 ms parse at
+// config 2); smaller batches and bigger frames leave its lanes idle
+// (1 MiB frames: 4,096 chains; 256 MiB batches: 4,096 frames).
+// Env ZSEEK_PARSE=scan|chunk forces one parse for every frame.
+uint32_t chunk_parse_min(uint32_t nframes);
 
 // Lane-per-frame decoder (lz4_lane.hip) + hand-offs to the wave kernel.
 int launch_lz4_lane(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
