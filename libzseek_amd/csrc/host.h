@@ -69,6 +69,26 @@ class FrameCache {
     std::unordered_map<size_t, std::list<Entry>::iterator> map_;
 };
 
+// Keeps the calling thread's current HIP device across a library call: the
+// reader switches to its own device (DeviceCtx::device) and this puts the
+// caller's back on every return path.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard()
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev)
+            (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 // Per-reader GPU context: one stream, device buffers and pinned staging
 // grown geometrically, created lazily at the first decode.
 struct DeviceCtx {

@@ -192,6 +192,7 @@ DeviceCtx::~DeviceCtx()
 {
     if (device < 0)
         return;
+    DeviceGuard keep;
     (void)hipSetDevice(device);
     if (stream)
         (void)hipStreamSynchronize(stream);

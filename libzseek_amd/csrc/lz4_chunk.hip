@@ -233,8 +233,10 @@ __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B
             } while (s == 255);
         }
         ml += kMinMatch;
-        if (off == 0 || off > op - B.floor_)
+        if (off > op - B.floor_)
             return ST_BLOCK_ERR;
+        if (off == 0)   // liblz4 writes zeros: the wave kernel decodes the frame
+            return ST_NOT_RUN;
         if (op + ml > B.oend - kLastLiterals)
             return ST_BLOCK_ERR;
         if (op + ml > B.dlen)

@@ -548,8 +548,12 @@ __device__ __forceinline__ void do_lit(Lane &L, Slot &S)
 __device__ __forceinline__ void match_measured(Lane &L)
 {
     L.ml += kMinMatch;
-    if (L.off == 0 || L.off > L.op - L.floor_) {
+    if (L.off > L.op - L.floor_) {
         fail_block(L);
+        return;
+    }
+    if (L.off == 0) {   // liblz4 writes zeros: the wave kernel decodes the frame
+        finish(L, ST_NOT_RUN);
         return;
     }
     if (L.op + L.ml > L.oend - kLastLiterals) {

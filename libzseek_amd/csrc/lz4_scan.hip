@@ -459,8 +459,12 @@ __device__ __forceinline__ void slow(Scan &L)
             } while (s == 255);
         }
         ml += kMinMatch;
-        if (off == 0 || off > L.op - L.floor_) {
+        if (off > L.op - L.floor_) {
             fail_block(L);
+            return;
+        }
+        if (off == 0) {   // liblz4 writes zeros: the wave kernel decodes it
+            finish(L, ST_NOT_RUN);
             return;
         }
         if (L.op + ml > L.oend - kLastLiterals) {

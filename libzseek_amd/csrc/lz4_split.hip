@@ -212,7 +212,9 @@ __device__ int32_t parse_block(LaneIn &in, Sink &sink, uint32_t ip, uint32_t bsi
             } while (s == 255);
         }
         ml += kMinMatch;
-        if (off == 0 || off > op - floor_)
+        if (off == 0)
+            return ST_NOT_RUN;   // zeros (liblz4): the wave kernel decodes the frame
+        if (off > op - floor_)
             return ST_BLOCK_ERR;
         if (op + ml > oend - kLastLiterals)
             return ST_BLOCK_ERR;

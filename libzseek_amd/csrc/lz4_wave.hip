@@ -170,6 +170,14 @@ struct WaveDec {
     // Copy an n-byte match at distance off to output offset op.
     __device__ __forceinline__ void copy_match(uint32_t op, uint32_t off, uint32_t n)
     {
+        if (off == 0) {   // liblz4 1.9.3 writes zeros for a zero offset
+            for (uint32_t c = 0; c < n; c += 64) {
+                if (c + lane < n)
+                    ring[(op + c + lane) & kMask] = 0;
+                flush_upto(op + (n - c < 64 ? n : c + 64));
+            }
+            return;
+        }
         uint32_t c = 0;
         uint32_t eff = off;
         if (off < 64) {
@@ -260,7 +268,9 @@ struct WaveDec {
                 } while (s == 255);
             }
             ml += kMinMatch;
-            if (off == 0 || off > op - floor_)
+            // offset 0 is accepted as liblz4 1.9.3 does (zeros; oracle
+            // decode_block)
+            if (off > op - floor_)
                 return ST_BLOCK_ERR;
             if (op + ml > oend - kLastLiterals)
                 return ST_BLOCK_ERR;
@@ -485,6 +495,10 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_wave_kernel(const FrameDesc *_
     w.flushed = 0;
     w.fail_op = 0;
     int32_t st = w.frame();
+    // a failed frame keeps the bytes of its blocks before the failing one
+    // (fail_op): no-cache reads ending there succeed, as in the reference
+    if (st != ST_OK && w.fail_op > w.flushed)
+        w.flush_tail(w.fail_op);
     if (w.lane == 0) {
         status[f] = st;
         if (fail_at)

@@ -282,6 +282,38 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
     return true;
 }
 
+// LZ4F_decompress (liblz4 1.9.3) as the reference's no-cache read drives it
+// (decompress.c:614-669): a block's data is decoded only once the request
+// reaches into it, but the header after a block that ends exactly at the
+// request's end is read and checked in the same call, and so is the end mark
+// with what follows it.  Failures met at a header (block size, truncation,
+// content size / checksum at the end) are therefore met by a request that ends
+// at the failing position; failures inside a block's data (and our
+// seek-table-size checks) only by one that goes past it.
+bool header_level(int32_t st)
+{
+    switch (st & 0xFFFF) {
+    case ST_MAXBLOCK:
+    case ST_TRUNCATED:
+    case ST_FRAME_SIZE:
+    case ST_CONTENT_CHECKSUM:
+        return true;
+    default:
+        return false;
+    }
+}
+
+// Does a no-cache request ending `end_in_frame` bytes into a failed LZ4 frame
+// succeed in the reference?  fail_at = output offset of the failing block (or
+// of the end mark); the decoders leave every byte before it in place.
+bool lz4_partial_ok(int32_t st, uint64_t fail_at, uint64_t end_in_frame)
+{
+    const int32_t code = st & 0xFFFF;
+    if (code == ST_SEEK_CHECKSUM || code == ST_NOT_RUN)
+        return false;
+    return header_level(st) ? end_in_frame < fail_at : end_in_frame <= fail_at;
+}
+
 // Error text for a failed frame, worded as the reference words the same
 // failure.  Cached reads decode the whole frame ("decompress frame: ...",
 // decompress.c:766-768); no-cache reads first decode-and-discard the
@@ -301,7 +333,9 @@ void frame_error(zseek_reader *r, const BatchResult &br, size_t frame, size_t of
     if (r->cache) {
         prefix = "decompress frame";
         room = dsize - at;
-    } else if (at < offset_in_frame) {
+    } else if (offset_in_frame > 0 &&
+               (header_level(st) ? at <= offset_in_frame : at < offset_in_frame)) {
+        // the discard pass (decode-and-drop of the in-frame prefix) met it
         prefix = "decompress discard data";
         room = offset_in_frame - at;
     } else {
@@ -379,6 +413,7 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
     if (fi < 0)
         return 0;   // EOF (ref decompress.c:695-697)
     std::lock_guard<std::mutex> guard(r->lock);
+    DeviceGuard keep_device;   // the caller's current device is restored on return
     const size_t f_first = (size_t)fi;
     const uint64_t end = offset + count < st.decompressed_size() ? offset + count
                                                                  : st.decompressed_size();
@@ -428,7 +463,12 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
         if (!gpu_decode(r, f, g_end, call_data, errbuf, &br))
             return done ? (ssize_t)done : -1;
         const uint64_t lo = offset > st.d_off[f] ? offset : st.d_off[f];
-        const uint64_t good_end = br.first_bad < g_end ? st.d_off[br.first_bad] : st.d_off[g_end];
+        uint64_t good_end = br.first_bad < g_end ? st.d_off[br.first_bad] : st.d_off[g_end];
+        // Without a cache the reference decodes a frame only as far as the
+        // request reaches (lz4_partial_ok); zstd failures carry no offset.
+        if (br.first_bad < g_end && !r->cache && r->type == ZSEEK_LZ4 &&
+            lz4_partial_ok(br.status, br.fail_at, end - st.d_off[br.first_bad]))
+            good_end = end;
         const uint64_t hi = end < good_end ? end : good_end;
         if (hi > lo) {
             if (!copy_out(r->gpu, (uint8_t *)buf + (lo - offset), lo - st.d_off[f], hi - lo,
@@ -436,15 +476,20 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
                 return done ? (ssize_t)done : -1;
             done += hi - lo;
         }
-        if (br.first_bad < g_end) {
+        if (br.first_bad < g_end && good_end < end) {
             if (done)
                 return (ssize_t)done;   // short read up to the corrupt frame
             frame_error(r, br, br.first_bad, offset - st.d_off[br.first_bad], count, errbuf);
             return -1;
         }
-        if (r->cache && g_end > f_last) {
-            size_t k = r->cache->capacity() < g_end - f ? r->cache->capacity() : g_end - f;
-            if (!cache_frames(r, f, g_end - k, g_end, errbuf))
+        // the cache ends as a reference caller's looping frame by frame over
+        // the range would leave it: the range's last `capacity` frames, MRU
+        // last, inserted batch by batch before the batch buffer is reused
+        if (r->cache) {
+            const size_t cap = r->cache->capacity();
+            const size_t keep_from = f_last + 1 > cap ? f_last + 1 - cap : 0;
+            const size_t a = keep_from > f ? keep_from : f;
+            if (a < g_end && !cache_frames(r, f, a, g_end, errbuf))
                 return (ssize_t)done;
         }
         f = g_end;

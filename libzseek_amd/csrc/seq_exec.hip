@@ -517,7 +517,12 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const uint32_t f = uni(blockIdx.x * kXW + w);
     if (f >= n)
         return;
-    if (uni((uint32_t)status[f]) != (uint32_t)ST_OK)
+    // LZ4: a frame the parse failed is executed over the items it emitted
+    // (every one validated; the blocks before the failing one), so its bytes
+    // before fail_at are in place for partial reads; hand-offs are left to
+    // the wave kernel, failed zstd frames to nobody
+    const int32_t fst = (int32_t)uni((uint32_t)status[f]);
+    if (fst != ST_OK && (lit || fst == ST_NOT_RUN))
         return;
     const FrameDesc d = desc[f];
     const uint32_t nit = uni(nitems[f]);

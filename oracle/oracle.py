@@ -108,7 +108,8 @@ class Oracle:
                                       C.byref(dl), C.byref(su), C.byref(fa), C.byref(bf),
                                       C.byref(mb))
         info = {"fail_at": fa.value, "block_fail": bool(bf.value), "max_block": mb.value}
-        return st, d[: dl.value].tobytes(), su.value, info
+        # a failed frame: the bytes of its blocks before the failing one
+        return st, d[: dl.value if st == 0 else fa.value].tobytes(), su.value, info
 
     def zstd_decode(self, src: bytes, dst_cap: int):
         """ZSTD_decompressDCtx restated -> (decoded bytes, 0) or (b"", zstd error code)."""
