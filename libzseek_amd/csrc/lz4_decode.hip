@@ -666,12 +666,23 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 79: return launch_lz4_split_stages(15, 0x20D, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 78: return launch_lz4_split_stages(15, 0x204, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 60: return launch_lz4_split_stages(2, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
-    // parse A/B: 80/81 = split decoder with the chunk / scan parse for every
-    // frame, 82/83 = plan + that parse only
+    // parse A/B: 80/81 = split decoder with the chunk / lane-per-frame (lean)
+    // parse for every frame, 82/83 = plan + that parse only
     case 80: return launch_lz4_split_stages(15, 0x4000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 81: return launch_lz4_split_stages(15, 0x2000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 82: return launch_lz4_split_stages(3, 0x4000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 83: return launch_lz4_split_stages(3, 0x2000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    // 85/86 = the split decoder / plan + parse with the older lz4_scan_kernel
+    // for every frame; 87/88 = plan + lz4_lean_kernel diagnostics (no item
+    // stores / every item to slot 0); 89 = split decoder, older scan for the
+    // frames the lane-per-frame parse takes by default
+    case 85: return launch_lz4_split_stages(15, 0xA20D, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 86: return launch_lz4_split_stages(3, 0xA000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 87: return launch_lz4_split_stages(3, 0x12000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 88: return launch_lz4_split_stages(3, 0x22000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 89: return launch_lz4_split_stages(15, 0x8000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    // 84 = execute v13 alone over the items the previous launch left
+    case 84: return launch_lz4_split_stages(4, 0x20D, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 38: return launch_lz4_split_stages(7, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0xA00, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 40: return launch_lz4_split_stages(7, 0x1801, d_desc, nframes, d_comp, d_out, d_status, stream);

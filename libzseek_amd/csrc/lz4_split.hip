@@ -868,20 +868,26 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     stage_mark(1, stream);
     // diag (tuning builds): 0x800 = the first-generation parse kernel,
     // 0x1000 = the first-generation execute kernel (low bits: its variants),
-    // 0x400 = the scan's if/return fast path,
+    // 0x400 = the older scan's if/return fast path,
     // 0x200/0x201 = LDS-ring staged execute v1/v2, 0x203..0x20A = seq_exec
-    // versions; 0 = the production pair lz4_scan_kernel + seq_exec v13
-    // 0x2000 = every frame to lz4_scan_kernel, 0x4000 = every frame to
-    // lz4_chunk_kernel; default: frames of >= kChunkParseMin compressed bytes
-    // to the chunk parse, the rest to the scan.  The first-generation execute
-    // steps 64 items at a time and needs the scan's padding items.
+    // versions; 0 = the production pair lz4_lean_kernel + seq_exec v13;
+    // 0x2000 = every frame to the lane-per-frame parse, 0x4000 = every frame
+    // to lz4_chunk_kernel (default: frames of >= chunk_parse_min compressed
+    // bytes to the chunk parse, the rest lane per frame); 0x8000 = the older
+    // lz4_scan_kernel as the lane-per-frame parse (bits 16-17: lean DIAG).
+    // The first-generation execute steps 64 items at a time and needs the
+    // older scan's padding items.
     const bool old_parse = (diag & 0x800) != 0, old_exec = (diag & 0x1000) != 0;
+    const bool old_scan = (diag & 0x8000) != 0 || old_exec;
     const int xd = diag & 0x3FF;
     const uint32_t cmin = ((diag & 0x2000) || old_exec) ? 0xFFFFFFFFu
                           : (diag & 0x4000)              ? 0u
                                                          : chunk_parse_min(nframes);
     if ((stages & 2) && !old_parse) {
-        if (cmin != 0)
+        if (cmin != 0 && !old_scan)
+            launch_lz4_lean(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
+                            s->nitems, d_status, d_fail_at, stream, cmin, (diag >> 16) & 3);
+        else if (cmin != 0)
             launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                             s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0, cmin);
         if (cmin != 0xFFFFFFFFu)

@@ -175,6 +175,13 @@ int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                     uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
                     int version = 0, uint32_t max_csize = 0xFFFFFFFFu);
 
+// Parse phase, streaming lane-per-frame with a one-sequence fast step
+// (lz4_lean.hip): the outputs of launch_lz4_chunk (items without padding).
+int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                    const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
+                    int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t max_csize,
+                    int diag = 0);
+
 // Parse phase, one wave per frame, chunk-parallel (lz4_chunk.hip): the same
 // outputs as launch_lz4_scan for the frames of min_csize compressed bytes and
 // more (other frames are left to lz4_scan_kernel), items without padding.

@@ -437,7 +437,7 @@ def seek_table_of(image: np.ndarray):
 # Decoder engines reachable through the (non-ABI) tuning hook
 # zsk_dev_lz4_decode_variant: each one a complete decoder incl. its hand-offs.
 ENGINES = {"wave": 20, "lane": 50, "split": 35, "stage": 34, "exec3": 37, "scan": 39, "exec4": 78,
-           "exec12": 77, "exec13": 79, "chunk": 80, "scanparse": 81}
+           "exec12": 77, "exec13": 79, "chunk": 80, "scanparse": 81, "scanold": 85}
 
 
 def decode_frames(desc, comp, out, status, stream: int | None = None,
