@@ -177,7 +177,7 @@ def main():
         names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel + zstd_huf_kernel + zstd_seq_kernel",
                   "execute": "seq_exec_kernel", "hand-off": "zstd_check_kernel"} if zstd else
                  {"plan": "lz4_plan_direct_kernel",
-                  "parse": "lz4_chunk_kernel" if chunk else "lz4_scan_kernel",
+                  "parse": "lz4_chunk_kernel" if chunk else "lz4_lean_kernel",
                   "execute": "seq_exec_kernel", "hand-off": "lz4_wave_kernel<4096, 4, true>"})
         stages = {k: {"kernel": names[k], "avg_ms": round(v, 4)} for k, v in stage_ms.items()}
         if not zstd:   # the dominant kernel of the launch

@@ -682,6 +682,10 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 88: return launch_lz4_split_stages(3, 0x22000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 89: return launch_lz4_split_stages(15, 0x8000, d_desc, nframes, d_comp, d_out, d_status, stream);
     // 84 = execute v13 alone over the items the previous launch left
+    // 90 = execute v13 with section timers (wave cycles per section; diagnostic)
+    case 90: return launch_lz4_split_stages(4, 0x20E, d_desc, nframes, d_comp, d_out, d_status, stream);
+    // 91 = split decoder with execute v15 (= the default), by version number
+    case 91: return launch_lz4_split_stages(15, 0x20F, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 84: return launch_lz4_split_stages(4, 0x20D, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 38: return launch_lz4_split_stages(7, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0xA00, d_desc, nframes, d_comp, d_out, d_status, stream);

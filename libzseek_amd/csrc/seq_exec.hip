@@ -313,6 +313,69 @@ __device__ __forceinline__ void copy_desc2(const Stage &S, const Out &O, const S
     }
 }
 
+// copy_desc2 with one flat 16-byte load per piece (literal source or frame
+// output by the piece's kind; stage pieces load the literal base, unused)
+// instead of two range-checked buffer loads with one disabled: half the
+// vector-memory ops and 16 fewer VGPRs for the four slots in flight.
+template <int DIAG>
+__device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase, const uint8_t *obase,
+                                           uint32_t descs, uint32_t flushed, uint32_t lane,
+                                           uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
+                                           uint32_t mb, uint32_t mn)
+{
+    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
+    const uint32_t inc = wave_incl_add(np);
+    const uint32_t T = lane_val(inc, 63);
+    if (T == 0)
+        return;
+    const uint32_t x = inc - np;
+    const uint64_t dl = ((uint64_t)((saddr(S, op) - S.base) | (lit < 16 ? lit : 16) << 16 | K_LIT << 24) << 32) | src;
+    const uint64_t dm = ((uint64_t)((saddr(S, mb) - S.base) | (mn < 16 ? mn : 16) << 16 | K_HBM << 24) << 32) | msrc;
+    const uint32_t lm = lit < 16 ? 0 : lit - 16, mm = mn < 16 ? 0 : mn - 16;
+    uint32_t a = descs + 8 * x;
+    for (uint32_t i = 0; __ballot(i < np); i++) {
+        if (i < np) {
+            const bool isl = i < lpn;
+            const uint32_t o = min(16 * (isl ? i : i - lpn), isl ? lm : mm);
+            uint64_t D = (isl ? dl : dm) + (uint64_t)o * 0x100000001ull;
+            if (!isl && msrc + o + 16 > flushed)
+                D += (uint64_t)(K_STAGE - K_HBM) << 56;
+            *lp<uint64_t>(a) = D;
+        }
+        a += 8;
+    }
+    wave_lds_sync();
+    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
+        u32x4 v[4];
+        uint32_t dw[4], sx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t t = t0 + 64 * j + lane;
+            const bool on = t < T;
+            const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
+            sx[j] = (uint32_t)D;
+            dw[j] = on ? (uint32_t)(D >> 32) : 0;
+            const uint32_t kind = dw[j] >> 24;
+            const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);
+            v[j] = (DIAG & 1) ? (u32x4){0, 0, 0, 0} : *reinterpret_cast<const u32x4_l *>(p);
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t n = (dw[j] >> 16) & 0xFF;
+            if (n) {
+                u32x4 w = v[j];
+                if ((dw[j] >> 24) == K_STAGE)
+                    w = lds16(saddr(S, sx[j]));
+                lds_put(S.base + (dw[j] & 0xFFFF), w, n);
+            }
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+    }
+}
+
 // copy_desc with piece-parallel descriptors: instead of each lane looping
 // over its own pieces (as many steps as the batch's longest run), each lane
 // writes its two runs to a table, marks its first piece in an owner array,
@@ -502,8 +565,8 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // MODE: 0 = lane-owned copies and frontier readiness (v3), 1 = piece
 // descriptors (v4), 2 = piece-parallel descriptors (v5), 3 = descriptors from
 // one base per run (v12), 4 = v12 with the rounds' readiness found by a binary
-// search over the pending destinations in LDS (v13, the default); 1-4 use exact
-// readiness
+// search over the pending destinations in LDS (v13), 5 = v13 with one flat
+// load per piece (v15, the default); 1-5 use exact readiness
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
@@ -535,6 +598,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     // literals (zstd scratch laid out like the output, 16 bytes of slack)
     const Span lsp = lit ? make_span(lit + d.d_off, (uint64_t)d.d_size + 16)
                          : make_span(comp + d.c_off, d.c_size);
+    const uint8_t *lbase = lit ? lit + d.d_off : comp + d.c_off;
     Stage S;
     S.base = (uint32_t)(uintptr_t)(lds + w * x_wave(OUTB));
     const uint32_t descs = S.base + x_buf(OUTB);
@@ -638,7 +702,9 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if (MODE == 3 || MODE == 4)
+        if (MODE == 5)
+            copy_desc3<DIAG>(S, lbase, O.o, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
+        else if (MODE == 3 || MODE == 4)
             copy_desc2<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
         else if (MODE == 2)
             copy_scan<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
@@ -661,7 +727,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         while (pending) {
             const bool mine = (pending >> lane) & 1;
             bool ready;
-            if (MODE == 4) {
+            if (MODE >= 4) {
                 // pending destinations are ascending and disjoint: compact
                 // them (lane order) into the descriptor area, then binary-
                 // search the first one below this lane that ends after msrc;
@@ -772,10 +838,15 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 11: ZSK_X(2, 0); break;
     case 12: ZSK_X(3, 0); break;
     case 13: ZSK_X(4, 0); break;
-    case 8: {
+    case 15: ZSK_X(5, 0); break;
+    case 8:
+    case 14: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
-        ZSK_X(1, 16);
+        if (version == 14)
+            ZSK_X(4, 16);
+        else
+            ZSK_X(1, 16);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_xstats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
         const double t = (double)(z[0] + z[1] + z[2] + z[3]);
@@ -799,7 +870,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<4, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<5, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
