@@ -561,12 +561,14 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
     __builtin_amdgcn_s_waitcnt(0);
 }
 
-// DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores
+// DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores, 4 = no
+// dependency rounds, 8 = no round 0, 32 = no flush at all
 // MODE: 0 = lane-owned copies and frontier readiness (v3), 1 = piece
 // descriptors (v4), 2 = piece-parallel descriptors (v5), 3 = descriptors from
 // one base per run (v12), 4 = v12 with the rounds' readiness found by a binary
 // search over the pending destinations in LDS (v13), 5 = v13 with one flat
-// load per piece (v15, the default); 1-5 use exact readiness
+// load per piece (v15), 6 = v15 with the next batch's items shifted in
+// before the flush (v16, the default); 1-6 use exact readiness
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
@@ -590,6 +592,9 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc d = desc[f];
     const uint32_t nit = uni(nitems[f]);
     const uint64_t *it = items + rec_base[f];
+    // the frame's items as a buffer resource: loads past nit return 0
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)it, 0, (int)(nit * 8), kRsrcDw3);
     Out O;
     O.o = out + d.d_off;
     O.dlen = d.d_size;
@@ -607,6 +612,8 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     uint32_t produced = 0;   // frame bytes decoded
     uint32_t fc = 0;         // output chunks [0, fc) are in HBM
     uint64_t cur = lane < nit ? it[lane] : 0;
+    if (MODE == 6)
+        __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
     uint32_t b = 0;
     uint64_t tsec[4] = {0, 0, 0, 0};
     uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
@@ -619,7 +626,9 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         tmark = tn;                                                   \
     }
     while (b < nit) {
-        const uint64_t nxt = b + 64 + lane < nit ? it[b + 64 + lane] : 0;
+        const uint64_t nxt =
+            MODE == 6 ? __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, 8 * (b + 64 + lane), 0, 0))
+                      : (b + 64 + lane < nit ? it[b + 64 + lane] : 0);
         const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
         const uint32_t w0n = dpp_next(w0, 0), w1n = dpp_next(w1, 0);
         const uint32_t w0p = dpp_prev(w0, 0);
@@ -702,7 +711,9 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if (MODE == 5)
+        if (DIAG & 8)
+            ;
+        else if (MODE >= 5)
             copy_desc3<DIAG>(S, lbase, O.o, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
         else if (MODE == 3 || MODE == 4)
             copy_desc2<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
@@ -715,7 +726,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         wave_lds_sync();   // stage bytes of other lanes from here on
         ZSK_T(1)
         // rounds: matches reading bytes of this batch
-        uint64_t pending = __ballot(ml != 0 && !early);
+        uint64_t pending = (DIAG & 4) ? 0 : __ballot(ml != 0 && !early);
         if (DIAG & 16) {
             tsec[4 - 4] += 0;
             cnt[0] += 1;
@@ -781,10 +792,18 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
                 cnt[5] += 1;
         }
         ZSK_T(2)
+        if (MODE == 6) {
+            // the next batch's items before the flush: the wait for nxt (issued
+            // at the top of this batch) then does not also wait for the
+            // flush's stores
+            const uint64_t a = __shfl_down(cur, nb & 63, 64);
+            const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
+            cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
+        }
         // flush complete chunks (the frame's last chunk exactly)
         const bool last = b + nb >= nit;
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
-        if (!(DIAG & 2))
+        if (!(DIAG & 34))
             for (uint32_t c = fc + lane; c < end_c; c += 64)
                 flush_chunk(S, O, c);
         fc = end_c;
@@ -800,9 +819,11 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         }
         wave_lds_sync();
         b += nb;
-        const uint64_t a = __shfl_down(cur, nb & 63, 64);
-        const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
-        cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
+        if (MODE != 6) {
+            const uint64_t a = __shfl_down(cur, nb & 63, 64);
+            const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
+            cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
+        }
         ZSK_T(3)
     }
 #undef ZSK_T
@@ -839,6 +860,11 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 12: ZSK_X(3, 0); break;
     case 13: ZSK_X(4, 0); break;
     case 15: ZSK_X(5, 0); break;
+    case 16: ZSK_X(6, 0); break;
+    case 17: ZSK_X(5, 4); break;
+    case 18: ZSK_X(5, 8); break;
+    case 19: ZSK_X(5, 34); break;
+    case 20: ZSK_X(5, 1); break;
     case 8:
     case 14: {
         unsigned long long z[12] = {0};
@@ -870,7 +896,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<5, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<6, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
