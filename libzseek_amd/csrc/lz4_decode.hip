@@ -687,12 +687,14 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     // 91 = split decoder with execute v15 (= the default), by version number
     case 91: return launch_lz4_split_stages(15, 0x20F, d_desc, nframes, d_comp, d_out, d_status, stream);
     // 93-96 = execute v15 diagnostics alone: no rounds / no round 0 / no flush / no piece loads
-    case 93: return launch_lz4_split_stages(4, 0x211, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 94: return launch_lz4_split_stages(4, 0x212, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 95: return launch_lz4_split_stages(4, 0x213, d_desc, nframes, d_comp, d_out, d_status, stream);
-    case 96: return launch_lz4_split_stages(4, 0x214, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 93: return launch_lz4_split_stages(4, 0x21B, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 94: return launch_lz4_split_stages(4, 0x21C, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 95: return launch_lz4_split_stages(4, 0x21D, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 96: return launch_lz4_split_stages(4, 0x21E, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 97: return launch_lz4_split_stages(4, 0x20F, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 98: return launch_lz4_split_stages(15, 0x210, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 99: return launch_lz4_split_stages(15, 0x211, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 100: return launch_lz4_split_stages(3, 0x42000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 84: return launch_lz4_split_stages(4, 0x20D, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 38: return launch_lz4_split_stages(7, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0xA00, d_desc, nframes, d_comp, d_out, d_status, stream);

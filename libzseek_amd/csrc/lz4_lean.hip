@@ -23,6 +23,7 @@
 //     compiler's vmcnt waits retire exactly the slot consumed).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "lz4_dev.h"
 #include "zsk_internal.h"
@@ -47,14 +48,15 @@ constexpr uint32_t kFlush = 8;           // item lines written per flush (one st
 // slots, so bytes up to ip + kRing - 47 always arrive: the fast step takes a
 // literal run only if its offset's 3 bytes lie within that reach
 constexpr uint32_t kLitFast = kRing - 47 - 5;
-constexpr uint32_t kD = 8;               // pipeline depth (slots of 32 bytes)
+constexpr uint32_t kD = 4;               // pipeline depth (slots of up to 64 bytes)
 constexpr uint32_t kOff = 0x80000000u;   // out-of-range buffer offset: op disabled
 
 enum : uint32_t { P_TOKEN = 0, P_LEXT, P_OFF, P_MEXT, P_BHDR, P_END, P_DONE };
 
 struct Fill {
-    u32x4 a, b;     // ring bytes [x, x + 32)
-    uint32_t x;     // ring coordinate, or kOff
+    u32x4 a, b, c, d;   // ring bytes [x, x + 64): the first 32, and the second 32 if h2
+    uint32_t x;         // ring coordinate, or kOff
+    bool h2;
 };
 
 struct Lane {
@@ -77,7 +79,10 @@ struct Lane {
     uint32_t kf;                       // items [0, kf) written to HBM (a multiple of 16)
     // the sub-step's item store: slots k0, k0+1 (nk = 0: none)
     uint32_t ia, ibw, ia2, ib2, nk;
+    uint32_t cnt[6];   // DIAG 4: sub-steps fast / exact-needed / waiting / done / slow-run, sequences
 };
+
+__device__ unsigned long long g_lean_stats[6];
 
 __device__ __forceinline__ uint32_t lds_u32(uint32_t a)
 {
@@ -294,7 +299,10 @@ __device__ __forceinline__ bool fast(Lane &L, uint32_t fe, uint32_t pc, u32x4 &f
     const bool t_ok = s_t >= 0;
     const bool full = L.k + 2 > L.kf + 32;   // the item buffer waits for a flush
     const bool wait = (!tok_av & (ip + 2 <= L.clen)) | (tok_av & t_ok & (s_av < 0)) | full;
-    return !go & (L.ph != P_DONE) & ((L.ph != P_TOKEN) | !wait);
+    // the exact step's phases wait here too while their next bytes are in
+    // flight (4 from ip, or the frame's end), rather than run to find out
+    const bool x_wait = (L.ph != P_END) & ((int32_t)(L.avail - (L.cx0 + ip + 4)) < 0) & (ip + 4 <= L.clen);
+    return !go & (L.ph != P_DONE) & ((L.ph != P_TOKEN) ? !x_wait : !wait);
 }
 
 // ---- exact step: byte at a time, every rule (parse_block / parse_frame) ------
@@ -534,18 +542,29 @@ __device__ __forceinline__ void flush_store(const Lane &L, uint64_t fe, const u3
 // sequence (fast, else the exact step where needed), buffer its item(s),
 // store the lines handed over last sub-step and hand over new ones, issue
 // S's next load.  Branch-free but for the exact step.
-template <bool SLOW, int DIAG>
+template <bool SLOW, bool FILL, int DIAG>
 __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t tab, uint32_t &fcnt)
 {
-    const bool in = S.x == L.avail;
-    ring_put(L, S.x, S.a, S.b, in);
-    L.avail = in ? L.avail + 32 : L.avail;
+    if (FILL) {
+        const bool in = S.x == L.avail;
+        ring_put(L, S.x, S.a, S.b, in);
+        ring_put(L, S.x + 32, S.c, S.d, in && S.h2);
+        L.avail = in ? L.avail + (S.h2 ? 64 : 32) : L.avail;
+    }
     const uint32_t g = lane >> 3, pc = lane & 7;
     const uint64_t fe = *lp<uint64_t>(tab + 8 * (g < fcnt ? g : kFlush));
     u32x4 fv;
     const bool need = fast(L, (uint32_t)fe, pc, fv);
+    if (DIAG & 4) {
+        L.cnt[0] += L.nk != 0;
+        L.cnt[1] += need;
+        L.cnt[2] += L.nk == 0 && !need && L.ph != P_DONE;
+        L.cnt[3] += L.ph == P_DONE;
+    }
     flush_store<DIAG>(L, fe, fv, g, pc, fcnt);
     if (SLOW && __builtin_expect(__ballot(need) != 0, 0)) {
+        if (DIAG & 4)
+            L.cnt[4] += 1;
         if (need)
             slow(L);
     }
@@ -563,22 +582,31 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
     wave_lds_sync();
     fcnt = flush_hand(L, tab);
     wave_lds_sync();
+    if (!FILL)
+        return;
     // the next byte needed was never requested (a long literal run was
     // skipped): restart the stream there
     const uint32_t need_x = L.cx0 + L.ip;
     const bool jump = need_x >= L.fill;
     L.fill = jump ? need_x & ~31u : L.fill;
     L.avail = jump ? L.fill : L.avail;
-    // ring fill: 32 bytes if that leaves every byte from ip on intact
-    const bool fl = (L.ph < P_END) & (L.fill < L.cx0 + L.clen) & (L.fill + 32 <= need_x + kRing - 16);
+    // ring fill: 32 bytes if that leaves every byte from ip on intact, and 32
+    // more if those do too
+    const uint32_t lim = need_x + kRing - 16;
+    const bool fl = (L.ph < P_END) & (L.fill < L.cx0 + L.clen) & (L.fill + 32 <= lim);
+    const bool f2 = fl & (L.fill + 32 < L.cx0 + L.clen) & (L.fill + 64 <= lim);
     const uint32_t fx = fl ? L.fill : kOff;
     S.x = fx;
+    S.h2 = f2;
     S.a = bload16(L.cin, fx);
     S.b = bload16(L.cin, fl ? fx + 16 : kOff);
-    L.fill = fl ? L.fill + 32 : L.fill;
+    S.c = bload16(L.cin, f2 ? fx + 32 : kOff);
+    S.d = bload16(L.cin, f2 ? fx + 48 : kOff);
+    L.fill = fl ? L.fill + (f2 ? 64 : 32) : L.fill;
 }
 
-// DIAG (tuning builds): 1 = no line stores, 2 = every line to the wave's first line
+// DIAG (tuning builds): 1 = no line stores, 2 = every line to the wave's first line,
+// 4 = sub-step outcome counters (printed)
 template <int DIAG>
 __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))) void lz4_lean_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
@@ -634,6 +662,8 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     L.k = L.kf = 0;
     L.cap = cap;
     L.ia = L.ibw = L.ia2 = L.ib2 = L.nk = 0;
+    for (int i = 0; i < 6; i++)
+        L.cnt[i] = 0;
     if (!act || cspan >= 0x7FFFFF00ull || ispan >= 0x7FFFFF00ull || d.c_size > kItemPos ||
         rb0 + cap > capacity) {
         finish(L, ST_NOT_RUN);
@@ -653,19 +683,21 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     Fill sl[kD];
 #pragma unroll
-    for (int i = 0; i < (int)kD; i++)
+    for (int i = 0; i < (int)kD; i++) {
         sl[i].x = kOff;
+        sl[i].h2 = false;
+    }
     uint32_t rounds = 0, fcnt = 0;
     // the table's sink entry names a valid line from the start
     *lp<uint64_t>(tab + 8 * kFlush) = L.ring + kIBuf;
     wave_lds_sync();
     for (;;) {
+        // two sub-steps per slot: the first retires and refills it, the
+        // second may run the exact step
 #pragma unroll
         for (int i = 0; i < (int)kD; i++) {
-            if ((i & 1) == 0)
-                sub<true, DIAG>(L, sl[i], lane, tab, fcnt);
-            else
-                sub<false, DIAG>(L, sl[i], lane, tab, fcnt);
+            sub<false, true, DIAG>(L, sl[i], lane, tab, fcnt);
+            sub<true, false, DIAG>(L, sl[i], lane, tab, fcnt);
         }
         const bool busy = L.ph != P_DONE;
         if (!__any(busy))
@@ -692,6 +724,11 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
                                 lp<uint32_t>(L.ring + kIBuf + 8 * ((x + 1) & 31))[1]};
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), L.irs, 8 * (L.ib + x), 0, 0);
     }
+    if ((DIAG & 4) && act) {
+        L.cnt[5] = L.k;
+        for (int i = 0; i < 6; i++)
+            atomicAdd(&g_lean_stats[i], (unsigned long long)L.cnt[i]);
+    }
     if (!act)
         return;
     status[f] = L.st;
@@ -710,7 +747,17 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     if (nframes == 0)
         return 0;
     const uint32_t per = 64 * kLW;
-    if (diag & 2)
+    if (diag & 4) {
+        unsigned long long z[6] = {0};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lean_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+        hipLaunchKernelGGL(lz4_lean_kernel<4>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
+                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize);
+        (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_lean_stats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        const double fr = nframes;
+        fprintf(stderr, "lean parse per frame: sub-steps fast %.1f exact-needed %.1f waiting %.1f done %.1f "
+                        "exact-step runs %.1f items %.1f\n", z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr);
+    } else if (diag & 2)
         hipLaunchKernelGGL(lz4_lean_kernel<2>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
                            nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize);
     else if (diag & 1)

@@ -870,7 +870,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     // 0x1000 = the first-generation execute kernel (low bits: its variants),
     // 0x400 = the older scan's if/return fast path,
     // 0x200/0x201 = LDS-ring staged execute v1/v2, 0x203..0x20A = seq_exec
-    // versions; 0 = the production pair lz4_lean_kernel + seq_exec v16;
+    // versions; 0 = the production pair lz4_lean_kernel + seq_exec v17;
     // 0x2000 = every frame to the lane-per-frame parse, 0x4000 = every frame
     // to lz4_chunk_kernel (default: frames of >= chunk_parse_min compressed
     // bytes to the chunk parse, the rest lane per frame); 0x8000 = the older
@@ -886,7 +886,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     if ((stages & 2) && !old_parse) {
         if (cmin != 0 && !old_scan)
             launch_lz4_lean(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                            s->nitems, d_status, d_fail_at, stream, cmin, (diag >> 16) & 3);
+                            s->nitems, d_status, d_fail_at, stream, cmin, (diag >> 16) & 7);
         else if (cmin != 0)
             launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                             s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0, cmin);
@@ -906,7 +906,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                               d_status, stream, xd == 0x201 ? 2 : 1);
     } else if ((stages & 4) && !old_exec) {
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                        stream, 16);
+                        stream, 17);
     } else if (stages & 4) {
         const dim3 grid((nframes + kExecWaves - 1) / kExecWaves), block(64 * kExecWaves);
 #define ZSK_EXEC(D, O)                                                                          \

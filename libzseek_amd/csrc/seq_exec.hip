@@ -508,6 +508,41 @@ __device__ __forceinline__ void copy_overlap(const Stage &S, const Out &O, uint3
 }
 
 // stage chunk k (output chunk cb + k) -> HBM; exact at the frame's edges
+__device__ __forceinline__ void put_chunk(const Out &O, uint32_t a0, uint32_t c, const u32x4 &v)
+{
+    const int64_t x0 = (int64_t)16 * c - a0;
+    if (x0 >= 0 && x0 + 16 <= O.dlen) {
+        *reinterpret_cast<u32x4 *>(O.o + x0) = v;
+    } else {
+        for (int k = 0; k < 16; k++) {
+            const int64_t x = x0 + k;
+            if (x >= 0 && x < O.dlen)
+                O.o[x] = (uint8_t)vbyte(v, k);
+        }
+    }
+}
+
+// chunks [fc, end_c) -> HBM, lane-strided, four chunks' LDS reads in flight
+// before their stores
+__device__ __forceinline__ void flush_chunks4(const Stage &S, const Out &O, uint32_t fc, uint32_t end_c,
+                                              uint32_t lane)
+{
+    for (uint32_t c0 = fc; c0 < end_c; c0 += 256) {
+        u32x4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t c = c0 + 64 * j + lane;
+            v[j] = *lp<u32x4>(c < end_c ? S.base + 16u * (c - S.cb) : S.base);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t c = c0 + 64 * j + lane;
+            if (c < end_c)
+                put_chunk(O, S.a0, c, v[j]);
+        }
+    }
+}
+
 __device__ __forceinline__ void flush_chunk(const Stage &S, const Out &O, uint32_t c)
 {
     const u32x4 v = *lp<u32x4>(S.base + 16u * (c - S.cb));
@@ -568,7 +603,8 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // one base per run (v12), 4 = v12 with the rounds' readiness found by a binary
 // search over the pending destinations in LDS (v13), 5 = v13 with one flat
 // load per piece (v15), 6 = v15 with the next batch's items shifted in
-// before the flush (v16, the default); 1-6 use exact readiness
+// before the flush (v16), 7 = v16 with four chunks' stage reads in flight per
+// flush step (v17, the default); 1-7 use exact readiness
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
@@ -612,7 +648,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     uint32_t produced = 0;   // frame bytes decoded
     uint32_t fc = 0;         // output chunks [0, fc) are in HBM
     uint64_t cur = lane < nit ? it[lane] : 0;
-    if (MODE == 6)
+    if (MODE >= 6)
         __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
     uint32_t b = 0;
     uint64_t tsec[4] = {0, 0, 0, 0};
@@ -627,7 +663,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     }
     while (b < nit) {
         const uint64_t nxt =
-            MODE == 6 ? __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, 8 * (b + 64 + lane), 0, 0))
+            MODE >= 6 ? __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, 8 * (b + 64 + lane), 0, 0))
                       : (b + 64 + lane < nit ? it[b + 64 + lane] : 0);
         const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
         const uint32_t w0n = dpp_next(w0, 0), w1n = dpp_next(w1, 0);
@@ -792,7 +828,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
                 cnt[5] += 1;
         }
         ZSK_T(2)
-        if (MODE == 6) {
+        if (MODE >= 6) {
             // the next batch's items before the flush: the wait for nxt (issued
             // at the top of this batch) then does not also wait for the
             // flush's stores
@@ -803,7 +839,11 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         // flush complete chunks (the frame's last chunk exactly)
         const bool last = b + nb >= nit;
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
-        if (!(DIAG & 34))
+        if (DIAG & 34)
+            ;
+        else if (MODE == 7)
+            flush_chunks4(S, O, fc, end_c, lane);
+        else
             for (uint32_t c = fc + lane; c < end_c; c += 64)
                 flush_chunk(S, O, c);
         fc = end_c;
@@ -819,7 +859,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         }
         wave_lds_sync();
         b += nb;
-        if (MODE != 6) {
+        if (MODE < 6) {
             const uint64_t a = __shfl_down(cur, nb & 63, 64);
             const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
             cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
@@ -861,10 +901,11 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 13: ZSK_X(4, 0); break;
     case 15: ZSK_X(5, 0); break;
     case 16: ZSK_X(6, 0); break;
-    case 17: ZSK_X(5, 4); break;
-    case 18: ZSK_X(5, 8); break;
-    case 19: ZSK_X(5, 34); break;
-    case 20: ZSK_X(5, 1); break;
+    case 17: ZSK_X(7, 0); break;
+    case 27: ZSK_X(5, 4); break;
+    case 28: ZSK_X(5, 8); break;
+    case 29: ZSK_X(5, 34); break;
+    case 30: ZSK_X(5, 1); break;
     case 8:
     case 14: {
         unsigned long long z[12] = {0};
@@ -896,7 +937,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<6, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<7, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
