@@ -173,11 +173,13 @@ def main():
     if n_timed:
         # the parse kernel the library picks for these frames (zsk_internal.h
         # chunk_parse_min: the chunk parse for big frames and small batches)
-        chunk = comp_bytes / nfr >= (49152 if nfr >= 32768 else 8192)
+        avg_c = comp_bytes / nfr
+        chunk = avg_c >= (49152 if nfr >= 32768 else 8192)
+        lane_parse = "lz4_lean_kernel" if avg_c >= 12288 else "lz4_scan_kernel"   # zsk_internal.h kLeanMinCsize
         names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": "zstd_frame_kernel + zstd_huf_kernel + zstd_seq_kernel",
                   "execute": "seq_exec_kernel", "hand-off": "zstd_check_kernel"} if zstd else
                  {"plan": "lz4_plan_direct_kernel",
-                  "parse": "lz4_chunk_kernel" if chunk else "lz4_lean_kernel",
+                  "parse": "lz4_chunk_kernel" if chunk else lane_parse,
                   "execute": "seq_exec_kernel", "hand-off": "lz4_wave_kernel<4096, 4, true>"})
         stages = {k: {"kernel": names[k], "avg_ms": round(v, 4)} for k, v in stage_ms.items()}
         if not zstd:   # the dominant kernel of the launch

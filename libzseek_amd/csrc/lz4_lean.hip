@@ -612,7 +612,7 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
-    uint32_t max_csize)
+    uint32_t max_csize, uint32_t min_csize)
 {
     __shared__ __attribute__((aligned(16))) uint8_t rings[kLW * 64 * kStride];
     __shared__ __attribute__((aligned(16))) uint64_t tabs[kLW * (kFlush + 1)];
@@ -622,8 +622,9 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     FrameDesc d = {0, 0, 0, 0};
     if (f < n)
         d = desc[f];
-    // frames of max_csize bytes and more belong to lz4_chunk_kernel
-    const bool act = f < n && d.c_size < max_csize;
+    // frames of max_csize bytes and more belong to lz4_chunk_kernel, frames
+    // under min_csize to lz4_scan_kernel
+    const bool act = f < n && d.c_size < max_csize && d.c_size >= min_csize;
     uint64_t rb0 = 0;
     uint32_t cap = 0;
     if (act) {
@@ -742,7 +743,7 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
 int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t max_csize,
-                    int diag)
+                    int diag, uint32_t min_csize)
 {
     if (nframes == 0)
         return 0;
@@ -751,7 +752,7 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
         unsigned long long z[6] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lean_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
         hipLaunchKernelGGL(lz4_lean_kernel<4>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize);
+                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_lean_stats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
         const double fr = nframes;
@@ -759,13 +760,13 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                         "exact-step runs %.1f items %.1f\n", z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr);
     } else if (diag & 2)
         hipLaunchKernelGGL(lz4_lean_kernel<2>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize);
+                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
     else if (diag & 1)
         hipLaunchKernelGGL(lz4_lean_kernel<1>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize);
+                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
     else
         hipLaunchKernelGGL(lz4_lean_kernel<0>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize);
+                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -884,12 +884,15 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                           : (diag & 0x4000)              ? 0u
                                                          : chunk_parse_min(nframes);
     if ((stages & 2) && !old_parse) {
-        if (cmin != 0 && !old_scan)
+        // lane per frame: lz4_lean_kernel for frames of [kLeanMinCsize, cmin)
+        // compressed bytes, lz4_scan_kernel below (or for all with 0x8000)
+        const uint32_t smax = old_scan ? cmin : min(cmin, kLeanMinCsize);
+        if (cmin > smax)
             launch_lz4_lean(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                            s->nitems, d_status, d_fail_at, stream, cmin, (diag >> 16) & 7);
-        else if (cmin != 0)
+                            s->nitems, d_status, d_fail_at, stream, cmin, (diag >> 16) & 7, smax);
+        if (smax != 0)
             launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                            s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0, cmin);
+                            s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0, smax);
         if (cmin != 0xFFFFFFFFu)
             launch_lz4_chunk(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                              s->nitems, d_status, d_fail_at, stream, cmin);

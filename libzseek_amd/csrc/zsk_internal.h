@@ -180,7 +180,11 @@ int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t max_csize,
-                    int diag = 0);
+                    int diag = 0, uint32_t min_csize = 0);
+// Frames under this many compressed bytes take the older lz4_scan_kernel
+// (its direct item stores beat the lean kernel's line flush on short frames:
+// 4 KiB frames 5.68 vs 6.71 ms per launch, config 3)
+constexpr uint32_t kLeanMinCsize = 12288;
 
 // Parse phase, one wave per frame, chunk-parallel (lz4_chunk.hip): the same
 // outputs as launch_lz4_scan for the frames of min_csize compressed bytes and
