@@ -17,7 +17,7 @@
 //     block headers, stored blocks, the end mark, every failure) goes to the
 //     exact byte-at-a-time step, which runs only when some lane of the wave
 //     needs it;
-//   * the ring is filled through a kD-deep software pipeline of 32-byte
+//   * the ring is filled through a D-deep software pipeline of 32-byte
 //     loads (one slot retired into the ring and one load issued per
 //     sub-step, every sub-step issuing the same vector-memory ops so the
 //     compiler's vmcnt waits retire exactly the slot consumed).
@@ -48,7 +48,6 @@ constexpr uint32_t kFlush = 8;           // item lines written per flush (one st
 // slots, so bytes up to ip + kRing - 47 always arrive: the fast step takes a
 // literal run only if its offset's 3 bytes lie within that reach
 constexpr uint32_t kLitFast = kRing - 47 - 5;
-constexpr uint32_t kD = 4;               // pipeline depth (slots of up to 64 bytes)
 constexpr uint32_t kOff = 0x80000000u;   // out-of-range buffer offset: op disabled
 
 enum : uint32_t { P_TOKEN = 0, P_LEXT, P_OFF, P_MEXT, P_BHDR, P_END, P_DONE };
@@ -606,8 +605,10 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
 }
 
 // DIAG (tuning builds): 1 = no line stores, 2 = every line to the wave's first line,
-// 4 = sub-step outcome counters (printed)
-template <int DIAG>
+// 4 = sub-step outcome counters (printed), 8 / 16 = a 4- / 1-deep fill pipeline
+// (default 2: at ~1,400 cycles per sub-step, 4 sub-steps cover the loads)
+// D: fill pipeline depth (slots of up to 64 bytes, retired every other sub-step)
+template <int DIAG, int D>
 __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))) void lz4_lean_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     const uint64_t ilo = uni64(wave_min64(act ? rb0 : ~0ull));
     const uint64_t ihi = uni64(wave_max64(act ? rb0 + cap : 0ull));
     const uint32_t steps = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(wave_max64(act ? (uint64_t)d.c_size : 0ull) * 2 + 64 * kD + 1024));
+        (int)(uint32_t)(wave_max64(act ? (uint64_t)d.c_size : 0ull) * 2 + 64 * D + 1024));
     if (clo == ~0ull)
         return;   // no frame in this wave (inactive lanes stay: flushes take all 64)
     Lane L;
@@ -682,9 +683,9 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
         if (hs >= 0)
             finish(L, hs);
     }
-    Fill sl[kD];
+    Fill sl[D];
 #pragma unroll
-    for (int i = 0; i < (int)kD; i++) {
+    for (int i = 0; i < D; i++) {
         sl[i].x = kOff;
         sl[i].h2 = false;
     }
@@ -696,7 +697,7 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
         // two sub-steps per slot: the first retires and refills it, the
         // second may run the exact step
 #pragma unroll
-        for (int i = 0; i < (int)kD; i++) {
+        for (int i = 0; i < D; i++) {
             sub<false, true, DIAG>(L, sl[i], lane, tab, fcnt);
             sub<true, false, DIAG>(L, sl[i], lane, tab, fcnt);
         }
@@ -751,7 +752,7 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     if (diag & 4) {
         unsigned long long z[6] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lean_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
-        hipLaunchKernelGGL(lz4_lean_kernel<4>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
+        hipLaunchKernelGGL((lz4_lean_kernel<4, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
                            nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_lean_stats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
@@ -759,13 +760,19 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
         fprintf(stderr, "lean parse per frame: sub-steps fast %.1f exact-needed %.1f waiting %.1f done %.1f "
                         "exact-step runs %.1f items %.1f\n", z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr);
     } else if (diag & 2)
-        hipLaunchKernelGGL(lz4_lean_kernel<2>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
+        hipLaunchKernelGGL((lz4_lean_kernel<2, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
                            nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
     else if (diag & 1)
-        hipLaunchKernelGGL(lz4_lean_kernel<1>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
+        hipLaunchKernelGGL((lz4_lean_kernel<1, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
+                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+    else if (diag & 8)
+        hipLaunchKernelGGL((lz4_lean_kernel<0, 4>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
+                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+    else if (diag & 16)
+        hipLaunchKernelGGL((lz4_lean_kernel<0, 1>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
                            nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
     else
-        hipLaunchKernelGGL(lz4_lean_kernel<0>, dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
+        hipLaunchKernelGGL((lz4_lean_kernel<0, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
                            nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

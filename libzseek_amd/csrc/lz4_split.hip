@@ -886,10 +886,10 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     if ((stages & 2) && !old_parse) {
         // lane per frame: lz4_lean_kernel for frames of [kLeanMinCsize, cmin)
         // compressed bytes, lz4_scan_kernel below (or for all with 0x8000)
-        const uint32_t smax = old_scan ? cmin : min(cmin, kLeanMinCsize);
+        const uint32_t smax = old_scan ? cmin : (cmin < kLeanMinCsize ? cmin : kLeanMinCsize);
         if (cmin > smax)
             launch_lz4_lean(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                            s->nitems, d_status, d_fail_at, stream, cmin, (diag >> 16) & 7, smax);
+                            s->nitems, d_status, d_fail_at, stream, cmin, (diag >> 16) & 31, smax);
         if (smax != 0)
             launch_lz4_scan(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                             s->nitems, d_status, d_fail_at, stream, (diag & 0x400) ? 1 : 0, smax);

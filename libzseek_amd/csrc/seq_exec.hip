@@ -604,7 +604,11 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // search over the pending destinations in LDS (v13), 5 = v13 with one flat
 // load per piece (v15), 6 = v15 with the next batch's items shifted in
 // before the flush (v16), 7 = v16 with four chunks' stage reads in flight per
-// flush step (v17, the default); 1-7 use exact readiness
+// flush step (v17, the default); 1-7 use exact readiness.  Tried and dropped
+// (same-box A/B, config 2): short runs' partial pieces dealt after the full
+// pieces so full slots write unconditionally (4.29 vs 4.13 ms per launch);
+// the rounds' readiness from an LDS bitmap of pending destination bytes set
+// and cleared with ds_or / ds_and (4.63 vs 4.13 ms)
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
@@ -841,7 +845,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
         if (DIAG & 34)
             ;
-        else if (MODE == 7)
+        else if (MODE >= 7)
             flush_chunks4(S, O, fc, end_c, lane);
         else
             for (uint32_t c = fc + lane; c < end_c; c += 64)
