@@ -607,6 +607,8 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // flush step (v17, the default); 1-7 use exact readiness.  Tried and dropped
 // (same-box A/B, config 2): short runs' partial pieces dealt after the full
 // pieces so full slots write unconditionally (4.29 vs 4.13 ms per launch);
+// each batch's flush deferred past the next batch's item decode (4.34 vs
+// 4.03 ms: round 0's load wait then also waits for the flush's stores);
 // the rounds' readiness from an LDS bitmap of pending destination bytes set
 // and cleared with ds_or / ds_and (4.63 vs 4.13 ms)
 template <int MODE, int DIAG, uint32_t OUTB>
