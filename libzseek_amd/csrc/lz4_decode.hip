@@ -697,6 +697,9 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     case 100: return launch_lz4_split_stages(3, 0x42000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 105: return launch_lz4_split_stages(3, 0x102000, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 104: return launch_lz4_split_stages(3, 0x82000, d_desc, nframes, d_comp, d_out, d_status, stream);
+    // 101 = execute v17 alone with its flush's stage reads but no stores (diagnostic)
+    case 101: return launch_lz4_split_stages(4, 0x21F, d_desc, nframes, d_comp, d_out, d_status, stream);
+    case 106: return launch_lz4_split_stages(4, 0x211, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 84: return launch_lz4_split_stages(4, 0x20D, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 38: return launch_lz4_split_stages(7, 0xA03, d_desc, nframes, d_comp, d_out, d_status, stream);
     case 34: return launch_lz4_split_stages(15, 0xA00, d_desc, nframes, d_comp, d_out, d_status, stream);

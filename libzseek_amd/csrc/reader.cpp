@@ -219,11 +219,12 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
     if (e == hipSuccess)
         e = hipMemsetD32Async((hipDeviceptr_t)g.d_status, ST_NOT_RUN, n, g.stream);
     if (r->type == ZSEEK_ZSTD) {
-        // zstd: plan + decode (zstd_decode.hip); failures carry no output offset
+        // zstd: plan + decode (zstd_decode.hip); a failure's output offset is
+        // its block's start (the frame's end for the end-of-frame checks)
         if (e == hipSuccess)
             e = hipMemsetD32Async((hipDeviceptr_t)g.d_fail, 0, n, g.stream);
         if (e == hipSuccess && zstd_decode_frames(g.d_desc, (uint32_t)n, g.d_comp, g.d_out,
-                                                  g.d_status, &g.zs, g.stream) != 0)
+                                                  g.d_status, &g.zs, g.stream, g.d_fail) != 0)
             e = hipErrorLaunchFailure;
     }
     const int engine = r->type == ZSEEK_ZSTD ? -1 : lz4_pick_engine((uint32_t)n);
@@ -314,6 +315,17 @@ bool lz4_partial_ok(int32_t st, uint64_t fail_at, uint64_t end_in_frame)
     return header_level(st) ? end_in_frame < fail_at : end_in_frame <= fail_at;
 }
 
+// The same for zstd: libzstd's streaming decoder (decompress.c:414-454)
+// decodes a block as soon as the previous one is flushed, so a request ending
+// exactly at the failing block's start meets the failure too (golden
+// zstd1m_block4_*: (0, 524287) succeeds, (0, 524288) fails).
+bool zstd_partial_ok(int32_t st, uint64_t fail_at, uint64_t end_in_frame)
+{
+    if (st == ST_SEEK_CHECKSUM || st == ST_NOT_RUN)
+        return false;
+    return end_in_frame < fail_at;
+}
+
 // Error text for a failed frame, worded as the reference words the same
 // failure.  Cached reads decode the whole frame ("decompress frame: ...",
 // decompress.c:766-768); no-cache reads first decode-and-discard the
@@ -347,11 +359,12 @@ void frame_error(zseek_reader *r, const BatchResult &br, size_t frame, size_t of
     if (r->type == ZSEEK_ZSTD) {
         // libzstd: ZSTD_decompressDCtx (cached) or ZSTD_decompressStream
         // (discard the in-frame prefix, then the caller's bytes,
-        // decompress.c:434-451); a whole-frame decode cannot tell in which
-        // of the two streaming calls libzstd would have met the failure, so
-        // a request starting inside the frame reports the discard phase
+        // decompress.c:434-451); the discard pass meets a failure whose block
+        // starts at or before the prefix's end (a block is decoded as soon
+        // as the previous one is flushed)
         if (!r->cache)
-            prefix = offset_in_frame ? "decompress discard data" : "decompress user data";
+            prefix = offset_in_frame > 0 && at <= offset_in_frame ? "decompress discard data"
+                                                                   : "decompress user data";
         set_error(errbuf, "%s: %s", prefix, status_name(st));
         return;
     }
@@ -465,9 +478,10 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
         const uint64_t lo = offset > st.d_off[f] ? offset : st.d_off[f];
         uint64_t good_end = br.first_bad < g_end ? st.d_off[br.first_bad] : st.d_off[g_end];
         // Without a cache the reference decodes a frame only as far as the
-        // request reaches (lz4_partial_ok); zstd failures carry no offset.
-        if (br.first_bad < g_end && !r->cache && r->type == ZSEEK_LZ4 &&
-            lz4_partial_ok(br.status, br.fail_at, end - st.d_off[br.first_bad]))
+        // request reaches (lz4_partial_ok, zstd_partial_ok).
+        if (br.first_bad < g_end && !r->cache &&
+            (r->type == ZSEEK_LZ4 ? lz4_partial_ok(br.status, br.fail_at, end - st.d_off[br.first_bad])
+                                  : zstd_partial_ok(br.status, br.fail_at, end - st.d_off[br.first_bad])))
             good_end = end;
         const uint64_t hi = end < good_end ? end : good_end;
         if (hi > lo) {

@@ -162,11 +162,16 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
 void zstd_scratch_free(ZstdScratch *s);
 int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      ZstdScratch *s, hipStream_t stream);
+// d_fail_at (optional): per failed frame, the output offset of its failing
+// block's start (its end for the end-of-frame checks); the execute still
+// writes the bytes before it.
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream);
+                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
+                       uint32_t *d_fail_at = nullptr);
 // plan + synchronize + reserve + decode
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream);
+                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
+                       uint32_t *d_fail_at = nullptr);
 
 // Parse phase, streaming lane-per-frame (lz4_scan.hip): same outputs as
 // lz4_parse_kernel.  version 1 = the if/return fast path (A/B builds).

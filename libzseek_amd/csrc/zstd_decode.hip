@@ -1636,7 +1636,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
     const uint8_t *__restrict__ slots, const uint8_t *__restrict__ hbad,
     const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
-    int32_t *__restrict__ status, uint64_t *__restrict__ ck)
+    int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at)
 {
     __shared__ uint32_t codes[89];
     __shared__ __attribute__((aligned(16))) uint64_t stage[8 * kSeqLanes];
@@ -1669,10 +1669,17 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
     uint64_t c = 0;
     int32_t st = zerr(ZE_GENERIC);
+    // output offset where a failure is met: the start of the failing block
+    // (every op of a block starts at its output start: literals advance
+    // nothing, sequences and runs advance o), the frame's end for its
+    // end-of-frame checks -- what libzstd's streaming decoder has produced
+    // when it meets the failure (decompress.c:414-454)
+    uint32_t fa = 0;
     auto replay = [&](__amdgpu_buffer_rsrc_t r, uint64_t base) {
         for (uint32_t k = 0; k < opn; k++) {
             const ZOp P = op[k];
             uint32_t err = 0;
+            fa = o;
             if (P.k == OP_LIT) {
                 const uint32_t h = *reinterpret_cast<const uint32_t *>(hbad + 4ull * P.a);
                 if (h)
@@ -1822,6 +1829,8 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     status[f] = st;
     nitems[f] = S.k;
     ck[f] = c;
+    if (fail_at)
+        fail_at[f] = st == ST_OK ? 0 : fa;
 }
 
 // XXH64 of [o0, cap) of a frame's output for frames flagged by the frame
@@ -1852,7 +1861,8 @@ __device__ __forceinline__ uint64_t xmerge(uint64_t acc, uint64_t v)
 __global__ __launch_bounds__(256) void zstd_check_kernel(const FrameDesc *__restrict__ desc, uint32_t n,
                                                          const uint8_t *__restrict__ out,
                                                          const uint64_t *__restrict__ ck,
-                                                         int32_t *__restrict__ status)
+                                                         int32_t *__restrict__ status,
+                                                         uint32_t *__restrict__ fail_at)
 {
     __shared__ uint64_t buf[4][128];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1914,8 +1924,11 @@ __global__ __launch_bounds__(256) void zstd_check_kernel(const FrameDesc *__rest
         h ^= h >> 29;
         h *= P64_3;
         h ^= h >> 32;
-        if ((uint32_t)h != want)
+        if ((uint32_t)h != want) {
             status[f] = zerr(ZE_CHECKSUM);
+            if (fail_at)
+                fail_at[f] = d.d_size;   // checked at the frame's end
+        }
     }
 }
 
@@ -2015,7 +2028,8 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 // Frame kernel -> Huffman kernel -> sequence kernel -> execute -> checksums,
 // back to back on the stream.  s must hold the last plan of these frames.
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream)
+                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
+                       uint32_t *d_fail_at)
 {
     if (nframes == 0)
         return 0;
@@ -2055,13 +2069,13 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     }
     hipLaunchKernelGGL(zstd_seq_kernel, dim3((nframes + kSeqLanes - 1) / kSeqLanes), dim3(64), 0, stream, d_desc, nframes,
                        d_comp, s->ops, s->blk_base, s->slots, s->hbad, s->rec_base, s->items, s->nitems,
-                       d_status, s->ck);
+                       d_status, s->ck, d_fail_at);
     stage_mark(2, stream);
     const int rc = launch_seq_exec_lit(d_desc, nframes, s->lit, d_out, s->rec_base, s->items,
                                        s->nitems, d_status, stream);
     stage_mark(3, stream);
     hipLaunchKernelGGL(zstd_check_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes,
-                       d_out, s->ck, d_status);
+                       d_out, s->ck, d_status, d_fail_at);
     stage_mark(4, stream);
     return rc == 0 && hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -2070,7 +2084,8 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 // synchronization point of the zstd path: the item slots and table slots of a
 // frame are only known once its block headers and sequence counts are read.
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream)
+                       uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
+                       uint32_t *d_fail_at)
 {
     if (nframes == 0)
         return 0;
@@ -2084,7 +2099,7 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         return -1;
     if (zstd_scratch_reserve(s, nframes, s->total[1], s->total[0], s->total[2], stream) != 0)
         return -1;
-    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream);
+    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
 }
 
 }   // namespace zsk

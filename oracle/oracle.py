@@ -72,6 +72,9 @@ class Oracle:
         L.orc_synth_gen.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
         L.orc_zstd_decode.restype = C.c_longlong
         L.orc_zstd_decode.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.orc_zstd_decode_at.restype = C.c_longlong
+        L.orc_zstd_decode_at.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                         C.POINTER(C.c_size_t)]
 
     # -- hashes -----------------------------------------------------------
     def xxh32(self, data: bytes, seed: int = 0) -> int:
@@ -119,6 +122,18 @@ class Oracle:
         if r < 0:
             return b"", -r
         return d[:r].tobytes(), 0
+
+    def zstd_decode_at(self, src: bytes, dst_cap: int):
+        """-> (decoded bytes, 0, None) or (bytes before the failing block, zstd
+        error code, fail_at): fail_at = output offset of the failing block's
+        start (frame end for the content-size / checksum checks)."""
+        s = np.frombuffer(src, np.uint8)
+        d = np.zeros(max(dst_cap, 1), np.uint8)
+        fa = C.c_size_t(0)
+        r = self.lib.orc_zstd_decode_at(s.ctypes.data, s.size, d.ctypes.data, dst_cap, C.byref(fa))
+        if r < 0:
+            return d[: fa.value].tobytes(), -r, fa.value
+        return d[:r].tobytes(), 0, None
 
     def seek_table(self, file: bytes):
         """-> dict(c_off, d_off, checksum, checksum_flag) or None."""

@@ -592,8 +592,9 @@ static int block(Dec *D, const uint8_t *p, size_t n, uint8_t *out, size_t cap, s
 
 /* one frame at src[0..n) (magic already checked); *used = its bytes */
 static int frame(const uint8_t *src, size_t n, uint8_t *out, size_t cap, size_t *produced,
-                 size_t *used, uint8_t *litbuf)
+                 size_t *used, uint8_t *litbuf, size_t *bstart)
 {
+    *bstart = 0;   /* output offset of the failing block (frame-level checks: the end) */
     if (n < 6 + 3)
         return -ZE_SRC_WRONG;
     const uint32_t fhd = src[4];
@@ -646,6 +647,7 @@ static int frame(const uint8_t *src, size_t n, uint8_t *out, size_t cap, size_t 
             rc = -ZE_SRC_WRONG;
             break;
         }
+        *bstart = o;
         const uint32_t bh = rd24(src + ip);
         const uint32_t last = bh & 1, type = (bh >> 1) & 3, bsize = bh >> 3;
         const size_t csz = type == 1 ? 1 : bsize;
@@ -681,6 +683,8 @@ static int frame(const uint8_t *src, size_t n, uint8_t *out, size_t cap, size_t 
         if (last)
             break;
     }
+    if (!rc)
+        *bstart = o;
     if (!rc && fcs != ~0ull && o != fcs)
         rc = -ZE_CORRUPTION;
     if (!rc && csum) {
@@ -701,17 +705,22 @@ static int frame(const uint8_t *src, size_t n, uint8_t *out, size_t cap, size_t 
 /*
  * ZSTD_decompressDCtx(dst, cap, src, n) restated: every frame in src
  * (skippable frames skipped).  Returns the decoded size (>= 0) or -code
- * (ZSTD_ErrorCode).
+ * (ZSTD_ErrorCode); on a failure *fail_at (if given) receives the output
+ * offset of the failing block's start (of the failing frame's end for its
+ * content-size / checksum checks, of the frame's start for its header), the
+ * bytes before it decoded in dst — the position libzstd's streaming decoder
+ * (decompress.c:414-454) reaches when it meets the failure.
  */
-long long orc_zstd_decode(const uint8_t *src, size_t n, uint8_t *dst, size_t cap)
+long long orc_zstd_decode_at(const uint8_t *src, size_t n, uint8_t *dst, size_t cap, size_t *fail_at)
 {
     uint8_t *lit = (uint8_t *)malloc(ZBLOCK_MAX + 64);
     if (!lit)
         return -ZE_GENERIC;
-    size_t o = 0;
+    size_t o = 0, fa = 0;
     long long rc = 0;
     int frames = 0;
     while (n >= 5) {
+        fa = o;
         const uint32_t magic = rd32(src);
         if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
             if (n < 8) {
@@ -732,9 +741,10 @@ long long orc_zstd_decode(const uint8_t *src, size_t n, uint8_t *dst, size_t cap
             break;
         }
         frames++;
-        size_t produced = 0, used = 0;
-        const int e = frame(src, n, dst + o, cap - o, &produced, &used, lit);
+        size_t produced = 0, used = 0, bs = 0;
+        const int e = frame(src, n, dst + o, cap - o, &produced, &used, lit, &bs);
         if (e) {
+            fa = o + bs;
             rc = e;
             break;
         }
@@ -742,8 +752,17 @@ long long orc_zstd_decode(const uint8_t *src, size_t n, uint8_t *dst, size_t cap
         src += used;
         n -= used;
     }
-    if (!rc && n)
+    if (!rc && n) {
+        fa = o;
         rc = -ZE_SRC_WRONG;
+    }
     free(lit);
+    if (rc && fail_at)
+        *fail_at = fa;
     return rc ? rc : (long long)o;
+}
+
+long long orc_zstd_decode(const uint8_t *src, size_t n, uint8_t *dst, size_t cap)
+{
+    return orc_zstd_decode_at(src, n, dst, cap, NULL);
 }

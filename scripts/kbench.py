@@ -68,7 +68,7 @@ def main():
         assert rc == 0, f"variant {v} launch failed"
 
     diag = {10, 11, 12, 31, 33, 38, 41, 44, 51, 53, 54, 60, 62, 63, 64, 65, 66, 67, 68, 69, 70, 74, 76,
-            82, 83, 84, 86, 87, 88, 90, 93, 94, 95, 96, 97, 100, 104, 105}
+            82, 83, 84, 86, 87, 88, 90, 93, 94, 95, 96, 97, 100, 104, 105, 101, 106}
 
     for v in variants:   # correctness once per variant
         out.zero_()

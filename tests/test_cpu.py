@@ -124,6 +124,60 @@ def test_oracle_errors_match_reference(oracle, golden, case):
             assert len(got) == q["ret"] and sha(got) == q["sha256"], q
 
 
+ZSTD_NAMES = {20: "Corrupted block detected", 22: "Restored data doesn't match checksum"}
+
+
+def _oracle_zstd_error(oracle, img, cache, off, cnt):
+    """The reference's zstd read restated on the oracle's decode: None or the
+    error string.  Without a cache libzstd's streaming decoder (decompress.c:
+    414-454) decodes a block as soon as the previous one is flushed, so a
+    request fails iff it ends at or past the failing block's start, and it
+    fails in the discard pass iff that block starts at or before the request."""
+    st = oracle.seek_table(img)
+    i = int(np.searchsorted(st["d_off"], np.uint64(off), side="right") - 1)
+    c0, c1 = int(st["c_off"][i]), int(st["c_off"][i + 1])
+    dsz = int(st["d_off"][i + 1] - st["d_off"][i])
+    _, code, fa = oracle.zstd_decode_at(img[c0:c1], dsz)
+    if code == 0:
+        return None
+    rel = off - int(st["d_off"][i])
+    if cache:
+        prefix = "decompress frame"
+    elif rel + min(cnt, dsz - rel) < fa:
+        return None
+    elif rel > 0 and fa <= rel:
+        prefix = "decompress discard data"
+    else:
+        prefix = "decompress user data"
+    return f"{prefix}: {ZSTD_NAMES[code]}"
+
+
+@pytest.mark.parametrize("case", ["zstd1m_block4_first", "zstd1m_block4_type"])
+def test_oracle_zstd_partial_reads_match_reference(oracle, golden, case):
+    """A corrupt 5th block of a 1 MiB zstd frame (golden, made by the compiled
+    reference): the oracle's failing-block offset and the streaming rule give
+    the reference's result for every query, bytes included."""
+    rec = golden["corrupt"][case]
+    img = bytearray(golden_file(rec["base"]))
+    for at, v in rec["mutations"]:
+        img[at] = v
+    img = bytes(img)
+    st = oracle.seek_table(img)
+    for q in rec["results"]:
+        err = _oracle_zstd_error(oracle, img, q["cache"], q["offset"], q["count"])
+        if q["ret"] == -1:
+            assert err == q["error"], q
+            continue
+        assert err is None, q
+        i = int(np.searchsorted(st["d_off"], np.uint64(q["offset"]), side="right") - 1)
+        c0, c1 = int(st["c_off"][i]), int(st["c_off"][i + 1])
+        dsz = int(st["d_off"][i + 1] - st["d_off"][i])
+        data, _, _ = oracle.zstd_decode_at(img[c0:c1], dsz)
+        rel = q["offset"] - int(st["d_off"][i])
+        got = data[rel: rel + min(q["count"], dsz - rel)]
+        assert len(got) == q["ret"] and sha(got) == q["sha256"], q
+
+
 def test_oracle_truncated_block_is_an_error(oracle, golden):
     """The reference spins forever here (golden: 'hang'); the restatement
     (and the GPU path) report an error instead."""

@@ -248,3 +248,25 @@ def test_zstd_corrupt_frame_error_text(gpu, zs, oracle, cache):
             with pytest.raises(zs.ZseekError) as e:
                 r.pread(100, 2 * 65536 + 1000)
             assert str(e.value) == "decompress discard data: Corrupted block detected"
+
+
+@pytest.mark.parametrize("case", ["zstd1m_block4_first", "zstd1m_block4_type"])
+def test_zstd_partial_reads_golden(gpu, zs, golden, case):
+    """A corrupt 5th block of a 1 MiB frame (golden, made by the compiled
+    reference): without a cache a request ending before the bad block gets its
+    bytes, one reaching it gets libzstd's user/discard-data error; with a
+    cache every read of the frame fails."""
+    rec = golden["corrupt"][case]
+    base = bytearray(golden_file(rec["base"]))
+    for at, v in rec["mutations"]:
+        base[at] = v
+    for q in rec["results"]:
+        with zs.Reader(bytes(base), q["cache"]) as r:
+            out = np.empty(max(q["count"], 1), np.uint8)
+            ret = r.pread_raw(out.ctypes.data, q["count"], q["offset"])
+            if q["ret"] < 0:
+                assert ret == -1, q
+                assert r.error == q["error"], q
+            else:
+                assert ret == q["ret"], q
+                assert sha(out[: q["ret"]]) == q["sha256"], q
