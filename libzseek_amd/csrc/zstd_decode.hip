@@ -1485,52 +1485,41 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
 // Replays the frame's op list: FSE states (tables from the block slots),
 // repeat offsets, every libzstd check, items in the LZ4 item format with the
 // full offset; then the final status, item count and checksum request.
-// Items of one lane, staged in LDS (8 per lane, item j of lane l at
-// stage + (j & 7) * 256 + 8 * l) and flushed to the frame's slots 4 or more
-// at a time.
+// Items go straight from registers to the frame's slots: every emit issues
+// exactly three 8-byte buffer stores (the ones it does not need are disabled
+// by an out-of-range offset), so the compiler's vmcnt waits for the next
+// sequence's bitstream window -- loaded before the stores -- never wait on
+// them.  Consecutive 8-byte stores of a lane fill its lines in L2.
 struct LSink {
-    uint64_t *base;
-    uint32_t k, f, cap;
-    uint32_t stage;
+    __amdgpu_buffer_rsrc_t r;   // the wave's item slots (one resource per replay)
+    uint32_t ib;                // this frame's slot 0 in r (items)
+    uint32_t k, cap;
 };
 
-__device__ __forceinline__ void lput(LSink &S, uint64_t v)
+typedef uint32_t u32x2s __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void lput3(const LSink &S, uint32_t n, uint64_t v0, uint64_t v1, uint64_t v2)
 {
-    *la<uint64_t>(S.stage + (S.k & 7) * 256) = v;
-    S.k++;
+    const uint32_t a = 8u * (S.ib + S.k);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2s, v0), S.r, n >= 1 ? a : kOOR, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2s, v1), S.r, n >= 2 ? a + 8 : kOOR + 8, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2s, v2), S.r, n >= 3 ? a + 16 : kOOR + 16, 0, 0);
 }
 
 // the 8-byte item format of lz4_split.hip (Sink), with the full offset in
-// extended items
+// extended items (an extended pair never starts in slot 63 of a 64-slot
+// group: a zero item pads it)
 __device__ __forceinline__ bool lemit(LSink &S, uint32_t src, uint32_t lit, uint32_t off, uint32_t ml)
 {
-    if (lit > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF) {
-        const uint32_t pad = (S.k & 63) == 63 ? 1 : 0;
-        if (S.k + pad + 2 > S.cap)
-            return false;
-        if (pad)
-            lput(S, 0);
-        lput(S, ((uint64_t)off << 32) | src | kItemExt);
-        lput(S, ((uint64_t)ml << 32) | lit);
-        return true;
-    }
-    if (S.k + 1 > S.cap)
-        return false;
-    lput(S, ((uint64_t)(off | lit << 16 | (ml ? ml - 3 : 0) << 24) << 32) | src);
-    return true;
-}
-
-__device__ __forceinline__ void lflush(LSink &S)
-{
-    for (uint32_t j = S.f; j < S.k; j++)
-        S.base[j] = *la<uint64_t>(S.stage + (j & 7) * 256);
-    S.f = S.k;
-}
-
-__device__ __forceinline__ void lmaybe(LSink &S)
-{
-    if (S.k - S.f >= 4)
-        lflush(S);
+    const bool ext = lit > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF;
+    const uint32_t pad = ext && (S.k & 63) == 63 ? 1u : 0u;
+    const uint32_t n = ext ? 2 + pad : 1;
+    const bool ok = S.k + n <= S.cap;
+    const uint64_t e0 = ((uint64_t)off << 32) | src | kItemExt, e1 = ((uint64_t)ml << 32) | lit;
+    const uint64_t sh = ((uint64_t)(off | lit << 16 | (ml ? ml - 3 : 0) << 24) << 32) | src;
+    lput3(S, ok ? n : 0, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
+    S.k += ok ? n : 0;
+    return ok;
 }
 
 // Sequence bitstream reader, no ring: at each sequence the lane loads the 16
@@ -1548,6 +1537,8 @@ struct SRd {
     uint64_t C;         // bits [base, base + 64)
     int32_t base, nb;   // nb = cur - base valid bits at the bottom of C
     uint32_t r1, r0;    // the two dwords below C
+    u32x4 L;            // the window in flight (sr_issue -> sr_use)
+    int32_t D;
 };
 
 // len >= 1.  False when the stream's last byte (its end mark) is 0.
@@ -1562,24 +1553,30 @@ __device__ __forceinline__ bool sr_init(SRd &b, __amdgpu_buffer_rsrc_t r, uint32
     return last != 0;
 }
 
-__device__ __forceinline__ uint32_t sr_dw(const SRd &b, int32_t k)
-{
-    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(b.r, k >= 0 ? b.x0 + 4u * (uint32_t)k : kOOR, 0, 0);
-}
-
-// the window below the cursor (issued with the step's table loads)
-__device__ __forceinline__ void sr_load(SRd &b)
+// the window below the cursor in two halves: sr_issue loads it (one 16-byte
+// load on every path, so the compiler's vmcnt counts stay exact; near the
+// stream's base it loads dwords [0, 4) and sr_use shifts them up by -k0,
+// dwords below the base reading as 0), sr_use unpacks it where it is first
+// needed -- a sequence's window is issued at the end of the one before,
+// ahead of that one's item stores
+__device__ __forceinline__ void sr_issue(SRd &b)
 {
     const int32_t D = (b.cur + 31) >> 5, k0 = D - 4;   // dwords [k0, D) hold bits [32 k0, 32 D)
+    b.L = __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(b.r, b.x0 + 4u * (uint32_t)(k0 > 0 ? k0 : 0), 0, 0));
+    b.D = D;
+}
+
+__device__ __forceinline__ void sr_use(SRd &b)
+{
+    const int32_t D = b.D, k0 = D - 4;
+    const u32x4 L = b.L;
+    const int32_t sft = k0 < 0 ? -k0 : 0;
     u32x4 w;
-    if (k0 >= 0) {
-        w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(b.r, b.x0 + 4u * (uint32_t)k0, 0, 0));
-    } else {   // near the stream's base: dwords below it read as 0
-        w.x = sr_dw(b, k0);
-        w.y = sr_dw(b, k0 + 1);
-        w.z = sr_dw(b, k0 + 2);
-        w.w = sr_dw(b, k0 + 3);
-    }
+    w.x = sft == 0 ? L.x : 0u;
+    w.y = sft == 0 ? L.y : sft == 1 ? L.x : 0u;
+    w.z = sft == 0 ? L.z : sft == 1 ? L.y : sft == 2 ? L.x : 0u;
+    w.w = sft == 0 ? L.w : sft == 1 ? L.z : sft == 2 ? L.y : sft == 3 ? L.x : 0u;
     if (k0 <= 0) {   // dword 0 holds the stream's first byte: clear the bits below it
         w.x &= above(b.xs, 32 * k0);
         w.y &= above(b.xs, 32 * k0 + 32);
@@ -1591,6 +1588,12 @@ __device__ __forceinline__ void sr_load(SRd &b)
     b.nb = b.cur - b.base;   // 33..64
     b.r1 = w.y;
     b.r0 = w.x;
+}
+
+__device__ __forceinline__ void sr_load(SRd &b)
+{
+    sr_issue(b);
+    sr_use(b);
 }
 
 __device__ __forceinline__ void sr_fill(SRd &b)
@@ -1639,7 +1642,6 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at)
 {
     __shared__ uint32_t codes[89];
-    __shared__ __attribute__((aligned(16))) uint64_t stage[8 * kSeqLanes];
     __shared__ __attribute__((aligned(16))) uint16_t ftab[kSeqLanes * kSeqCells];
     for (uint32_t i = threadIdx.x; i < 89; i += 64)
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
@@ -1660,10 +1662,10 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const ZOp *op = reinterpret_cast<const ZOp *>(ops) + ob;
     LSink S;
     const uint64_t rb = rec_base[f];
-    S.base = items + rb;
-    S.k = S.f = 0;
+    S.k = 0;
     S.cap = (uint32_t)(rec_base[f + 1] - rb);
-    S.stage = (uint32_t)(uintptr_t)lp<uint64_t>(&stage[lane]);
+    // the wave's item slots as one resource (else lane by lane, as comp)
+    const uint64_t ilo = uni64(wave_min64(rb)), ihi = uni64(wave_max64(rb + S.cap));
     uint16_t *const mytab = &ftab[lane * kSeqCells];
     const uint32_t cap = d.d_size;
     uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
@@ -1675,7 +1677,9 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     // end-of-frame checks -- what libzstd's streaming decoder has produced
     // when it meets the failure (decompress.c:414-454)
     uint32_t fa = 0;
-    auto replay = [&](__amdgpu_buffer_rsrc_t r, uint64_t base) {
+    auto replay = [&](__amdgpu_buffer_rsrc_t r, uint64_t base, __amdgpu_buffer_rsrc_t ir, uint64_t i0) {
+        S.r = ir;
+        S.ib = (uint32_t)(rb - i0);
         for (uint32_t k = 0; k < opn; k++) {
             const ZOp P = op[k];
             uint32_t err = 0;
@@ -1699,7 +1703,8 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
                         const uint32_t nll = 1u << tll, nof = 1u << tof, nml = 1u << tml;
                         const uint16_t *TL = gt + kFseOff[0], *TO = gt + kFseOff[1], *TM = gt + kFseOff[2];
-                        if (nll + nof + nml <= 768) {
+                        const bool fit = nll + nof + nml <= 768;
+                        if (fit) {
                             auto cp = [&](const uint16_t *src, uint32_t at, uint32_t cells) {
                                 for (uint32_t c = 0; c < cells; c += 8)
                                     *reinterpret_cast<u32x4 *>(mytab + at + c) = *reinterpret_cast<const u32x4 *>(src + c);
@@ -1707,69 +1712,83 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             cp(TL, 0, nll);
                             cp(TO, nll, nof);
                             cp(TM, nll + nof, nml);
-                            TL = mytab;
-                            TO = mytab + nll;
-                            TM = mytab + nll + nof;
                         }
-                        sr_load(b);
-
-                        uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
-                        sr_done(b);
-                        for (uint32_t i = 0; i < nseq; i++) {
-                            const uint32_t ell = TL[sll], eof = TO[sof], eml = TM[sml];
+                        // the sequence loop, over tables in LDS (ds_read: the
+                        // lookups' waits stay off vmcnt) or in the slot
+                        auto seqs = [&](auto TLf, auto TOf, auto TMf) {
                             sr_load(b);
-                            const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
-                            if (llc > 35 || ofc > 31 || mlc > 52) {
-                                err = ZE_CORRUPT;
-                                break;
-                            }
-                            // offset bits (<= 31; the window holds >= 33), a fill before
-                            // the ML + LL extra bits (<= 32) and one before the three
-                            // state updates (<= 26)
-                            const uint64_t ofv = (1ull << ofc) + sr_take(b, ofc);
-                            const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
-                            sr_fill(b);
-                            const uint32_t ml = (mlcode & 0xFFFFFF) + sr_take(b, mlcode >> 24);
-                            const uint32_t ll = (llcode & 0xFFFFFF) + sr_take(b, llcode >> 24);
-                            uint64_t off;
-                            if (ofv > 3) {
-                                off = ofv - 3;
-                                rep2 = rep1;
-                                rep1 = rep0;
-                                rep0 = (uint32_t)off;
-                            } else {
-                                const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0);
-                                if (idx == 0) {
-                                    off = rep0;
-                                } else {
-                                    off = idx == 1 ? rep1 : idx == 2 ? rep2 : rep0 - 1;
-                                    if (off == 0)
-                                        off = 1;
-                                    if (idx != 1)
-                                        rep2 = rep1;
+
+                            uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
+                            sr_done(b);
+                            sr_issue(b);
+                            // three disabled stores: the loop's entry then has the
+                            // VMEM pattern of its back edge (window, then three
+                            // stores), so the window's wait stays vmcnt(3)
+                            lput3(S, 0, 0, 0, 0);
+                            for (uint32_t i = 0; i < nseq; i++) {
+                                const uint32_t ell = TLf(sll), eof = TOf(sof), eml = TMf(sml);
+                                sr_use(b);
+                                const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
+                                if (llc > 35 || ofc > 31 || mlc > 52) {
+                                    err = ZE_CORRUPT;
+                                    break;
+                                }
+                                // offset bits (<= 31; the window holds >= 33), a fill before
+                                // the ML + LL extra bits (<= 32) and one before the three
+                                // state updates (<= 26)
+                                const uint64_t ofv = (1ull << ofc) + sr_take(b, ofc);
+                                const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
+                                sr_fill(b);
+                                const uint32_t ml = (mlcode & 0xFFFFFF) + sr_take(b, mlcode >> 24);
+                                const uint32_t ll = (llcode & 0xFFFFFF) + sr_take(b, llcode >> 24);
+                                uint64_t off;
+                                if (ofv > 3) {
+                                    off = ofv - 3;
+                                    rep2 = rep1;
                                     rep1 = rep0;
                                     rep0 = (uint32_t)off;
+                                } else {
+                                    const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0);
+                                    if (idx == 0) {
+                                        off = rep0;
+                                    } else {
+                                        off = idx == 1 ? rep1 : idx == 2 ? rep2 : rep0 - 1;
+                                        if (off == 0)
+                                            off = 1;
+                                        if (idx != 1)
+                                            rep2 = rep1;
+                                        rep1 = rep0;
+                                        rep0 = (uint32_t)off;
+                                    }
                                 }
+                                sr_fill(b);
+                                sll = fse_next(b, ell, tll);
+                                sml = fse_next(b, eml, tml);
+                                sof = fse_next(b, eof, tof);
+                                sr_done(b);
+                                sr_issue(b);
+                                if ((uint64_t)o + ll + ml > cap)
+                                    err = ZE_DST_SMALL;
+                                else if (le - lp_ < ll)
+                                    err = ZE_CORRUPT;
+                                else if (off > (uint64_t)o + ll)
+                                    err = ZE_CORRUPT;
+                                else if (!lemit(S, lp_, ll, (uint32_t)off, ml))
+                                    err = ZE_GENERIC;
+                                if (err)
+                                    break;
+                                lp_ += ll;
+                                o += ll + ml;
                             }
-                            sr_fill(b);
-                            sll = fse_next(b, ell, tll);
-                            sml = fse_next(b, eml, tml);
-                            sof = fse_next(b, eof, tof);
-                            sr_done(b);
-                            if ((uint64_t)o + ll + ml > cap)
-                                err = ZE_DST_SMALL;
-                            else if (le - lp_ < ll)
-                                err = ZE_CORRUPT;
-                            else if (off > (uint64_t)o + ll)
-                                err = ZE_CORRUPT;
-                            else if (!lemit(S, lp_, ll, (uint32_t)off, ml))
-                                err = ZE_GENERIC;
-                            if (err)
-                                break;
-                            lmaybe(S);
-                            lp_ += ll;
-                            o += ll + ml;
-                        }
+                        };
+                        const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(mytab);
+                        if (fit)
+                            seqs([&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * x); },
+                                 [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + x)); },
+                                 [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + nof + x)); });
+                        else
+                            seqs([&](uint32_t x) -> uint32_t { return TL[x]; }, [&](uint32_t x) -> uint32_t { return TO[x]; },
+                                 [&](uint32_t x) -> uint32_t { return TM[x]; });
                         if (!err && b.cur - b.xs > 0)
                             err = ZE_CORRUPT;
                     }
@@ -1811,19 +1830,21 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                 st = zerr(err);
                 break;
             }
-            lmaybe(S);
         }
-        lflush(S);
     };
-    if (hi > lo && hi - lo < kMaxSpan) {
-        replay(span_rsrc(comp, lo, hi - lo), lo);
+    auto irsrc = [&](uint64_t a, uint64_t b) {
+        return __builtin_amdgcn_make_buffer_rsrc((void *)(items + a), 0, (int)(uint32_t)(8 * (b - a)), kRsrcDw3);
+    };
+    if (hi > lo && hi - lo < kMaxSpan && 8 * (ihi - ilo) < kMaxSpan) {
+        replay(span_rsrc(comp, lo, hi - lo), lo, irsrc(ilo, ihi), ilo);
     } else {
         for (uint64_t m = __ballot(true); m; m &= m - 1) {
             const int l = __builtin_ctzll(m);
             const uint64_t s0 = uni64(__shfl(d.c_off, l, 64)) & ~15ull;
             const uint64_t s1 = uni64(__shfl(d.c_off + d.c_size, l, 64));
+            const uint64_t i0 = uni64(__shfl(rb, l, 64)), i1 = uni64(__shfl(rb + S.cap, l, 64));
             if ((int)lane == l)
-                replay(span_rsrc(comp, s0, s1 - s0), s0);
+                replay(span_rsrc(comp, s0, s1 - s0), s0, irsrc(i0, i1), i0);
         }
     }
     status[f] = st;
