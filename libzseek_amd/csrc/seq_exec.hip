@@ -613,7 +613,10 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // each batch's flush deferred past the next batch's item decode (4.34 vs
 // 4.03 ms: round 0's load wait then also waits for the flush's stores);
 // the rounds' readiness from an LDS bitmap of pending destination bytes set
-// and cleared with ds_or / ds_and (4.63 vs 4.13 ms)
+// and cleared with ds_or / ds_and (4.63 vs 4.13 ms; six waves per SIMD (80 VGPRs: 10
+// spilled, 5.33 vs 4.04 ms); round 0's slot loads retired inside each deal
+// step, so the deal's first step issues without waiting on the item prefetch
+// and the last flush (4.001 vs 4.006 ms, no gain)
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
