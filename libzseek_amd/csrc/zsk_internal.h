@@ -146,6 +146,7 @@ struct ZstdScratch {
     uint64_t *blk_base = nullptr;  // n + 1 block slot offsets
     uint32_t *nitems = nullptr;
     uint64_t *ck = nullptr;        // per-frame checksum request
+    uint32_t *stop = nullptr;      // per-frame op index the sequence replay stopped at
     uint8_t *lit = nullptr;        // literal scratch (output-sized + 64)
     uint64_t *items = nullptr;
     uint8_t *ops = nullptr;        // per-frame op lists (4 per block + 4), 32 B each
@@ -154,6 +155,8 @@ struct ZstdScratch {
     uint8_t *hbad = nullptr;       // per Huffman stream: 1 = corrupt
     uint64_t *d_total = nullptr;   // [0] item total, [1] output extent, [2] blocks
     uint64_t *total = nullptr;     // pinned host copy of d_total
+    hipStream_t side = nullptr;    // the Huffman kernel's stream (beside the sequence replay)
+    hipEvent_t ev_tab = nullptr, ev_huf = nullptr;
     uint32_t frames_cap = 0;
     uint64_t lit_cap = 0, items_cap = 0, blocks_cap = 0, ops_cap = 0;
 };

@@ -1335,6 +1335,7 @@ __device__ __forceinline__ int32_t br_left(const BRd &b)
 // shift takes the cell's low 5 bits, nbits).  16 decoded bytes are stored at
 // a time, aligned.
 constexpr uint32_t kHufLdsCells = 2048;
+__device__ u32x4 g_huf_sink[64];   // the first step's store of every stream (never read)
 
 template <int G, int F, int DIAG, typename Tab>
 __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *out, uint64_t dst, uint32_t cnt,
@@ -1363,8 +1364,10 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     while (i + 16 <= lim) {
         if (!(DIAG & 2))
             br_step<F>(b);
-        if (i != i0 && !(DIAG & 1))
-            *reinterpret_cast<u32x4 *>(out + i - 16) = prev;
+        // unconditional (the first step's goes to a sink): a conditional
+        // store would make the compiler's chunk waits vmcnt(0), i.e. wait on it
+        if (!(DIAG & 1))
+            *(i != i0 ? reinterpret_cast<u32x4 *>(out + i - 16) : &g_huf_sink[threadIdx.x & 63]) = prev;
         u32x4 acc = {0, 0, 0, 0};
         uint32_t w = 0, used = 0;
 #pragma unroll
@@ -1636,8 +1639,8 @@ constexpr uint32_t kSeqCells = 800;   // u16 cells per frame (768 + copy slack)
 
 __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
-    const uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
-    const uint8_t *__restrict__ slots, const uint8_t *__restrict__ hbad,
+    uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
+    const uint8_t *__restrict__ slots, uint32_t *__restrict__ stop,
     const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
     int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at)
 {
@@ -1659,7 +1662,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
         return;
     const uint64_t ob = op_base(blk_base, f);
     const uint32_t opn = (uint32_t)(op_base(blk_base, f + 1) - ob);
-    const ZOp *op = reinterpret_cast<const ZOp *>(ops) + ob;
+    ZOp *op = reinterpret_cast<ZOp *>(ops) + ob;
     LSink S;
     const uint64_t rb = rec_base[f];
     S.k = 0;
@@ -1677,6 +1680,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     // end-of-frame checks -- what libzstd's streaming decoder has produced
     // when it meets the failure (decompress.c:414-454)
     uint32_t fa = 0;
+    uint32_t kstop = opn;   // the op the replay stopped at
     auto replay = [&](__amdgpu_buffer_rsrc_t r, uint64_t base, __amdgpu_buffer_rsrc_t ir, uint64_t i0) {
         S.r = ir;
         S.ib = (uint32_t)(rb - i0);
@@ -1684,10 +1688,13 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
             const ZOp P = op[k];
             uint32_t err = 0;
             fa = o;
+            kstop = k;
             if (P.k == OP_LIT) {
-                const uint32_t h = *reinterpret_cast<const uint32_t *>(hbad + 4ull * P.a);
-                if (h)
-                    err = ZE_CORRUPT;
+                // the Huffman kernel runs beside this one: whether this
+                // block's literals decoded is settled by zstd_lit_fix_kernel,
+                // from the item count and output offset kept here
+                op[k].b = S.k;
+                op[k].c = o;
             } else if (P.k == OP_SEQ) {
                 const uint32_t nseq = P.a;
                 uint32_t lp_ = P.d;
@@ -1850,8 +1857,38 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     status[f] = st;
     nitems[f] = S.k;
     ck[f] = c;
+    stop[f] = kstop;
     if (fail_at)
         fail_at[f] = st == ST_OK ? 0 : fa;
+}
+
+// After the Huffman and sequence kernels (which run side by side): a frame
+// whose replay passed a literals op of a block with a corrupt Huffman stream
+// fails there, as libzstd does — that block's literals are decoded before its
+// sequences — with the items and output offset the replay had at that op.
+__global__ __launch_bounds__(256) void zstd_lit_fix_kernel(uint32_t n, const uint8_t *__restrict__ ops,
+                                                           const uint64_t *__restrict__ blk_base,
+                                                           const uint8_t *__restrict__ hbad,
+                                                           const uint32_t *__restrict__ stop,
+                                                           int32_t *__restrict__ status,
+                                                           uint32_t *__restrict__ nitems,
+                                                           uint32_t *__restrict__ fail_at)
+{
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= n)
+        return;
+    const ZOp *op = reinterpret_cast<const ZOp *>(ops) + op_base(blk_base, f);
+    const uint32_t ks = stop[f];
+    for (uint32_t k = 0; k < ks; k++) {
+        const ZOp P = op[k];
+        if (P.k == OP_LIT && *reinterpret_cast<const uint32_t *>(hbad + 4ull * P.a)) {
+            status[f] = zerr(ZE_CORRUPT);
+            nitems[f] = P.b;
+            if (fail_at)
+                fail_at[f] = P.c;
+            return;
+        }
+    }
 }
 
 // XXH64 of [o0, cap) of a frame's output for frames flagged by the frame
@@ -1978,15 +2015,20 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
                          uint64_t blocks, hipStream_t stream)
 {
     (void)stream;
+    if (!s->side &&
+        (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
+         hipEventCreateWithFlags(&s->ev_tab, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&s->ev_huf, hipEventDisableTiming) != hipSuccess))
+        return -1;
     if (frames + 1 > s->frames_cap) {
         const uint32_t cap = frames + 1 < 4096 ? 4096 : frames + 1;
         for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
-                        (void *)s->nitems, (void *)s->ck, (void *)s->d_total})
+                        (void *)s->nitems, (void *)s->ck, (void *)s->stop, (void *)s->d_total})
             if (p)
                 (void)hipFree(p);
         if (s->total)
             (void)hipHostFree(s->total);
-        s->bound = s->bblk = s->nitems = nullptr;
+        s->bound = s->bblk = s->nitems = s->stop = nullptr;
         s->rec_base = s->blk_base = s->ck = s->d_total = s->total = nullptr;
         s->frames_cap = 0;
         if (hipMalloc((void **)&s->bound, sizeof(uint32_t) * cap) != hipSuccess ||
@@ -1995,6 +2037,7 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
             hipMalloc((void **)&s->blk_base, sizeof(uint64_t) * (cap + 1)) != hipSuccess ||
             hipMalloc((void **)&s->nitems, sizeof(uint32_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->ck, sizeof(uint64_t) * cap) != hipSuccess ||
+            hipMalloc((void **)&s->stop, sizeof(uint32_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->d_total, 4 * sizeof(uint64_t)) != hipSuccess ||
             hipHostMalloc((void **)&s->total, 4 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
             return -1;
@@ -2017,12 +2060,18 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
 void zstd_scratch_free(ZstdScratch *s)
 {
     for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
-                    (void *)s->nitems, (void *)s->ck, (void *)s->lit, (void *)s->items, (void *)s->ops,
-                    (void *)s->hjobs, (void *)s->slots, (void *)s->hbad, (void *)s->d_total})
+                    (void *)s->nitems, (void *)s->ck, (void *)s->stop, (void *)s->lit, (void *)s->items,
+                    (void *)s->ops, (void *)s->hjobs, (void *)s->slots, (void *)s->hbad, (void *)s->d_total})
         if (p)
             (void)hipFree(p);
     if (s->total)
         (void)hipHostFree(s->total);
+    if (s->ev_tab)
+        (void)hipEventDestroy(s->ev_tab);
+    if (s->ev_huf)
+        (void)hipEventDestroy(s->ev_huf);
+    if (s->side)
+        (void)hipStreamDestroy(s->side);
     *s = ZstdScratch();
 }
 
@@ -2063,34 +2112,47 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     hipLaunchKernelGGL(zstd_frame_kernel, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc,
                        nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops,
                        s->slots, s->hjobs);
+    // the Huffman streams decode on a side stream beside the sequence replay
+    // (neither reads the other's output); zstd_lit_fix_kernel joins them
     if (nj) {
+        if (hipEventRecord(s->ev_tab, stream) != hipSuccess || hipStreamWaitEvent(s->side, s->ev_tab, 0) != hipSuccess)
+            return -1;
         static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
         const dim3 g((nj + 63) / 64), b(64);
+        hipStream_t const hs = s->side;
         if (diag) {
             unsigned int z[32] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
         }
         switch (diag) {
-        case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        case 7: hipLaunchKernelGGL(zstd_huf_kernel<7>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        default: hipLaunchKernelGGL(zstd_huf_kernel<8>, g, b, 0, stream, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        case 7: hipLaunchKernelGGL(zstd_huf_kernel<7>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
+        default: hipLaunchKernelGGL(zstd_huf_kernel<8>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
         }
         if (diag) {
             unsigned int z[32] = {};
-            (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_hdiag), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
-            (void)hipStreamSynchronize(stream);
+            (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_hdiag), sizeof(z), 0, hipMemcpyDeviceToHost, hs);
+            (void)hipStreamSynchronize(hs);
             fprintf(stderr, "huf diag %d: lgmax", diag);
             for (int i = 0; i < 16; i++)
                 if (z[i])
                     fprintf(stderr, " %d:%u", i, z[i]);
             fprintf(stderr, "  global %u lds %u\n", z[16], z[17]);
         }
+        if (hipEventRecord(s->ev_huf, hs) != hipSuccess)
+            return -1;
     }
     hipLaunchKernelGGL(zstd_seq_kernel, dim3((nframes + kSeqLanes - 1) / kSeqLanes), dim3(64), 0, stream, d_desc, nframes,
-                       d_comp, s->ops, s->blk_base, s->slots, s->hbad, s->rec_base, s->items, s->nitems,
+                       d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
                        d_status, s->ck, d_fail_at);
+    if (nj) {
+        if (hipStreamWaitEvent(stream, s->ev_huf, 0) != hipSuccess)
+            return -1;
+        hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, nframes, s->ops,
+                           s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at);
+    }
     stage_mark(2, stream);
     const int rc = launch_seq_exec_lit(d_desc, nframes, s->lit, d_out, s->rec_base, s->items,
                                        s->nitems, d_status, stream);
