@@ -60,38 +60,48 @@ constexpr uint32_t kMapW = kMap / 32;       // dwords per lane
 constexpr uint32_t kMinChunk = 256;         // shortest chunk worth a lane
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-// The frame's compressed bytes through a 16-byte register window: frame
-// offset x is resource byte x + s0; the window holds resource bytes
-// [base, base + 16), base 4-aligned (dword range checks: see load16u).
+// The frame's compressed bytes through a 64-byte per-lane window in LDS:
+// frame offset x is resource byte x + s0; the window holds resource bytes
+// [base, base + 64), base 16-aligned, refilled with four 16-byte loads issued
+// together (a sequence spans ~21 bytes on the synthetic, so a refill serves
+// about three; the 16-byte register window it replaces reloaded, and waited,
+// about twice per sequence).  Loads past the span read 0 (dword range checks).
 struct Src {
     __amdgpu_buffer_rsrc_t r;
     uint32_t s0;
 };
 
 struct Win {
-    u32x4 w;
+    uint32_t lds;    // this lane's window (64 bytes of LDS)
     uint32_t base;
 };
-
-__device__ __forceinline__ uint32_t rd4(const Src &S, Win &W, uint32_t x)
-{
-    const uint32_t rx = x + S.s0;
-    if (rx - W.base > 12u) {
-        W.base = rx & ~3u;
-        W.w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(S.r, W.base, 0, 0));
-    }
-    return vword(W.w, rx - W.base);
-}
-
-__device__ __forceinline__ uint32_t rd1(const Src &S, Win &W, uint32_t x)
-{
-    return rd4(S, W, x) & 0xFF;
-}
 
 template <typename T>
 __device__ __forceinline__ __attribute__((address_space(3))) T *lp(uint32_t a)
 {
     return (__attribute__((address_space(3))) T *)(uintptr_t)a;
+}
+
+__device__ __forceinline__ uint32_t rd4(const Src &S, Win &W, uint32_t x)
+{
+    const uint32_t rx = x + S.s0;
+    if (rx - W.base > 59u) {
+        W.base = rx & ~15u;
+        u32x4 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(S.r, W.base + 16 * i, 0, 0));
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            *lp<u32x4>(W.lds + 16 * i) = v[i];
+    }
+    const uint32_t o = rx - W.base, a = W.lds + (o & ~3u);
+    return __builtin_amdgcn_alignbyte(*lp<uint32_t>(a + 4), *lp<uint32_t>(a), o & 3);
+}
+
+__device__ __forceinline__ uint32_t rd1(const Src &S, Win &W, uint32_t x)
+{
+    return rd4(S, W, x) & 0xFF;
 }
 
 // One sequence of a chain, no validation (passes 1, 2 and the count).
@@ -372,6 +382,7 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
     uint32_t min_csize)
 {
     __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
+    __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t f = uni(blockIdx.x * kCW + w);
@@ -392,8 +403,8 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
         S.s0 = sp.s0;
     }
     Win W;
-    W.base = 0xFFFFFFF0u;
-    W.w = (u32x4){0, 0, 0, 0};
+    W.base = 0x80000000u;   // no resource byte is within 59 of it: the first read refills
+    W.lds = (uint32_t)(uintptr_t)(wins) + 64 * threadIdx.x;
     uint32_t op = 0, k = 0, fail_op = 0;
     int32_t st = ST_OK;
     do {
