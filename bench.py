@@ -186,6 +186,13 @@ def main():
             kname = max(("parse", "execute"), key=lambda k: stage_ms[k])
             kname = names[kname]
     value = dsum * world * args.steps / t_max / 1e9
+    workload = ("config5: zstd 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
+                "compressed image resident in HBM" if zstd else
+                "config2: LZ4 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
+                "compressed image resident in HBM" if args.frame == 64 << 10 else
+                f"config3 (frame-size sweep): LZ4 {args.frame >> 10}KiB frames, "
+                f"{args.size / 2**30:g} GiB synthetic per GPU, full-range decode, "
+                "compressed image resident in HBM")
     line = {
         "metric": METRIC_ZSTD if zstd else METRIC,
         "value": round(value, 2),
@@ -201,19 +208,13 @@ def main():
         "data": ("synthetic (SURVEY §8d generator, compressed with libzstd 1.4.9 level 3 / strategy 1 "
                  "as the reference writer does)" if zstd else
                  "synthetic (SURVEY §8d generator, compressed with liblz4 1.9.3 as the reference writer does)"),
-        "config": {"workload": ("config5: zstd 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
-                                "compressed image resident in HBM" if zstd else
-                                "config2: LZ4 64KiB frames, 4 GiB synthetic per GPU, full-range decode, "
-                                "compressed image resident in HBM" if args.frame == 64 << 10 else
-                                f"config3 (frame-size sweep): LZ4 {args.frame >> 10}KiB frames, "
-                                f"{args.size / 2**30:g} GiB synthetic per GPU, full-range decode, "
-                                "compressed image resident in HBM"),
+        "config": {"workload": workload,
                    "frame_bytes": args.frame, "frames_per_gpu": nfr,
                    "decoded_bytes_per_gpu": dsum, "compressed_bytes_per_gpu": comp_bytes,
                    "parallelism": f"frames sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic_from_profile(kname),
+                     "traffic": traffic_from_profile(kname, workload),
                      "kernel": kname, "launch": "zsk_lz4_decode_frames (stages below, back to back)",
                      "avg_launch_ms": round(avg_kernel_s * 1e3, 4),
                      "stages": stages,
@@ -264,17 +265,18 @@ def end_to_end(z, img, size):
     return {"GBps": round(n / dt / 1e9, 2), "bytes": int(n), "api": "zseek_pread (host buffer)"}
 
 
-def traffic_from_profile(kernel):
+def traffic_from_profile(kernel, workload):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by scripts/round_profiles.py), used
-    only when it was recorded for the kernel this build launches."""
+    only when it was recorded for the kernel this build launches on this
+    same workload (a config-3 sweep line gets none)."""
     for name in ("pmc_traffic.json", "pmc_traffic_zstd.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 rec = json.load(f)
         except (OSError, ValueError):
             continue
-        if kernel in rec.get("kernel", ""):
+        if kernel in rec.get("kernel", "") and rec.get("workload") == workload:
             return rec.get("hbm_bytes_per_launch")
     return None
 

@@ -41,7 +41,7 @@ LAUNCH = ("lz4_plan_direct_kernel", "lz4_plan_kernel", "lz4_lean_kernel", "lz4_c
 ZSTD = "zstd" in bench["metric"]
 if ZSTD:   # zsk_zstd_decode_frames: plan + scan + frame + literal + sequence + execute + check
     LAUNCH = ("zstd_plan_kernel", "zstd_scan_kernel", "zstd_frame_kernel", "zstd_huf_kernel",
-              "zstd_seq_kernel", "seq_exec_kernel", "zstd_check_kernel")
+              "zstd_seq_kernel", "zstd_lit_fix_kernel", "seq_exec_kernel", "zstd_check_kernel")
 OUT = "pmc_traffic_zstd.json" if ZSTD else "pmc_traffic.json"
 
 
@@ -78,6 +78,7 @@ alg = bench["roofline"]["algorithmic_bytes_per_launch"]
 out = {
     "round": tag,
     "kernel": KERNEL,
+    "workload": bench["config"]["workload"],
     "launch_kernels": {k: {**kern.get(k, {}), "fetch_bytes_raw": per.get(k, {}).get("FETCH_SIZE"),
                            "write_bytes": per.get(k, {}).get("WRITE_SIZE")} for k in sorted(set(kern) | set(per))},
     "launch_avg_ns_rocprof": sum(v["avg_ns"] for v in kern.values()),
