@@ -616,7 +616,10 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // and cleared with ds_or / ds_and (4.63 vs 4.13 ms; six waves per SIMD (80 VGPRs: 10
 // spilled, 5.33 vs 4.04 ms); round 0's slot loads retired inside each deal
 // step, so the deal's first step issues without waiting on the item prefetch
-// and the last flush (4.001 vs 4.006 ms, no gain)
+// and the last flush (4.001 vs 4.006 ms, no gain); O(1) readiness tests
+// (prefix max of the pending destinations below, the lowest one) before the
+// binary search (4.068 vs 3.996 ms: two more scans per round, the search
+// still needed in most)
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
