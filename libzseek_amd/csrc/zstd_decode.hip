@@ -1257,7 +1257,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const uint8_t *comp,
 
 // The stream at offset x (len >= 1 bytes) of resource r, ring at LDS address
 // ring.  False when its last byte (the end mark) is 0.
-__device__ __forceinline__ bool br_init(BRd &b, __amdgpu_buffer_rsrc_t r, uint32_t x, uint32_t len, uint32_t ring)
+__device__ __forceinline__ bool br_init(BRd &b, __amdgpu_buffer_rsrc_t r, uint32_t x, uint32_t len, uint32_t ring,
+                                        bool d2 = false)
 {
     b.r = r;
     b.ring = ring;
@@ -1283,14 +1284,38 @@ __device__ __forceinline__ bool br_init(BRd &b, __amdgpu_buffer_rsrc_t r, uint32
     b.pos = 32 * D;
     b.C = top & ((1u << (xm & 31)) - 1) & above(b.xs, b.pos);
     b.nb = xm & 31;
+    if (d2) {   // a second chunk in flight (br_step<1, 2>), room permitting
+        const int32_t qcur = (b.pos - 32) >> 7;
+        const bool room = b.pq >= qcur - (kRS - 1);
+        const int32_t t = room ? b.pq : b.pq + 1;
+        b.P2 = chunk16(b, t);
+        b.pend2 = t;
+        b.pq = room ? b.pq - 1 : b.pq;
+    }
     return last != 0;
 }
 
 // Once per decode step: commit the pending chunk(s), fetch the next one(s)
-// (F = 1 or 2 chunks per step).
-template <int F = 1>
+// (F = 1 or 2 chunks per step).  D = 2 (with F = 1): two chunks in flight,
+// each committed two steps after its load, so the load's wait never waits
+// on the literal store of the step just before it (vmcnt retires in issue
+// order): a store has two steps to land instead of one.  A room check at
+// issue suffices: the slot it fills held a chunk above the one then in use.
+template <int F = 1, int D = 1>
 __device__ __forceinline__ void br_step(BRd &b)
 {
+    if (D == 2) {
+        slot_put(b, b.pend, b.P);
+        b.P = b.P2;
+        b.pend = b.pend2;
+        const int32_t qcur = (b.pos - 32) >> 7;
+        const bool room = b.pq >= qcur - (kRS - 1);
+        const int32_t t = room ? b.pq : b.pq + 1;
+        b.P2 = chunk16(b, t);
+        b.pend2 = t;
+        b.pq = room ? b.pq - 1 : b.pq;
+        return;
+    }
     slot_put(b, b.pend, b.P);
     if (F == 2)
         slot_put(b, b.pend2, b.P2);
@@ -1363,7 +1388,7 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     const uint32_t i0 = i;
     while (i + 16 <= lim) {
         if (!(DIAG & 2))
-            br_step<F>(b);
+            br_step<F, F == 1 ? 2 : 1>(b);
         // unconditional (the first step's goes to a sink): a conditional
         // store would make the compiler's chunk waits vmcnt(0), i.e. wait on it
         if (!(DIAG & 1))
@@ -1393,7 +1418,7 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     if (i != i0)
         *reinterpret_cast<u32x4 *>(out + i - 16) = prev;
     while (i < cnt) {
-        br_step<F>(b);
+        br_step<F, F == 1 ? 2 : 1>(b);
         br_fill(b);
         const uint32_t s = one();
         if (i < lim)
@@ -1453,7 +1478,8 @@ __global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict_
     bool bad = false;
     auto run = [&](__amdgpu_buffer_rsrc_t r, uint64_t base) {
         BRd b;
-        bad = !br_init(b, r, (uint32_t)(J.src - base), J.len, (uint32_t)(uintptr_t)lp<uint8_t>(rings) + 4 * lane);
+        bad = !br_init(b, r, (uint32_t)(J.src - base), J.len, (uint32_t)(uintptr_t)lp<uint8_t>(rings) + 4 * lane,
+                       in_lds && lgmax <= 8);   // huf_stream<4, 1>: two chunks in flight
         uint8_t *out = lit + J.dst;
         if (in_lds) {
             const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(&tabs[first]);
