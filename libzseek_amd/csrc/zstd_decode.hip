@@ -1360,7 +1360,6 @@ __device__ __forceinline__ int32_t br_left(const BRd &b)
 // shift takes the cell's low 5 bits, nbits).  16 decoded bytes are stored at
 // a time, aligned.
 constexpr uint32_t kHufLdsCells = 2048;
-__device__ u32x4 g_huf_sink[64];   // the first step's store of every stream (never read)
 
 template <int G, int F, int DIAG, typename Tab>
 __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *out, uint64_t dst, uint32_t cnt,
@@ -1381,18 +1380,10 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
             out[i] = (uint8_t)s;
         i++;
     }
-    // 16 symbols per step; each step's 16 bytes are stored after the next
-    // step's loads are issued, so the wait that commits a chunk never waits
-    // on a store issued just before it
-    u32x4 prev = {0, 0, 0, 0};
-    const uint32_t i0 = i;
-    while (i + 16 <= lim) {
+    // 16 symbols per step
+    auto step16 = [&]() -> u32x4 {
         if (!(DIAG & 2))
             br_step<F, F == 1 ? 2 : 1>(b);
-        // unconditional (the first step's goes to a sink): a conditional
-        // store would make the compiler's chunk waits vmcnt(0), i.e. wait on it
-        if (!(DIAG & 1))
-            *(i != i0 ? reinterpret_cast<u32x4 *>(out + i - 16) : &g_huf_sink[threadIdx.x & 63]) = prev;
         u32x4 acc = {0, 0, 0, 0};
         uint32_t w = 0, used = 0;
 #pragma unroll
@@ -1412,11 +1403,38 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
                 acc[k >> 2] |= (e >> 8) << (8 * (k & 3));
         }
         b.nb -= (int32_t)used;
-        prev = acc;
+        return acc;
+    };
+    auto put16 = [&](uint32_t at, const u32x4 &v) {
+        if (!(DIAG & 1))
+            *reinterpret_cast<u32x4 *>(out + at) = v;
+    };
+    // to a 128-byte boundary of the output, a step at a time
+    while (i + 16 <= lim && ((dst + i) & 63)) {
+        const u32x4 v = step16();
+        put16(i, v);
         i += 16;
     }
-    if (i != i0)
-        *reinterpret_cast<u32x4 *>(out + i - 16) = prev;
+    // then 4 steps per iteration and their 64 bytes stored back to back: a
+    // line arrives in two halves, where 16-byte stores a step apart left
+    // partial lines in L2 to be evicted (and merged in HBM) under this
+    // kernel's write load (5.2 -> 3.9 ms; no stores at all: 1.9 ms; 8 steps
+    // need more than the 128 VGPRs four waves per SIMD leave: spills)
+    while (i + 64 <= lim) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            v[k] = step16();
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            put16(i + 16 * k, v[k]);
+        i += 64;
+    }
+    while (i + 16 <= lim) {
+        const u32x4 v = step16();
+        put16(i, v);
+        i += 16;
+    }
     while (i < cnt) {
         br_step<F, F == 1 ? 2 : 1>(b);
         br_fill(b);
@@ -1430,7 +1448,7 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
 __device__ unsigned int g_hdiag[32];   // diagnostic builds: waves per lgmax, LDS / global path
 
 template <int DIAG>
-__global__ __launch_bounds__(64) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
                                                       const uint8_t *__restrict__ comp,
                                                       const uint8_t *__restrict__ slots,
                                                       uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
