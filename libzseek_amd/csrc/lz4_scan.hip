@@ -6,7 +6,7 @@
 // 1.9.3 validation order (parse_block / parse_frame there, decode_block in
 // oracle/lz4_oracle.c), but never waits on a dependent global load:
 //
-//   * each lane's compressed bytes stream into a 512-byte LDS ring through a
+//   * each lane's compressed bytes stream into a 128-byte LDS ring through a
 //     D-deep software pipeline (32 bytes per sub-step; a slot's registers are
 //     written to the ring D sub-steps after its load was issued);
 //   * a sub-step parses one whole sequence from the ring (token + one
@@ -37,9 +37,13 @@ using namespace lz4d;
 constexpr uint32_t kItemExt = 0x80000000u;
 constexpr uint32_t kItemPos = 0x3FFFFFFFu;
 constexpr uint32_t kSW = 4;              // waves per workgroup
-constexpr uint32_t kRing = 512;          // per-lane ring bytes
-constexpr uint32_t kStride = 528;        // bytes between lanes' rings (bank spread)
-constexpr uint32_t kD = 8;               // pipeline depth (slots)
+// per-lane ring bytes: 128 (4 waves per SIMD by LDS) parses the 4 KiB
+// frames' config in 1.93 ms, 256 (2 waves) in 2.10, 512 (1 wave) in 2.27 —
+// the many short chains want waves to hide their LDS round trips more than
+// lookahead (a literal run past it only parks the offset for a sub-step)
+constexpr uint32_t kRing = 128;
+constexpr uint32_t kStride = 144;        // bytes between lanes' rings (bank spread)
+constexpr uint32_t kD = 3;               // pipeline depth (slots)
 constexpr uint32_t kOff = 0x80000000u;   // out-of-range buffer offset: op disabled
 
 enum : uint32_t { P_TOKEN = 0, P_OFF, P_BHDR, P_END, P_DONE };
@@ -593,7 +597,7 @@ __device__ __forceinline__ bool sub(Scan &L, Fill &S)
 }
 
 template <bool BR>
-__global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(1, 1))) void lz4_scan_kernel(
+__global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(4, 4))) void lz4_scan_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
