@@ -619,7 +619,11 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // and the last flush (4.001 vs 4.006 ms, no gain); O(1) readiness tests
 // (prefix max of the pending destinations below, the lowest one) before the
 // binary search (4.068 vs 3.996 ms: two more scans per round, the search
-// still needed in most)
+// still needed in most); a persistent grid (1,280 workgroups, frames f,
+// f + stride, ...) prefetching the next frame's item count, base and first
+// items (4.258 vs 4.028 ms; 4 KiB frames 6.255 vs 5.703: the hardware's
+// dynamic dispatch balances frames better than a static stride, and the
+// prefetch registers spill at five waves per SIMD)
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
