@@ -1702,17 +1702,24 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     // one resource over the wave's frames (else lane by lane, each its own)
     const uint64_t lo = uni64(wave_min64(act ? d.c_off : ~0ull)) & ~15ull;
     const uint64_t hi = uni64(wave_max64(act ? d.c_off + d.c_size : 0ull));
+    // the wave's item slots as one resource (else lane by lane, as comp);
+    // reduced over the active lanes with every lane still present (an idle
+    // lane's registers are not a value)
+    uint64_t rb = 0;
+    uint32_t icap = 0;
+    if (act) {
+        rb = rec_base[f];
+        icap = (uint32_t)(rec_base[f + 1] - rb);
+    }
+    const uint64_t ilo = uni64(wave_min64(act ? rb : ~0ull)), ihi = uni64(wave_max64(act ? rb + icap : 0ull));
     if (!act)
         return;
     const uint64_t ob = op_base(blk_base, f);
     const uint32_t opn = (uint32_t)(op_base(blk_base, f + 1) - ob);
     ZOp *op = reinterpret_cast<ZOp *>(ops) + ob;
     LSink S;
-    const uint64_t rb = rec_base[f];
     S.k = 0;
-    S.cap = (uint32_t)(rec_base[f + 1] - rb);
-    // the wave's item slots as one resource (else lane by lane, as comp)
-    const uint64_t ilo = uni64(wave_min64(rb)), ihi = uni64(wave_max64(rb + S.cap));
+    S.cap = icap;
     uint16_t *const mytab = &ftab[lane * kSeqCells];
     const uint32_t cap = d.d_size;
     uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
