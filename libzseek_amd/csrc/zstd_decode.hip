@@ -2110,6 +2110,12 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
 
 void zstd_scratch_free(ZstdScratch *s)
 {
+    // the side stream drained before anything goes (the caller drained the
+    // main stream only; destroying a stream, or its events, with the
+    // runtime's bookkeeping of its last record still pending corrupted the
+    // host heap)
+    if (s->side)
+        (void)hipStreamSynchronize(s->side);
     for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
                     (void *)s->nitems, (void *)s->ck, (void *)s->stop, (void *)s->lit, (void *)s->items,
                     (void *)s->ops, (void *)s->hjobs, (void *)s->slots, (void *)s->hbad, (void *)s->d_total})
@@ -2117,12 +2123,12 @@ void zstd_scratch_free(ZstdScratch *s)
             (void)hipFree(p);
     if (s->total)
         (void)hipHostFree(s->total);
+    if (s->side)
+        (void)hipStreamDestroy(s->side);
     if (s->ev_tab)
         (void)hipEventDestroy(s->ev_tab);
     if (s->ev_huf)
         (void)hipEventDestroy(s->ev_huf);
-    if (s->side)
-        (void)hipStreamDestroy(s->side);
     *s = ZstdScratch();
 }
 
@@ -2170,7 +2176,8 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             return -1;
         static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
         const dim3 g((nj + 63) / 64), b(64);
-        hipStream_t const hs = s->side;
+        static const bool serial = getenv("ZSEEK_ZSTD_SERIAL") != nullptr;   // diagnostics: one stream
+        hipStream_t const hs = serial ? stream : s->side;
         if (diag) {
             unsigned int z[32] = {};
             (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);

@@ -270,3 +270,23 @@ def test_zstd_partial_reads_golden(gpu, zs, golden, case):
             else:
                 assert ret == q["ret"], q
                 assert sha(out[: q["ret"]]) == q["sha256"], q
+
+
+def test_device_zstd_partial_waves(gpu, zs, oracle, zstd):
+    """Batches that leave lanes of the kernels' last wave idle (1, 2, 31, 33
+    and 65 frames), each decoded right after a 64-frame batch, so idle lanes
+    hold another launch's registers: every frame bit-exact (the sequence
+    kernel once reduced its item span over idle lanes)."""
+    data = datasets(oracle)["synth"]
+    frames, sizes = [], []
+    for k in range(96):
+        src = data[(k * 4096) % 300_000:][:4096]
+        frames.append(compress(zstd, src, {P_LEVEL: 3}))
+        sizes.append(len(src))
+    full, st = device_decode(zs, gpu, frames, sizes)
+    assert (st == 0).all()
+    for n in (1, 2, 31, 33, 65):
+        device_decode(zs, gpu, frames[:64], sizes[:64])
+        out, st = device_decode(zs, gpu, frames[:n], sizes[:n])
+        assert (st == 0).all(), n
+        assert out == full[:n], n
