@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(1024) void zstd_scan_kernel(const FrameDesc *__rest
 // (raw / RLE literals straight into the scratch), Huffman and FSE tables
 // (built in LDS, stored to the block's slot), Huffman stream jobs and the op
 // list the sequence kernel replays.
-__global__ __launch_bounds__(64 * kZW) void zstd_frame_kernel(
+__global__ __launch_bounds__(64 * kZW) __attribute__((amdgpu_waves_per_eu(4))) void zstd_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ lit, uint64_t lit_cap, const uint64_t *__restrict__ rec_base,
     uint64_t capacity, const uint64_t *__restrict__ blk_base, uint8_t *__restrict__ ops,
