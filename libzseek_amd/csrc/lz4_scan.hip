@@ -40,7 +40,8 @@ constexpr uint32_t kSW = 4;              // waves per workgroup
 // per-lane ring bytes: 128 (4 waves per SIMD by LDS) parses the 4 KiB
 // frames' config in 1.93 ms, 256 (2 waves) in 2.10, 512 (1 wave) in 2.27 —
 // the many short chains want waves to hide their LDS round trips more than
-// lookahead (a literal run past it only parks the offset for a sub-step)
+// lookahead (a literal run past it only parks the offset for a sub-step);
+// 64 bytes is too short for the frame header's synchronous first read
 constexpr uint32_t kRing = 128;
 constexpr uint32_t kStride = 144;        // bytes between lanes' rings (bank spread)
 constexpr uint32_t kD = 3;               // pipeline depth (slots)
