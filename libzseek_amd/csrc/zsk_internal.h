@@ -157,6 +157,7 @@ struct ZstdScratch {
     uint64_t *total = nullptr;     // pinned host copy of d_total
     hipStream_t side = nullptr;    // the Huffman kernel's stream (beside the sequence replay)
     hipEvent_t ev_tab = nullptr, ev_huf = nullptr;
+    int side_dev = -1;   // the device the side set belongs to (pooled, zstd_decode.hip)
     uint32_t frames_cap = 0;
     uint64_t lit_cap = 0, items_cap = 0, blocks_cap = 0, ops_cap = 0;
 };

@@ -30,6 +30,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
+#include <vector>
+
 #include "lz4_dev.h"
 #include "zsk_internal.h"
 
@@ -1013,12 +1016,20 @@ __device__ __forceinline__ uint32_t decode_entry(ZLds &L, Frame &F, uint32_t cle
 __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restrict__ desc, uint32_t n,
                                                         const uint8_t *__restrict__ comp,
                                                         uint32_t *__restrict__ bound,
-                                                        uint32_t *__restrict__ bblk)
+                                                        uint32_t *__restrict__ bblk,
+                                                        unsigned long long *__restrict__ extent)
 {
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    FrameDesc d = {0, 0, 0, 0};
+    if (f < n)
+        d = desc[f];
+    // the output extent max(d_off + d_size), a wave at a time (the scan then
+    // reads no descriptors)
+    const uint64_t wx = wave_max64(f < n ? d.d_off + d.d_size : 0ull);
+    if ((threadIdx.x & 63) == 0 && wx)
+        atomicMax(extent, (unsigned long long)wx);
     if (f >= n)
         return;
-    const FrameDesc d = desc[f];
     const Span sp = make_span(comp + d.c_off, d.c_size);
     auto B = [&](uint32_t p) -> uint32_t {
         return p < d.c_size ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(sp.r, sp.s0 + p, 0, 0) : 0u;
@@ -1083,57 +1094,87 @@ __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restr
 // rec_base[0..n], blk_base[0..n]; item total, output extent max(d_off +
 // d_size) and block total into total[0..2] (device memory, copied to the host
 // by the launcher; one workgroup)
-__global__ __launch_bounds__(1024) void zstd_scan_kernel(const FrameDesc *__restrict__ desc,
-                                                         const uint32_t *__restrict__ bound,
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(1024) void zstd_scan_kernel(const uint32_t *__restrict__ bound,
                                                          const uint32_t *__restrict__ bblk, uint32_t n,
                                                          uint64_t *__restrict__ rec_base,
                                                          uint64_t *__restrict__ blk_base,
                                                          uint64_t *__restrict__ total)
 {
-    __shared__ uint64_t part[1024];
-    __shared__ uint64_t partb[1024];
-    __shared__ uint64_t ext[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t chunk = (n + 1023) / 1024;
-    const uint32_t i0 = t * chunk < n ? t * chunk : n;
-    const uint32_t i1 = i0 + chunk < n ? i0 + chunk : n;
-    uint64_t s = 0, sb = 0, e = 0;
-    for (uint32_t i = i0; i < i1; i++) {
-        s += bound[i];
-        sb += bblk[i];
-        const uint64_t x = desc[i].d_off + desc[i].d_size;
-        e = x > e ? x : e;
-    }
-    part[t] = s;
-    partb[t] = sb;
-    ext[t] = e;
-    __syncthreads();
-    for (uint32_t d = 512; d >= 1; d >>= 1) {
-        if (t < d && ext[t + d] > ext[t])
-            ext[t] = ext[t + d];
+    // tiles of 4096 frames, four per thread, loaded 16 bytes at a time
+    // (coalesced) and scanned a wave at a time; a thread per frame chunk with
+    // a dependent load per element cost ~0.3 ms at 65,536 frames
+    __shared__ uint64_t wsum[16], wsumb[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint64_t carry = 0, carryb = 0;
+    auto load4 = [&](const uint32_t *a, uint32_t x) -> u32x4 {
+        if (x + 4 <= n)
+            return *reinterpret_cast<const u32x4 *>(a + x);
+        u32x4 v = {0, 0, 0, 0};
+        for (uint32_t q = 0; q < 4; q++)
+            if (x + q < n)
+                v[q] = a[x + q];
+        return v;
+    };
+    const uint32_t x0 = 4 * t;
+    u32x4 a = load4(bound, x0), c = load4(bblk, x0);
+    for (uint32_t b = 0; b < n; b += 4096) {
+        const uint32_t x = b + x0;
+        const u32x4 ca = a, cc = c;
+        if (b + 4096 < n) {   // the next tile's loads in flight during this one's scan
+            a = load4(bound, x + 4096);
+            c = load4(bblk, x + 4096);
+        }
+        const uint64_t s = (uint64_t)ca.x + ca.y + ca.z + ca.w;
+        const uint64_t sb = (uint64_t)cc.x + cc.y + cc.z + cc.w;
+        uint64_t is = s, isb = sb;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t v = __shfl_up(is, d, 64), vb = __shfl_up(isb, d, 64);
+            if (lane >= d) {
+                is += v;
+                isb += vb;
+            }
+        }
+        if (lane == 63) {
+            wsum[w] = is;
+            wsumb[w] = isb;
+        }
         __syncthreads();
+        uint64_t pre = carry, preb = carryb, tot = carry, totb = carryb;
+        for (uint32_t k = 0; k < 16; k++) {
+            pre += k < w ? wsum[k] : 0;
+            preb += k < w ? wsumb[k] : 0;
+            tot += wsum[k];
+            totb += wsumb[k];
+        }
+        __syncthreads();   // wsum free for the next tile
+        uint64_t r = pre + is - s, rb = preb + isb - sb;
+        if (x < n) {
+            const uint64_t r1 = r + ca.x, r2 = r1 + ca.y, r3 = r2 + ca.z;
+            const uint64_t q1 = rb + cc.x, q2 = q1 + cc.y, q3 = q2 + cc.z;
+            if (x + 4 <= n) {
+                *reinterpret_cast<u64x2 *>(rec_base + x) = (u64x2){r, r1};
+                *reinterpret_cast<u64x2 *>(rec_base + x + 2) = (u64x2){r2, r3};
+                *reinterpret_cast<u64x2 *>(blk_base + x) = (u64x2){rb, q1};
+                *reinterpret_cast<u64x2 *>(blk_base + x + 2) = (u64x2){q2, q3};
+            } else {
+                const uint64_t rr[4] = {r, r1, r2, r3}, qq[4] = {rb, q1, q2, q3};
+                for (uint32_t q = 0; x + q < n; q++) {
+                    rec_base[x + q] = rr[q];
+                    blk_base[x + q] = qq[q];
+                }
+            }
+        }
+        carry = tot;
+        carryb = totb;
     }
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint64_t v = t >= d ? part[t - d] : 0;
-        const uint64_t vb = t >= d ? partb[t - d] : 0;
-        __syncthreads();
-        part[t] += v;
-        partb[t] += vb;
-        __syncthreads();
-    }
-    uint64_t run = part[t] - s, runb = partb[t] - sb;
-    for (uint32_t i = i0; i < i1; i++) {
-        rec_base[i] = run;
-        blk_base[i] = runb;
-        run += bound[i];
-        runb += bblk[i];
-    }
-    if (t == 1023) {
-        rec_base[n] = part[t];
-        blk_base[n] = partb[t];
-        total[0] = part[t];
-        total[1] = ext[0];
-        total[2] = partb[t];
+    if (t == 0) {
+        rec_base[n] = carry;
+        blk_base[n] = carryb;
+        total[0] = carry;
+        total[2] = carryb;
     }
 }
 
@@ -2060,16 +2101,75 @@ int grow(T **p, uint64_t &cap, uint64_t want, uint64_t unit)
     cap = want;
     return 0;
 }
+
+// The Huffman side stream and its two events come from a process-wide pool
+// and are never destroyed: a reader's teardown with the runtime still holding
+// an event's last record (on the reader's own stream, destroyed right after)
+// corrupted the host heap now and then.  A released set is drained and its
+// events re-recorded on its own stream, so nothing in the pool refers to a
+// stream that may go away.
+struct SideSet {
+    int dev;
+    hipStream_t side;
+    hipEvent_t ev_tab, ev_huf;
+};
+std::mutex g_side_mu;
+std::vector<SideSet> g_side_pool;
+
+int side_acquire(ZstdScratch *s)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        return -1;
+    {
+        std::lock_guard<std::mutex> lk(g_side_mu);
+        for (size_t i = 0; i < g_side_pool.size(); i++)
+            if (g_side_pool[i].dev == dev) {
+                s->side_dev = dev;
+                s->side = g_side_pool[i].side;
+                s->ev_tab = g_side_pool[i].ev_tab;
+                s->ev_huf = g_side_pool[i].ev_huf;
+                g_side_pool.erase(g_side_pool.begin() + i);
+                return 0;
+            }
+    }
+    SideSet x = {dev, nullptr, nullptr, nullptr};
+    if (hipStreamCreateWithFlags(&x.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&x.ev_tab, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.ev_huf, hipEventDisableTiming) != hipSuccess) {
+        // partly created, nothing recorded on it yet
+        if (x.ev_tab)
+            (void)hipEventDestroy(x.ev_tab);
+        if (x.side)
+            (void)hipStreamDestroy(x.side);
+        return -1;
+    }
+    s->side_dev = dev;
+    s->side = x.side;
+    s->ev_tab = x.ev_tab;
+    s->ev_huf = x.ev_huf;
+    return 0;
+}
+
+void side_release(ZstdScratch *s)
+{
+    if (!s->side)
+        return;
+    (void)hipEventRecord(s->ev_tab, s->side);
+    (void)hipEventRecord(s->ev_huf, s->side);
+    (void)hipStreamSynchronize(s->side);
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    g_side_pool.push_back({s->side_dev, s->side, s->ev_tab, s->ev_huf});
+    s->side = nullptr;
+    s->ev_tab = s->ev_huf = nullptr;
+}
 }   // namespace
 
 int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, uint64_t items,
                          uint64_t blocks, hipStream_t stream)
 {
     (void)stream;
-    if (!s->side &&
-        (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
-         hipEventCreateWithFlags(&s->ev_tab, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&s->ev_huf, hipEventDisableTiming) != hipSuccess))
+    if (!s->side && side_acquire(s) != 0)
         return -1;
     if (frames + 1 > s->frames_cap) {
         const uint32_t cap = frames + 1 < 4096 ? 4096 : frames + 1;
@@ -2110,12 +2210,7 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
 
 void zstd_scratch_free(ZstdScratch *s)
 {
-    // the side stream drained before anything goes (the caller drained the
-    // main stream only; destroying a stream, or its events, with the
-    // runtime's bookkeeping of its last record still pending corrupted the
-    // host heap)
-    if (s->side)
-        (void)hipStreamSynchronize(s->side);
+    side_release(s);   // drains the side stream before anything goes
     for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
                     (void *)s->nitems, (void *)s->ck, (void *)s->stop, (void *)s->lit, (void *)s->items,
                     (void *)s->ops, (void *)s->hjobs, (void *)s->slots, (void *)s->hbad, (void *)s->d_total})
@@ -2123,12 +2218,6 @@ void zstd_scratch_free(ZstdScratch *s)
             (void)hipFree(p);
     if (s->total)
         (void)hipHostFree(s->total);
-    if (s->side)
-        (void)hipStreamDestroy(s->side);
-    if (s->ev_tab)
-        (void)hipEventDestroy(s->ev_tab);
-    if (s->ev_huf)
-        (void)hipEventDestroy(s->ev_huf);
     *s = ZstdScratch();
 }
 
@@ -2140,9 +2229,11 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 {
     if (nframes == 0)
         return 0;
+    if (hipMemsetAsync(s->d_total, 0, 4 * sizeof(uint64_t), stream) != hipSuccess)
+        return -1;
     hipLaunchKernelGGL(zstd_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
-                       nframes, d_comp, s->bound, s->bblk);
-    hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, s->bound, s->bblk, nframes,
+                       nframes, d_comp, s->bound, s->bblk, reinterpret_cast<unsigned long long *>(s->d_total + 1));
+    hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, s->bound, s->bblk, nframes,
                        s->rec_base, s->blk_base, s->d_total);
     if (hipGetLastError() != hipSuccess)
         return -1;
