@@ -290,3 +290,40 @@ def test_device_zstd_partial_waves(gpu, zs, oracle, zstd):
         out, st = device_decode(zs, gpu, frames[:n], sizes[:n])
         assert (st == 0).all(), n
         assert out == full[:n], n
+
+
+def test_zstd_readers_concurrent(gpu, zs):
+    """Readers opened, read and closed from several threads at once, and one
+    reader shared by them (the reader serialises its own preads): every read
+    bit-exact.  Exercises the pooled Huffman side stream (zstd_decode.hip
+    side_acquire / side_release) under interleaved open/close."""
+    import threading
+    data = zs.synth_buffer(48 * 65536 + 1234)
+    img = bytes(zs.zstd_seekable(data, 65536).tobytes())
+    shared = zs.Reader(img, 0)
+    errors = []
+
+    def work(seed):
+        rng = np.random.default_rng(seed)
+        try:
+            for rnd in range(3):
+                r = zs.Reader(img, int(rng.integers(0, 3)))
+                for _ in range(6):
+                    off = int(rng.integers(0, len(data)))
+                    cnt = int(rng.integers(1, 5 * 65536))
+                    src = r if rng.integers(0, 2) else shared
+                    got = src.pread(cnt, off)
+                    if got != data[off: off + cnt].tobytes():
+                        errors.append((seed, rnd, off, cnt))
+                r.close()
+        except Exception as e:   # reported below, not lost in the thread
+            errors.append((seed, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(s,)) for s in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    shared.close()
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:4]
