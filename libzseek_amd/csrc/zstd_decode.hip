@@ -1718,10 +1718,15 @@ __device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 // frame's three FSE tables are copied into 1600 bytes of LDS when they fit
 // (else read from the slot), so the per-sequence lookups stay on chip; with
 // three such workgroups per CU the LDS, not the lanes, sets how many frames
-// are in flight.
+// are in flight.  Same-box A/B at config 5 (sequence kernel alone in the
+// profile, beside the Huffman kernel): 5.6 ms as here; tables read from the
+// slot only, 64 or 32 frames per wave, 9.3 ms; 408 or 544 cells per frame
+// (more workgroups per CU, more blocks' tables read from the slot) 8.2 and
+// 6.6 ms.
 constexpr uint32_t kSeqLanes = 32;
 constexpr uint32_t kSeqCells = 800;   // u16 cells per frame (768 + copy slack)
 
+template <uint32_t LANES, uint32_t CELLS>
 __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
@@ -1730,13 +1735,13 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at)
 {
     __shared__ uint32_t codes[89];
-    __shared__ __attribute__((aligned(16))) uint16_t ftab[kSeqLanes * kSeqCells];
+    __shared__ __attribute__((aligned(16))) uint16_t ftab[CELLS ? LANES * CELLS : 8];
     for (uint32_t i = threadIdx.x; i < 89; i += 64)
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
     __syncthreads();
     const uint32_t lane = threadIdx.x;
-    const uint32_t f = blockIdx.x * kSeqLanes + lane;
-    const bool act = lane < kSeqLanes && f < n;
+    const uint32_t f = blockIdx.x * LANES + lane;
+    const bool act = lane < LANES && f < n;
     FrameDesc d = {0, 0, 0, 0};
     if (act)
         d = desc[f];
@@ -1761,7 +1766,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     LSink S;
     S.k = 0;
     S.cap = icap;
-    uint16_t *const mytab = &ftab[lane * kSeqCells];
+    uint16_t *const mytab = &ftab[CELLS ? lane * CELLS : 0];
     const uint32_t cap = d.d_size;
     uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
     uint64_t c = 0;
@@ -1802,7 +1807,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
                         const uint32_t nll = 1u << tll, nof = 1u << tof, nml = 1u << tml;
                         const uint16_t *TL = gt + kFseOff[0], *TO = gt + kFseOff[1], *TM = gt + kFseOff[2];
-                        const bool fit = nll + nof + nml <= 768;
+                        const bool fit = CELLS && nll + nof + nml + 32 <= CELLS;
                         if (fit) {
                             auto cp = [&](const uint16_t *src, uint32_t at, uint32_t cells) {
                                 for (uint32_t c = 0; c < cells; c += 8)
@@ -2134,7 +2139,12 @@ int side_acquire(ZstdScratch *s)
             }
     }
     SideSet x = {dev, nullptr, nullptr, nullptr};
-    if (hipStreamCreateWithFlags(&x.side, hipStreamNonBlocking) != hipSuccess ||
+    // the side stream at the lowest priority: the sequence kernel, the longer
+    // of the two, gets the CUs' LDS first (10.9 -> 10.6 ms per launch at
+    // config 5; launching the sequence kernel first made no difference)
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&x.side, hipStreamNonBlocking, lo) != hipSuccess ||
         hipEventCreateWithFlags(&x.ev_tab, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&x.ev_huf, hipEventDisableTiming) != hipSuccess) {
         // partly created, nothing recorded on it yet
@@ -2262,6 +2272,11 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                        s->slots, s->hjobs);
     // the Huffman streams decode on a side stream beside the sequence replay
     // (neither reads the other's output); zstd_lit_fix_kernel joins them
+    auto seq = [&] {
+        hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells>), dim3((nframes + kSeqLanes - 1) / kSeqLanes),
+                           dim3(64), 0, stream, d_desc, nframes, d_comp, s->ops, s->blk_base, s->slots, s->stop,
+                           s->rec_base, s->items, s->nitems, d_status, s->ck, d_fail_at);
+    };
     if (nj) {
         if (hipEventRecord(s->ev_tab, stream) != hipSuccess || hipStreamWaitEvent(s->side, s->ev_tab, 0) != hipSuccess)
             return -1;
@@ -2293,9 +2308,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         if (hipEventRecord(s->ev_huf, hs) != hipSuccess)
             return -1;
     }
-    hipLaunchKernelGGL(zstd_seq_kernel, dim3((nframes + kSeqLanes - 1) / kSeqLanes), dim3(64), 0, stream, d_desc, nframes,
-                       d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
-                       d_status, s->ck, d_fail_at);
+    seq();
     if (nj) {
         if (hipStreamWaitEvent(stream, s->ev_huf, 0) != hipSuccess)
             return -1;
