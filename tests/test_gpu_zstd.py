@@ -327,3 +327,13 @@ def test_zstd_readers_concurrent(gpu, zs):
     shared.close()
     assert not any(t.is_alive() for t in ts)
     assert not errors, errors[:4]
+
+
+@pytest.mark.parametrize("nframes", [4095, 4096, 4099, 8197])
+def test_zstd_many_small_frames(gpu, zs, nframes):
+    """Batches across the item-bound scan's 4,096-frame tiles (zstd_scan_kernel),
+    ragged at the end: a full-range read of 1 KiB frames, bit-exact."""
+    data = zs.synth_buffer(nframes * 1024 - 17)
+    img = bytes(zs.zstd_seekable(data, 1024).tobytes())
+    with zs.Reader(img, 0) as r:
+        assert r.read_all(data.size, 0) == data.tobytes()
