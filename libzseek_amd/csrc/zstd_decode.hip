@@ -1724,7 +1724,9 @@ __device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 // (more workgroups per CU, more blocks' tables read from the slot) 8.2 and
 // 6.6 ms; 1,056 or 1,312 cells (more blocks' tables in LDS, fewer frames per
 // CU) 11.4 and 12.8 ms per launch against 10.6; the LL / ML code tables
-// computed (packed constants and selects) instead of read from LDS, 11.05.
+// computed (packed constants and selects) instead of read from LDS, 11.05;
+// 24 or 20 frames per wave (four or five single-wave workgroups per CU, one
+// per SIMD) the same as 32.
 constexpr uint32_t kSeqLanes = 32;
 constexpr uint32_t kSeqCells = 800;   // u16 cells per frame (768 + copy slack)
 
