@@ -625,7 +625,8 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // dynamic dispatch balances frames better than a static stride, and the
 // prefetch registers spill at five waves per SIMD); nontemporal item and / or
 // literal loads, to leave L2 to the match sources (4.020 / 4.039 / 4.016 vs
-// 4.009 ms)
+// 4.009 ms); 1, 2, 5 or 8 waves per workgroup instead of kXW = 4 (4.27, 4.19,
+// 5.88, 4.46 vs 4.04 ms)
 template <int MODE, int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
