@@ -81,12 +81,35 @@ ZSEEK_EXPORT int zsk_zstd_decode_frames(const zsk_frame_desc_t *d_desc,
  * LZ4 frames, ZSTD_getErrorName strings for zstd frames). */
 ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
 
+/*
+ * zsk_lz4_decode_frames with one of the library's production decoders forced
+ * for every frame (testing, tooling): ZSK_DECODER_AUTO is the library's own
+ * choice (= zsk_lz4_decode_frames); WAVE the wave-per-frame decoder; LEAN,
+ * SCAN and CHUNK the two-phase decoder with that parse kernel for every frame.
+ * Returns -1 for an unknown decoder.
+ */
+#define ZSK_DECODER_AUTO 0
+#define ZSK_DECODER_WAVE 1
+#define ZSK_DECODER_LEAN 2
+#define ZSK_DECODER_SCAN 3
+#define ZSK_DECODER_CHUNK 4
+ZSEEK_EXPORT int zsk_lz4_decode_frames_ex(const zsk_frame_desc_t *d_desc,
+    uint32_t nframes, const void *d_comp, void *d_out, int32_t *d_status,
+    void *stream, int decoder);
+
 /* Name of the dominant HIP kernel zsk_lz4_decode_frames launches for a
  * batch of nframes frames (as it appears in a rocprofv3 kernel trace,
- * without namespace), for tooling.  Large batches use the two-phase decoder
- * (lz4_scan_kernel parse + seq_exec_kernel execute), small ones the
- * wave-per-frame decoder (env ZSEEK_HIP_KERNEL=lane|split|wave overrides). */
+ * without namespace), for tooling: batches of 64 frames and more use the
+ * two-phase decoder (its execute, seq_exec_kernel), smaller ones the
+ * wave-per-frame decoder (env ZSEEK_HIP_KERNEL=split|wave overrides). */
 ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes);
+
+/* Name of the parse kernel the two-phase decoder runs for a frame of
+ * @c_size compressed bytes in a batch of @nframes frames (lz4_lean_kernel,
+ * lz4_scan_kernel or lz4_chunk_kernel; lz4_wave_kernel for small batches):
+ * the library's routing, exposed so tools attribute time and traffic to the
+ * kernel that actually runs. */
+ZSEEK_EXPORT const char *zsk_lz4_parse_kernel_name(uint32_t nframes, uint32_t c_size);
 
 /* Measurement hook: while on, every two-phase decode launch records HIP
  * events between its stages (plan, parse, execute, hand-off) on its stream.

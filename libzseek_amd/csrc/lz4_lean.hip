@@ -752,31 +752,34 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     if (nframes == 0)
         return 0;
     const uint32_t per = 64 * kLW;
+    const dim3 grid((nframes + per - 1) / per), block(per);
+#define ZSK_LEAN(D, P)                                                                                  \
+    hipLaunchKernelGGL((lz4_lean_kernel<D, P>), grid, block, 0, stream, d_desc, nframes, d_comp, rec_base, \
+                       capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize)
+#ifdef ZSK_TUNING
     if (diag & 4) {
         unsigned long long z[6] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lean_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
-        hipLaunchKernelGGL((lz4_lean_kernel<4, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+        ZSK_LEAN(4, 2);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_lean_stats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
         const double fr = nframes;
         fprintf(stderr, "lean parse per frame: sub-steps fast %.1f exact-needed %.1f waiting %.1f done %.1f "
                         "exact-step runs %.1f items %.1f\n", z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr);
     } else if (diag & 2)
-        hipLaunchKernelGGL((lz4_lean_kernel<2, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+        ZSK_LEAN(2, 2);
     else if (diag & 1)
-        hipLaunchKernelGGL((lz4_lean_kernel<1, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+        ZSK_LEAN(1, 2);
     else if (diag & 8)
-        hipLaunchKernelGGL((lz4_lean_kernel<0, 4>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+        ZSK_LEAN(0, 4);
     else if (diag & 16)
-        hipLaunchKernelGGL((lz4_lean_kernel<0, 1>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+        ZSK_LEAN(0, 1);
     else
-        hipLaunchKernelGGL((lz4_lean_kernel<0, 2>), dim3((nframes + per - 1) / per), dim3(per), 0, stream, d_desc,
-                           nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize);
+#else
+    (void)diag;
+#endif
+        ZSK_LEAN(0, 2);
+#undef ZSK_LEAN
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -703,19 +703,14 @@ __global__ __launch_bounds__(64 * kSW) __attribute__((amdgpu_waves_per_eu(4, 4))
 int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items,
                     uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
-                    int version, uint32_t max_csize)
+                    uint32_t max_csize)
 {
     if (nframes == 0)
         return 0;
     const uint32_t per = 64 * kSW;
-    if (version == 1)
-        hipLaunchKernelGGL(lz4_scan_kernel<true>, dim3((nframes + per - 1) / per), dim3(per), 0, stream,
-                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
-                           max_csize);
-    else
-        hipLaunchKernelGGL(lz4_scan_kernel<false>, dim3((nframes + per - 1) / per), dim3(per), 0, stream,
-                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
-                           max_csize);
+    hipLaunchKernelGGL(lz4_scan_kernel<false>, dim3((nframes + per - 1) / per), dim3(per), 0, stream,
+                       d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
+                       max_csize);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -506,16 +506,6 @@ __global__ __launch_bounds__(64 * WAVES) void lz4_wave_kernel(const FrameDesc *_
     }
 }
 
-template <int RING, int WAVES>
-int launch_wave(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
-{
-    dim3 grid((nframes + WAVES - 1) / WAVES);
-    hipLaunchKernelGGL((lz4_wave_kernel<RING, WAVES>), grid, dim3(64 * WAVES), 0, stream,
-                       d_desc, nframes, d_comp, d_out, d_status, d_fail_at);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 }   // namespace
 
 int launch_lz4_wave_deferred(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
@@ -530,18 +520,14 @@ int launch_lz4_wave_deferred(const FrameDesc *d_desc, uint32_t nframes, const ui
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_lz4_wave(int variant, const FrameDesc *d_desc, uint32_t nframes,
-                    const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
-                    uint32_t *d_fail_at, hipStream_t stream)
+int launch_lz4_wave(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                    uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream)
 {
     if (nframes == 0)
         return 0;
-    switch (variant) {
-    case 0: return launch_wave<4096, 4>(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
-    case 1: return launch_wave<4096, 1>(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
-    case 2: return launch_wave<8192, 2>(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
-    default: return -1;
-    }
+    hipLaunchKernelGGL((lz4_wave_kernel<4096, 4>), dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc,
+                       nframes, d_comp, d_out, d_status, d_fail_at);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }   // namespace zsk

@@ -52,6 +52,7 @@ struct zseek_reader {
     std::mutex lock;   // serialises decode + cache (ref uses a rwlock, :38)
     SeekTable st;
     FrameCache *cache = nullptr;   // NULL when cache_size == 0 (ref :219-227)
+    std::mutex cursor_lock;        // zseek_read: cursor read, pread, advance as one step
     size_t pos = 0;                // zseek_read cursor (ref :826-835)
     size_t batch_bytes = kDefaultBatch;
     bool verify = false;   // check seek-table frame checksums (the reference never does)
@@ -228,13 +229,8 @@ bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *er
             e = hipErrorLaunchFailure;
     }
     const int engine = r->type == ZSEEK_ZSTD ? -1 : lz4_pick_engine((uint32_t)n);
-    if (e == hipSuccess && engine == ENGINE_LANE &&
-        launch_lz4_lane(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
-                        g.stream) != 0)
-        e = hipErrorLaunchFailure;
     if (e == hipSuccess && engine == ENGINE_WAVE &&
-        launch_lz4_wave(0, g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
-                        g.stream) != 0)
+        launch_lz4_wave(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail, g.stream) != 0)
         e = hipErrorLaunchFailure;
     if (e == hipSuccess && engine == ENGINE_SPLIT &&
         split_scratch_reserve(&g.split, (uint32_t)n, split_items_needed(g.h_desc, (uint32_t)n),
@@ -533,6 +529,11 @@ extern "C" ZSEEK_EXPORT ssize_t zseek_read(zseek_reader_t *reader, void *buf, si
         set_error(errbuf, "invalid reader");
         return 0;
     }
+    // the reference reads and advances pos outside its lock
+    // (decompress.c:831-832) although zseek.h:404 documents the call as safe
+    // to call concurrently; here concurrent zseek_read calls take disjoint
+    // consecutive ranges
+    std::lock_guard<std::mutex> guard(reader->cursor_lock);
     ssize_t ret = zseek_pread(reader, buf, count, reader->pos, call_data, errbuf);
     if (ret > 0)
         reader->pos += (size_t)ret;
@@ -574,8 +575,30 @@ extern "C" ZSEEK_EXPORT int zsk_lz4_decode_frames(const zsk_frame_desc_t *d_desc
                              d_status, nullptr, static_cast<hipStream_t>(stream));
 }
 
-// Kernel tuning hook (not part of the stable ABI): decode with an explicit
-// launch variant, see launch_lz4_frames_variant.
+extern "C" ZSEEK_EXPORT int zsk_lz4_decode_frames_ex(const zsk_frame_desc_t *d_desc, uint32_t nframes,
+                                                     const void *d_comp, void *d_out, int32_t *d_status,
+                                                     void *stream, int decoder)
+{
+    if (decoder < ZSK_DECODER_AUTO || decoder > ZSK_DECODER_CHUNK)
+        return -1;
+    return launch_lz4_frames(reinterpret_cast<const FrameDesc *>(d_desc), nframes,
+                             static_cast<const uint8_t *>(d_comp), static_cast<uint8_t *>(d_out),
+                             d_status, nullptr, static_cast<hipStream_t>(stream), decoder);
+}
+
+extern "C" ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes)
+{
+    return zsk::lz4_kernel_name(nframes);
+}
+
+extern "C" ZSEEK_EXPORT const char *zsk_lz4_parse_kernel_name(uint32_t nframes, uint32_t c_size)
+{
+    return zsk::parse_kernel_name(nframes, c_size);
+}
+
+#ifdef ZSK_TUNING
+// Kernel tuning hook (libzseek_tune.so only): decode with an explicit launch
+// variant, see launch_lz4_frames_variant (tuning.hip).
 extern "C" ZSEEK_EXPORT int zsk_dev_lz4_decode_variant(int variant, const zsk_frame_desc_t *d_desc,
                                                        uint32_t nframes, const void *d_comp,
                                                        void *d_out, int32_t *d_status,
@@ -586,11 +609,7 @@ extern "C" ZSEEK_EXPORT int zsk_dev_lz4_decode_variant(int variant, const zsk_fr
                                      static_cast<uint8_t *>(d_out), d_status,
                                      static_cast<hipStream_t>(stream));
 }
-
-extern "C" ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes)
-{
-    return zsk::lz4_kernel_name(nframes);
-}
+#endif
 
 extern "C" ZSEEK_EXPORT int zsk_zstd_decode_frames(const zsk_frame_desc_t *d_desc,
                                                    uint32_t nframes, const void *d_comp,

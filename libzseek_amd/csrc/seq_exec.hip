@@ -1,33 +1,23 @@
 // seq_exec.hip — sequence execution for the two-phase decoders (gfx950).
 //
-// Input: per-sequence items (lz4_parse_kernel, lz4_split.hip) = literal run
-// (source offset + length) followed by a match (offset, length).  One wave
-// executes one frame, 64 sequences (one per lane) per batch; the batch's
-// output is assembled in a small per-wave *linear* LDS stage and leaves it as
-// aligned 16-byte chunks, consecutive lanes -> consecutive chunks, so HBM
-// sees only full coalesced writes of exactly the output bytes.
+// Input: per-sequence items (the LZ4 parse kernels lz4_lean / lz4_scan /
+// lz4_chunk, or zstd_seq_kernel) = a literal run (source offset + length)
+// followed by a match (offset, length).  One wave executes one frame, 64
+// sequences (one per lane) per batch; the batch's output is assembled in a
+// small per-wave *linear* LDS stage and leaves it as aligned 16-byte chunks,
+// consecutive lanes -> consecutive chunks, so HBM sees only full coalesced
+// writes of exactly the output bytes.  Per batch:
+//   * item decode and the output prefix sum on DPP (row_shr / row_bcast /
+//     wave_shl), no ds_bpermute chains;
+//   * round 0: literal runs and matches whose source precedes the batch — one
+//     8-byte descriptor per 16-byte piece from one base per run, the wave's
+//     pieces dealt one per lane per slot, four slots' loads in flight;
+//   * dependency rounds: a match whose source meets a lower pending match's
+//     destination waits; readiness by binary search over the pending
+//     destinations compacted in LDS (1.7 rounds per batch on the synthetic);
+//   * flush: four chunks' stage reads in flight before their stores; the next
+//     batch's items are shifted in before it.
 //
-// Versus lz4_stage.hip (v1/v2) this engine is built for occupancy and short
-// dependency chains:
-//   * 4 KiB stage per wave (no ring, no mirror pads): ~8 waves per SIMD;
-//   * prefix sums and neighbour exchange on DPP (row_shr / row_bcast /
-//     wave_shl), not ds_bpermute chains;
-//   * each lane copies its own runs, 16-byte pieces, two pieces of each run
-//     per step with every load issued before any write (no piece->run
-//     search);
-//   * loads that a lane does not need are disabled by an out-of-range buffer
-//     offset instead of a branch, so the compiler can keep them in flight
-//     together.
-//
-// Stage layout: stage index i holds frame output byte x = i + 16*cb - a0,
-// a0 = output address & 15, so stage chunk k (16 bytes at 16k) is output
-// chunk cb + k, 16-byte aligned in HBM.  The stage always holds chunk fc - 1
-// (flushed, kept for sources in [flushed - 16, flushed)) and the partial
-// chunk fc onward; after a batch, those two chunks move to index 0.
-//
-// Semantics follow LZ4_decompress_safe (liblz4 1.9.3) sequence execution as
-// used by the reference reader (decompress.c:631,653,762); validation already
-// happened in the parse phase, which only hands frames with status ST_OK here.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -45,18 +35,10 @@ constexpr uint32_t kItemExt = 0x80000000u;
 constexpr uint32_t kItemPos = 0x3FFFFFFFu;
 constexpr uint32_t kXW = 4;                 // waves (frames) per workgroup
 // per wave, for OUTB output bytes staged per batch at most: the stage (2 kept
-// chunks + read slack) and the piece descriptors (one per 16-byte piece)
+// chunks + read slack) and the piece descriptors (one per 16-byte piece, 8 B)
 constexpr uint32_t x_buf(uint32_t outb) { return outb + 80; }
 constexpr uint32_t x_pieces(uint32_t outb) { return outb / 16 + 2 * 64; }
-// after the stage: piece descriptors (copy_desc, 8 B per piece) or the run
-// table + piece owners (copy_scan, 32 B per lane + 4 B per piece)
-constexpr uint32_t kXOwn = 6;   // piece owners per lane in the blocked scan
-constexpr uint32_t x_wave(uint32_t outb)
-{
-    return x_buf(outb) + (8 * x_pieces(outb) > 32 * 64 + 4 * 64 * kXOwn ? 8 * x_pieces(outb)
-                                                                        : 32 * 64 + 4 * 64 * kXOwn);
-}
-static_assert(x_pieces(4096) <= 64 * kXOwn, "piece owners");
+constexpr uint32_t x_wave(uint32_t outb) { return x_buf(outb) + 8 * x_pieces(outb); }
 constexpr uint32_t kBad = 0x80000000u;      // buffer offset past any range: load returns 0
 
 typedef u32x4 u32x4_l __attribute__((aligned(1)));
@@ -144,35 +126,6 @@ __device__ __forceinline__ u32x4 src16(const Stage &S, const Out &O, uint32_t fl
     return h ? vh : vl;
 }
 
-// Copy this lane's literal run (lit bytes of the literal source at src ->
-// output op) and a match run (mn bytes from output msrc -> mb; final source,
-// no overlap) into the stage: pieces j, j+1 of both runs per step, all four
-// loads issued before the writes.
-__device__ __forceinline__ void copy_own(const Stage &S, const Out &O, const Span &lsp,
-                                         uint32_t flushed, uint32_t src, uint32_t op,
-                                         uint32_t lit, uint32_t msrc, uint32_t mb, uint32_t mn)
-{
-    const uint32_t lpn = npieces(lit), mpn = npieces(mn);
-    const uint32_t ln = lit < 16 ? lit : 16, mnn = mn < 16 ? mn : 16;
-    for (uint32_t j = 0; __ballot(j < lpn || j < mpn); j += 2) {
-        const bool l0 = j < lpn, l1 = j + 1 < lpn, m0 = j < mpn, m1 = j + 1 < mpn;
-        const uint32_t ol0 = piece_off(lit, j), ol1 = piece_off(lit, j + 1);
-        const uint32_t om0 = piece_off(mn, j), om1 = piece_off(mn, j + 1);
-        const u32x4 vl0 = load16u(lsp.r, l0 ? lsp.s0 + src + ol0 : kBad);
-        const u32x4 vl1 = load16u(lsp.r, l1 ? lsp.s0 + src + ol1 : kBad);
-        const u32x4 vm0 = src16(S, O, flushed, msrc + om0, m0);
-        const u32x4 vm1 = src16(S, O, flushed, msrc + om1, m1);
-        if (l0)
-            lds_put(saddr(S, op + ol0), vl0, ln);
-        if (l1)
-            lds_put(saddr(S, op + ol1), vl1, 16);
-        if (m0)
-            lds_put(saddr(S, mb + om0), vm0, mnn);
-        if (m1)
-            lds_put(saddr(S, mb + om1), vm1, 16);
-    }
-}
-
 // 16 bytes at byte offset x of a resource: one unaligned load.  Safe for the
 // LZ4 sources because the hardware range-checks per dword and every byte a
 // piece needs lies at least 4 bytes before its span's end (literal runs are
@@ -189,139 +142,22 @@ __device__ unsigned long long g_xstats[12];   // DIAG 16: cycles per section, co
 
 // Copy, for every lane, a literal run (lit bytes of the literal source at src
 // -> output op) and a match run (mn bytes from output msrc -> mb; final
-// source, no overlap) into the stage.  Each lane first writes one 8-byte
-// descriptor per 16-byte piece (source, stage destination, length, kind) at
-// its piece-prefix position in LDS; then the wave's pieces are dealt one per
-// lane per slot, four slots' loads in flight before any write.
+// source, no overlap) into the stage.  Each lane writes one 8-byte descriptor
+// per 16-byte piece (stage destination, length, kind, source) at its
+// piece-prefix position in LDS — piece o of a run is base + o * (1 + 2^32),
+// source and destination advancing together, a match piece's kind turning
+// from HBM to stage once its source reaches `flushed`; then the wave's pieces
+// are dealt one per lane per slot, four slots' flat 16-byte loads in flight
+// before any write.  A short literal piece near the end of the literal source
+// (the frame's last literals: 16 bytes from their start would pass the
+// frame's end mark, and the last frame's past the caller's buffer) is loaded
+// through the range-checked resource `lsp` instead, whose bytes past llen
+// read as zero.
 template <int DIAG>
-__device__ __forceinline__ void copy_desc(const Stage &S, const Out &O, const Span &lsp,
-                                          uint32_t descs, uint32_t flushed, uint32_t lane,
-                                          uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
-                                          uint32_t mb, uint32_t mn)
-{
-    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
-    const uint32_t inc = wave_incl_add(np);
-    const uint32_t T = lane_val(inc, 63);
-    if (T == 0)
-        return;
-    const uint32_t x = inc - np;
-    for (uint32_t i = 0; __ballot(i < np); i++) {
-        if (i < np) {
-            const bool isl = i < lpn;
-            const uint32_t n = isl ? lit : mn;
-            const uint32_t o = piece_off(n, isl ? i : i - lpn);
-            const uint32_t sx = (isl ? src : msrc) + o;
-            const uint32_t kind = isl ? K_LIT : (sx + 16 <= flushed ? K_HBM : K_STAGE);
-            const uint32_t da = saddr(S, (isl ? op : mb) + o) - S.base;   // < 8 KiB
-            *lp<uint64_t>(descs + 8 * (x + i)) =
-                ((uint64_t)(da | (n < 16 ? n : 16) << 16 | kind << 24) << 32) | sx;
-        }
-    }
-    wave_lds_sync();
-    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
-        u32x4 vl[4], vm[4];
-        uint32_t dw[4], sx[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t t = t0 + 64 * j + lane;
-            const bool on = t < T;
-            const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
-            sx[j] = (uint32_t)D;
-            dw[j] = on ? (uint32_t)(D >> 32) : 0;
-            const uint32_t kind = dw[j] >> 24;
-            vl[j] = bload16(lsp.r, on && kind == K_LIT && !(DIAG & 1) ? lsp.s0 + sx[j] : kBad);
-            vm[j] = bload16(O.sp.r, on && kind == K_HBM && !(DIAG & 1) ? O.sp.s0 + sx[j] : kBad);
-            if (t0 + 64 * j + 64 >= T)
-                break;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t n = (dw[j] >> 16) & 0xFF;
-            if (n) {
-                u32x4 v = vl[j] | vm[j];   // the disabled load returned zeros
-                if ((dw[j] >> 24) == K_STAGE)
-                    v = lds16(saddr(S, sx[j]));
-                lds_put(S.base + (dw[j] & 0xFFFF), v, n);
-            }
-            if (t0 + 64 * j + 64 >= T)
-                break;
-        }
-    }
-}
-
-// copy_desc with cheaper descriptor generation: one base descriptor per run
-// (literal, match); piece o of a run is base + o * (1 + 2^32) — its source and
-// its stage destination advance together — and a match piece's kind turns
-// from HBM to stage once its source reaches `flushed`.  Same descriptors,
-// same loads and writes as copy_desc.
-template <int DIAG>
-__device__ __forceinline__ void copy_desc2(const Stage &S, const Out &O, const Span &lsp,
-                                           uint32_t descs, uint32_t flushed, uint32_t lane,
-                                           uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
-                                           uint32_t mb, uint32_t mn)
-{
-    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
-    const uint32_t inc = wave_incl_add(np);
-    const uint32_t T = lane_val(inc, 63);
-    if (T == 0)
-        return;
-    const uint32_t x = inc - np;
-    const uint64_t dl = ((uint64_t)((saddr(S, op) - S.base) | (lit < 16 ? lit : 16) << 16 | K_LIT << 24) << 32) | src;
-    const uint64_t dm = ((uint64_t)((saddr(S, mb) - S.base) | (mn < 16 ? mn : 16) << 16 | K_HBM << 24) << 32) | msrc;
-    const uint32_t lm = lit < 16 ? 0 : lit - 16, mm = mn < 16 ? 0 : mn - 16;
-    uint32_t a = descs + 8 * x;
-    for (uint32_t i = 0; __ballot(i < np); i++) {
-        if (i < np) {
-            const bool isl = i < lpn;
-            const uint32_t o = min(16 * (isl ? i : i - lpn), isl ? lm : mm);
-            uint64_t D = (isl ? dl : dm) + (uint64_t)o * 0x100000001ull;
-            if (!isl && msrc + o + 16 > flushed)
-                D += (uint64_t)(K_STAGE - K_HBM) << 56;
-            *lp<uint64_t>(a) = D;
-        }
-        a += 8;
-    }
-    wave_lds_sync();
-    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
-        u32x4 vl[4], vm[4];
-        uint32_t dw[4], sx[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t t = t0 + 64 * j + lane;
-            const bool on = t < T;
-            const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
-            sx[j] = (uint32_t)D;
-            dw[j] = on ? (uint32_t)(D >> 32) : 0;
-            const uint32_t kind = dw[j] >> 24;
-            vl[j] = bload16(lsp.r, on && kind == K_LIT && !(DIAG & 1) ? lsp.s0 + sx[j] : kBad);
-            vm[j] = bload16(O.sp.r, on && kind == K_HBM && !(DIAG & 1) ? O.sp.s0 + sx[j] : kBad);
-            if (t0 + 64 * j + 64 >= T)
-                break;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t n = (dw[j] >> 16) & 0xFF;
-            if (n) {
-                u32x4 v = vl[j] | vm[j];   // the disabled load returned zeros
-                if ((dw[j] >> 24) == K_STAGE)
-                    v = lds16(saddr(S, sx[j]));
-                lds_put(S.base + (dw[j] & 0xFFFF), v, n);
-            }
-            if (t0 + 64 * j + 64 >= T)
-                break;
-        }
-    }
-}
-
-// copy_desc2 with one flat 16-byte load per piece (literal source or frame
-// output by the piece's kind; stage pieces load the literal base, unused)
-// instead of two range-checked buffer loads with one disabled: half the
-// vector-memory ops and 16 fewer VGPRs for the four slots in flight.
-template <int DIAG>
-__device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase, const uint8_t *obase,
-                                           uint32_t descs, uint32_t flushed, uint32_t lane,
-                                           uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
-                                           uint32_t mb, uint32_t mn)
+__device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase, const Span &lsp,
+                                           uint32_t llen, const uint8_t *obase, uint32_t descs,
+                                           uint32_t flushed, uint32_t lane, uint32_t src, uint32_t op,
+                                           uint32_t lit, uint32_t msrc, uint32_t mb, uint32_t mn)
 {
     const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
     const uint32_t inc = wave_incl_add(np);
@@ -348,6 +184,7 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
     for (uint32_t t0 = 0; t0 < T; t0 += 256) {
         u32x4 v[4];
         uint32_t dw[4], sx[4];
+        bool tail[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t t = t0 + 64 * j + lane;
@@ -356,8 +193,11 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
             sx[j] = (uint32_t)D;
             dw[j] = on ? (uint32_t)(D >> 32) : 0;
             const uint32_t kind = dw[j] >> 24;
-            const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);
+            tail[j] = on && kind == K_LIT && sx[j] + 16 > llen;
+            const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT && !tail[j] ? sx[j] : 0);
             v[j] = (DIAG & 1) ? (u32x4){0, 0, 0, 0} : *reinterpret_cast<const u32x4_l *>(p);
+            if (__ballot(tail[j]))
+                v[j] = tail[j] ? bload16(lsp.r, lsp.s0 + sx[j]) : v[j];
             if (t0 + 64 * j + 64 >= T)
                 break;
         }
@@ -369,84 +209,6 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
                 if ((dw[j] >> 24) == K_STAGE)
                     w = lds16(saddr(S, sx[j]));
                 lds_put(S.base + (dw[j] & 0xFFFF), w, n);
-            }
-            if (t0 + 64 * j + 64 >= T)
-                break;
-        }
-    }
-}
-
-// copy_desc with piece-parallel descriptors: instead of each lane looping
-// over its own pieces (as many steps as the batch's longest run), each lane
-// writes its two runs to a table, marks its first piece in an owner array,
-// and one blocked prefix max over the array gives every piece slot its
-// owning lane; a slot then reads its run from the table.  Same loads, same
-// writes, same order as copy_desc.
-template <int DIAG>
-__device__ __forceinline__ void copy_scan(const Stage &S, const Out &O, const Span &lsp,
-                                          uint32_t tab, uint32_t flushed, uint32_t lane,
-                                          uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc,
-                                          uint32_t mb, uint32_t mn)
-{
-    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
-    const uint32_t inc = wave_incl_add(np);
-    const uint32_t T = lane_val(inc, 63);
-    if (T == 0)
-        return;
-    const uint32_t x = inc - np;
-    const uint32_t own = tab + 32 * 64;   // owner + 1 of piece t at own + 4 t
-    *lp<u32x4>(tab + 32 * lane) = (u32x4){src, op, lit, x};
-    *lp<u32x4>(tab + 32 * lane + 16) = (u32x4){msrc, mb, mn, lpn};
-    const uint32_t ob = own + 4 * kXOwn * lane;   // this lane's block of owners
-    // one access type for the owner array (uint32_t): a mixed-width
-    // access would let the compiler forward the cleared value past the marks
-#pragma unroll
-    for (uint32_t k = 0; k < kXOwn; k++)
-        *lp<uint32_t>(ob + 4 * k) = 0;
-    if (np)
-        *lp<uint32_t>(own + 4 * x) = lane + 1;
-    wave_lds_sync();
-    uint32_t o[kXOwn];
-#pragma unroll
-    for (uint32_t k = 0; k < kXOwn; k++)
-        o[k] = *lp<uint32_t>(ob + 4 * k);
-#pragma unroll
-    for (uint32_t k = 1; k < kXOwn; k++)
-        o[k] = max(o[k], o[k - 1]);
-    const uint32_t carry = dpp_prev(wave_incl_max(o[kXOwn - 1]), 0);
-#pragma unroll
-    for (uint32_t k = 0; k < kXOwn; k++)
-        *lp<uint32_t>(ob + 4 * k) = max(o[k], carry);
-    wave_lds_sync();
-    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
-        u32x4 vl[4], vm[4];
-        uint32_t da[4], sx[4], nn[4], kd[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t t = t0 + 64 * j + lane;
-            const bool on = t < T;
-            const uint32_t r = on ? *lp<uint32_t>(own + 4 * t) - 1 : 0;
-            const u32x4 e0 = *lp<u32x4>(tab + 32 * r), e1 = *lp<u32x4>(tab + 32 * r + 16);
-            const uint32_t i = t - e0.w;
-            const bool isl = i < e1.w;
-            const uint32_t n = isl ? e0.z : e1.z;
-            const uint32_t po = piece_off(n, isl ? i : i - e1.w);
-            sx[j] = (isl ? e0.x : e1.x) + po;
-            da[j] = saddr(S, (isl ? e0.y : e1.y) + po);
-            nn[j] = on ? (n < 16 ? n : 16) : 0;
-            kd[j] = isl ? K_LIT : (sx[j] + 16 <= flushed ? K_HBM : K_STAGE);
-            vl[j] = bload16(lsp.r, on && kd[j] == K_LIT && !(DIAG & 1) ? lsp.s0 + sx[j] : kBad);
-            vm[j] = bload16(O.sp.r, on && kd[j] == K_HBM && !(DIAG & 1) ? O.sp.s0 + sx[j] : kBad);
-            if (t0 + 64 * j + 64 >= T)
-                break;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (nn[j]) {
-                u32x4 v = vl[j] | vm[j];   // the disabled load returned zeros
-                if (kd[j] == K_STAGE)
-                    v = lds16(saddr(S, sx[j]));
-                lds_put(da[j], v, nn[j]);
             }
             if (t0 + 64 * j + 64 >= T)
                 break;
@@ -600,34 +362,16 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 }
 
 // DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores, 4 = no
-// dependency rounds, 8 = no round 0, 32 = no flush at all
-// MODE: 0 = lane-owned copies and frontier readiness (v3), 1 = piece
-// descriptors (v4), 2 = piece-parallel descriptors (v5), 3 = descriptors from
-// one base per run (v12), 4 = v12 with the rounds' readiness found by a binary
-// search over the pending destinations in LDS (v13), 5 = v13 with one flat
-// load per piece (v15), 6 = v15 with the next batch's items shifted in
-// before the flush (v16), 7 = v16 with four chunks' stage reads in flight per
-// flush step (v17, the default); 1-7 use exact readiness.  Tried and dropped
-// (same-box A/B, config 2): short runs' partial pieces dealt after the full
-// pieces so full slots write unconditionally (4.29 vs 4.13 ms per launch);
-// each batch's flush deferred past the next batch's item decode (4.34 vs
-// 4.03 ms: round 0's load wait then also waits for the flush's stores);
-// the rounds' readiness from an LDS bitmap of pending destination bytes set
-// and cleared with ds_or / ds_and (4.63 vs 4.13 ms; six waves per SIMD (80 VGPRs: 10
-// spilled, 5.33 vs 4.04 ms); round 0's slot loads retired inside each deal
-// step, so the deal's first step issues without waiting on the item prefetch
-// and the last flush (4.001 vs 4.006 ms, no gain); O(1) readiness tests
-// (prefix max of the pending destinations below, the lowest one) before the
-// binary search (4.068 vs 3.996 ms: two more scans per round, the search
-// still needed in most); a persistent grid (1,280 workgroups, frames f,
-// f + stride, ...) prefetching the next frame's item count, base and first
-// items (4.258 vs 4.028 ms; 4 KiB frames 6.255 vs 5.703: the hardware's
-// dynamic dispatch balances frames better than a static stride, and the
-// prefetch registers spill at five waves per SIMD); nontemporal item and / or
-// literal loads, to leave L2 to the match sources (4.020 / 4.039 / 4.016 vs
-// 4.009 ms); 1, 2, 5 or 8 waves per workgroup instead of kXW = 4 (4.27, 4.19,
-// 5.88, 4.46 vs 4.04 ms)
-template <int MODE, int DIAG, uint32_t OUTB>
+// dependency rounds, 8 = no round 0, 16 = section timers and counters
+// (g_xstats), 32 = no flush at all, 64 = flush stage reads without stores.
+// Tried and dropped (same-box A/B, config 2): short runs'
+// partial pieces dealt after the full pieces; each batch's flush deferred past
+// the next batch's item decode; the rounds' readiness from an LDS bitmap; six
+// waves per SIMD (80 VGPRs, spills); round 0's slot loads retired inside each
+// deal step; O(1) readiness pre-tests before the binary search; a persistent
+// grid with next-frame prefetch; nontemporal item / literal loads; 1, 2, 5 or
+// 8 waves per workgroup instead of kXW = 4.
+template <int DIAG, uint32_t OUTB>
 __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
@@ -659,9 +403,9 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     O.sp = make_span(O.o, d.d_size);
     // literal source: the compressed frame (LZ4), or the frame's decoded
     // literals (zstd scratch laid out like the output, 16 bytes of slack)
-    const Span lsp = lit ? make_span(lit + d.d_off, (uint64_t)d.d_size + 16)
-                         : make_span(comp + d.c_off, d.c_size);
+    const uint32_t llen = lit ? d.d_size + 16 : d.c_size;
     const uint8_t *lbase = lit ? lit + d.d_off : comp + d.c_off;
+    const Span lsp = make_span(lbase, llen);
     Stage S;
     S.base = (uint32_t)(uintptr_t)(lds + w * x_wave(OUTB));
     const uint32_t descs = S.base + x_buf(OUTB);
@@ -670,8 +414,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     uint32_t produced = 0;   // frame bytes decoded
     uint32_t fc = 0;         // output chunks [0, fc) are in HBM
     uint64_t cur = lane < nit ? it[lane] : 0;
-    if (MODE >= 6)
-        __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
+    __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
     uint32_t b = 0;
     uint64_t tsec[4] = {0, 0, 0, 0};
     uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
@@ -685,28 +428,27 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
     }
     while (b < nit) {
         const uint64_t nxt =
-            MODE >= 6 ? __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, 8 * (b + 64 + lane), 0, 0))
-                      : (b + 64 + lane < nit ? it[b + 64 + lane] : 0);
+            __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, 8 * (b + 64 + lane), 0, 0));
         const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
         const uint32_t w0n = dpp_next(w0, 0), w1n = dpp_next(w1, 0);
         const uint32_t w0p = dpp_prev(w0, 0);
         const bool act0 = b + lane < nit;
         const uint32_t src = w0 & kItemPos;
         const uint32_t off = (w0 & kItemExt) ? w1 : (w1 & 0xFFFF);   // extended: full offset
-        uint32_t lit = 0, ml = 0;
+        uint32_t lit_n = 0, ml = 0;
         if (act0 && !(w0p & kItemExt)) {
             if (w0 & kItemExt) {
-                lit = w0n;
+                lit_n = w0n;
                 ml = w1n;
             } else {
-                lit = (w1 >> 16) & 0xFF;
+                lit_n = (w1 >> 16) & 0xFF;
                 const uint32_t mc = w1 >> 24;
                 ml = mc ? mc + 3 : 0;
             }
         }
         // batch = the lanes before the first whose output would pass OUTB;
         // an extended item keeps its second half
-        const uint32_t len = lit + ml;
+        const uint32_t len = lit_n + ml;
         const uint32_t inc = wave_incl_add(len);
         const uint64_t over = __ballot(act0 && inc > OUTB);
         uint32_t nb = over ? (uint32_t)__builtin_ctzll(over) : 64;
@@ -719,7 +461,7 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         const uint32_t flushed = 16 * fc > S.a0 ? 16 * fc - S.a0 : 0;   // frame bytes < this are in HBM
         if (nb == 0) {
             // lane 0 alone is too long to stage: flush, copy in HBM, reload
-            const uint32_t l0 = lane_val(lit, 0), m0 = lane_val(ml, 0);
+            const uint32_t l0 = lane_val(lit_n, 0), m0 = lane_val(ml, 0);
             const uint32_t s0 = lane_val(src, 0), o0 = lane_val(off, 0);
             const uint32_t end_c = (produced + S.a0 + 15) >> 4;
             for (uint32_t c = fc + lane; c < end_c; c += 64)
@@ -755,12 +497,12 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
             continue;
         }
         if (lane >= nb) {
-            lit = 0;
+            lit_n = 0;
             ml = 0;
         }
         const uint32_t bstart = produced;
         const uint32_t op = produced + inc - len;
-        const uint32_t mb = op + lit;
+        const uint32_t mb = op + lit_n;
         const uint32_t me = mb + ml;
         const uint32_t msrc = mb - off;
         const bool overlap = ml != 0 && off < ml;
@@ -769,24 +511,14 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if (DIAG & 8)
-            ;
-        else if (MODE >= 5)
-            copy_desc3<DIAG>(S, lbase, O.o, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
-        else if (MODE == 3 || MODE == 4)
-            copy_desc2<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
-        else if (MODE == 2)
-            copy_scan<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
-        else if (MODE == 1)
-            copy_desc<DIAG>(S, O, lsp, descs, flushed, lane, src, op, lit, msrc, mb, early ? ml : 0);
-        else
-            copy_own(S, O, lsp, flushed, src, op, lit, msrc, mb, early ? ml : 0);
+        if (!(DIAG & 8))
+            copy_desc3<DIAG>(S, lbase, lsp, llen, O.o, descs, flushed, lane, src, op, lit_n, msrc, mb,
+                             early ? ml : 0);
         wave_lds_sync();   // stage bytes of other lanes from here on
         ZSK_T(1)
         // rounds: matches reading bytes of this batch
         uint64_t pending = (DIAG & 4) ? 0 : __ballot(ml != 0 && !early);
         if (DIAG & 16) {
-            tsec[4 - 4] += 0;
             cnt[0] += 1;
             cnt[1] += __builtin_popcountll(pending);
             cnt[2] += __builtin_popcountll(__ballot(ml != 0 && !early && msrc < bstart));
@@ -795,65 +527,42 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         }
         while (pending) {
             const bool mine = (pending >> lane) & 1;
-            bool ready;
-            if (MODE >= 4) {
-                // pending destinations are ascending and disjoint: compact
-                // them (lane order) into the descriptor area, then binary-
-                // search the first one below this lane that ends after msrc;
-                // blocked iff it also starts before need
-                const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-                    (uint32_t)(pending >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pending, 0u));
-                if (mine)
-                    *lp<uint64_t>(descs + 8 * below) = ((uint64_t)me << 32) | mb;
-                wave_lds_sync();
-                uint32_t lo = 0, hi = mine ? below : 0;
-                while (__ballot(lo < hi)) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    const uint32_t mem = lo < hi ? (uint32_t)(*lp<uint64_t>(descs + 8 * mid) >> 32) : 0;
-                    if (lo < hi) {
-                        if (mem > msrc)
-                            hi = mid;
-                        else
-                            lo = mid + 1;
-                    }
+            // pending destinations are ascending and disjoint: compact them
+            // (lane order) into the descriptor area, then binary-search the
+            // first one below this lane that ends after msrc; blocked iff it
+            // also starts before need
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(pending >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pending, 0u));
+            if (mine)
+                *lp<uint64_t>(descs + 8 * below) = ((uint64_t)me << 32) | mb;
+            wave_lds_sync();
+            uint32_t lo = 0, hi = mine ? below : 0;
+            while (__ballot(lo < hi)) {
+                const uint32_t mid = (lo + hi) >> 1;
+                const uint32_t mem = lo < hi ? (uint32_t)(*lp<uint64_t>(descs + 8 * mid) >> 32) : 0;
+                if (lo < hi) {
+                    if (mem > msrc)
+                        hi = mid;
+                    else
+                        lo = mid + 1;
                 }
-                const uint32_t mbl = (uint32_t)*lp<uint64_t>(descs + 8 * (mine && lo < below ? lo : 0));
-                ready = mine && !(lo < below && mbl < need);
-                wave_lds_sync();
-            } else if (MODE != 0) {
-                // blocked while the source meets a lower pending match's destination
-                bool blocked = false;
-                uint64_t pj = pending;
-                while (pj) {
-                    const int j = __builtin_ctzll(pj);
-                    pj &= pj - 1;
-                    const uint32_t mbj = lane_val(mb, j), mej = lane_val(me, j);
-                    blocked = blocked || ((uint32_t)j < lane && mbj < need && mej > msrc);
-                }
-                ready = mine && !blocked;
-            } else {
-                const uint64_t below = pending & ((1ull << lane) - 1);
-                const int hb = below ? 63 - __builtin_clzll(below) : (int)lane;
-                const uint32_t me_hb = (uint32_t)__shfl(me, hb, 64);
-                const uint32_t frontier = lane_val(mb, __builtin_ctzll(pending));
-                ready = mine && (below == 0 || need <= frontier || msrc >= me_hb);
             }
+            const uint32_t mbl = (uint32_t)*lp<uint64_t>(descs + 8 * (mine && lo < below ? lo : 0));
+            const bool ready = mine && !(lo < below && mbl < need);
+            wave_lds_sync();
             if (ready && overlap)
                 copy_overlap(S, O, flushed, mb, off, ml);
-            if (MODE != 0)
-                copy_round(S, O, flushed, msrc, mb, ready && !overlap ? ml : 0);
-            else
-                copy_own(S, O, lsp, flushed, 0, 0, 0, msrc, mb, ready && !overlap ? ml : 0);
+            copy_round(S, O, flushed, msrc, mb, ready && !overlap ? ml : 0);
             pending &= ~__ballot(ready);
             wave_lds_sync();
             if (DIAG & 16)
                 cnt[5] += 1;
         }
         ZSK_T(2)
-        if (MODE >= 6) {
-            // the next batch's items before the flush: the wait for nxt (issued
-            // at the top of this batch) then does not also wait for the
-            // flush's stores
+        // the next batch's items before the flush: the wait for nxt (issued
+        // at the top of this batch) then does not also wait for the flush's
+        // stores
+        {
             const uint64_t a = __shfl_down(cur, nb & 63, 64);
             const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
             cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
@@ -861,13 +570,8 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         // flush complete chunks (the frame's last chunk exactly)
         const bool last = b + nb >= nit;
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
-        if (DIAG & 34)
-            ;
-        else if (MODE >= 7)
+        if (!(DIAG & 34))
             flush_chunks4<DIAG>(S, O, fc, end_c, lane);
-        else
-            for (uint32_t c = fc + lane; c < end_c; c += 64)
-                flush_chunk(S, O, c);
         fc = end_c;
         // keep chunks fc-1 (flushed) and fc (partial) at stage index 0
         wave_lds_sync();
@@ -881,11 +585,6 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
         }
         wave_lds_sync();
         b += nb;
-        if (MODE < 6) {
-            const uint64_t a = __shfl_down(cur, nb & 63, 64);
-            const uint64_t c2 = __shfl(nxt, (int)((lane + nb) & 63), 64);
-            cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
-        }
         ZSK_T(3)
     }
 #undef ZSK_T
@@ -899,6 +598,8 @@ __global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
 
 }   // namespace
 
+// version: 0 = the production kernel; tuning builds add diagnostics
+// (DIAG bits above) as 0x100 | DIAG.
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
@@ -907,36 +608,20 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     if (nframes == 0)
         return 0;
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
-#define ZSK_X(D, G)   ZSK_XB(D, G, 4096)
-#define ZSK_XB(D, G, B)                                                                        \
-    hipLaunchKernelGGL((seq_exec_kernel<D, G, B>), grid, block, 0, stream, d_desc, nframes, d_comp, \
+#define ZSK_X(D)                                                                                   \
+    hipLaunchKernelGGL((seq_exec_kernel<D, 4096>), grid, block, 0, stream, d_desc, nframes, d_comp, \
                        d_out, rec_base, items, nitems, d_status, nullptr)
+#ifdef ZSK_TUNING
     switch (version) {
-    case 3: ZSK_X(0, 0); break;
-    case 5: ZSK_X(1, 1); break;
-    case 6: ZSK_X(1, 2); break;
-    case 7: ZSK_X(1, 3); break;
-    case 9: ZSK_XB(1, 0, 3072); break;
-    case 10: ZSK_XB(1, 0, 2048); break;
-    case 11: ZSK_X(2, 0); break;
-    case 12: ZSK_X(3, 0); break;
-    case 13: ZSK_X(4, 0); break;
-    case 15: ZSK_X(5, 0); break;
-    case 16: ZSK_X(6, 0); break;
-    case 17: ZSK_X(7, 0); break;
-    case 27: ZSK_X(5, 4); break;
-    case 28: ZSK_X(5, 8); break;
-    case 29: ZSK_X(5, 34); break;
-    case 30: ZSK_X(5, 1); break;
-    case 31: ZSK_X(7, 64); break;
-    case 8:
-    case 14: {
+    case 0x101: ZSK_X(1); break;
+    case 0x104: ZSK_X(4); break;
+    case 0x108: ZSK_X(8); break;
+    case 0x122: ZSK_X(34); break;
+    case 0x140: ZSK_X(64); break;
+    case 0x110: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
-        if (version == 14)
-            ZSK_X(4, 16);
-        else
-            ZSK_X(1, 16);
+        ZSK_X(16);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_xstats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
         (void)hipStreamSynchronize(stream);
         const double t = (double)(z[0] + z[1] + z[2] + z[3]);
@@ -947,10 +632,13 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                 z[8] / nb, z[5] / nb, z[6] / nb, z[7] / nb, z[9] / nb);
         break;
     }
-    default: ZSK_X(1, 0); break;
+    default: ZSK_X(0); break;
     }
+#else
+    (void)version;
+    ZSK_X(0);
+#endif
 #undef ZSK_X
-#undef ZSK_XB
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -960,7 +648,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<7, 0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+    hipLaunchKernelGGL((seq_exec_kernel<0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

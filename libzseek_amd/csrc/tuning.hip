@@ -1,0 +1,67 @@
+// tuning.hip — launch variants for A/B timing (scripts/kbench.py).
+//
+// Compiled only into libzseek_amd/lib/libzseek_tune.so (-DZSK_TUNING); the
+// product library libzseek.so carries the production kernels alone.  A
+// variant is a route, a subset of the two-phase decoder's stages, or a
+// diagnostic build of one kernel (wrong output, timing only).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <mutex>
+
+#include "zsk_internal.h"
+
+namespace zsk {
+
+namespace {
+std::mutex g_mu;
+SplitScratch g_s;
+
+int staged(int stages, int route, int tune, const FrameDesc *d_desc, uint32_t nframes,
+           const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status, hipStream_t stream)
+{
+    std::lock_guard<std::mutex> g(g_mu);
+    uint64_t want = (uint64_t)nframes * slots_of(65536 + 64);
+    if (want > (512ull << 20))
+        want = 512ull << 20;
+    if (g_s.total && *g_s.total > want)
+        want = *g_s.total;
+    if (split_scratch_reserve(&g_s, nframes, want, stream) != 0)
+        return -1;
+    return launch_lz4_split(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, &g_s, route,
+                            stages, tune);
+}
+}   // namespace
+
+// variant:
+//   0          production (launch_lz4_frames)
+//   1..4       routes: wave / lean / scan / chunk for every frame
+//   10 + r     plan + parse only (route r)
+//   20         execute only, over the items the previous launch left
+//   0x1xx      execute diagnostic DIAG = xx alone (seq_exec.hip; 0x110 prints
+//              section timers)
+//   0x2xx      plan + lean parse with diagnostic bits xx (lz4_lean.hip;
+//              0x204 prints sub-step counters)
+int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
+                              const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                              hipStream_t stream)
+{
+    if (nframes == 0)
+        return 0;
+    if (variant == 0)
+        return launch_lz4_frames(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream);
+    if (variant >= 1 && variant <= 4)
+        return launch_lz4_frames(d_desc, nframes, d_comp, d_out, d_status, nullptr, stream, variant);
+    if (variant >= 10 && variant <= 14)
+        return staged(3, variant - 10, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    if (variant == 20)
+        return staged(4, ROUTE_AUTO, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
+    if ((variant & 0xF00) == 0x100)
+        return staged(4, ROUTE_AUTO, (variant & 0x1FF) << 8, d_desc, nframes, d_comp, d_out, d_status,
+                      stream);
+    if ((variant & 0xF00) == 0x200)
+        return staged(3, ROUTE_LEAN, variant & 0xFF, d_desc, nframes, d_comp, d_out, d_status, stream);
+    return -1;
+}
+
+}   // namespace zsk

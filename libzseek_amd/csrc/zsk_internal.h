@@ -56,16 +56,22 @@ inline uint32_t status_max_block(int32_t st)
     return 1u << (8 + 2 * (((st >> ST_BSID_SHIFT) & 3) + 4));
 }
 
-// Launch the LZ4 frame decoder over nframes frames (asynchronous on stream).
-// d_fail_at (optional) receives, per frame, the output offset of the block
-// whose decode failed.
-// Name (template instance) of the kernel launch_lz4_frames uses, for
-// matching profiler output.
+// Name of the dominant kernel launch_lz4_frames uses for nframes frames
+// (execute kernel of the two-phase decoder, or the wave kernel), for matching
+// profiler output.
 const char *lz4_kernel_name(uint32_t nframes);
 
+// Production decoders a batch can be forced through (tests; ROUTE_AUTO is the
+// library's own choice).  LEAN / SCAN / CHUNK: the two-phase decoder with that
+// parse for every frame.
+enum : int { ROUTE_AUTO = 0, ROUTE_WAVE = 1, ROUTE_LEAN = 2, ROUTE_SCAN = 3, ROUTE_CHUNK = 4 };
+
+// Launch the LZ4 frame decoder over nframes frames (asynchronous on stream).
+// d_fail_at (optional) receives, per frame, the output offset of the block
+// whose decode failed.  tune: tuning builds only (0 = production kernels).
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
-                      hipStream_t stream);
+                      hipStream_t stream, int route = ROUTE_AUTO, int tune = 0);
 
 // Scratch of the two-phase decoder (lz4_split.hip): per-frame item slot
 // offsets and counts, and the items themselves (one u32 per LZ4 sequence).
@@ -85,16 +91,34 @@ uint64_t split_items_needed(const FrameDesc *h_desc, uint32_t n);
 int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipStream_t stream);
 void split_scratch_free(SplitScratch *s);
 
+// Scratch for device-API calls (no reader): a small pool per device of
+// scratch sets, each reused in stream order (an event recorded after the
+// launches that use it; a later call on another stream waits on that event
+// instead of allocating).  Bounded: kPoolSets sets per device.
+constexpr int kPoolSets = 4;
+SplitScratch *stream_scratch(hipStream_t stream);
+void stream_scratch_done(SplitScratch *s, hipStream_t stream);
+
+// Parse routing of the two-phase decoder: frames of >= chunk_min compressed
+// bytes take lz4_chunk_kernel, of [lean_min, chunk_min) lz4_lean_kernel,
+// shorter ones lz4_scan_kernel.
+struct ParseRoute {
+    uint32_t chunk_min, lean_min;
+};
+ParseRoute parse_route(uint32_t nframes, int route);
+// The parse kernel a frame of c_size compressed bytes takes in a batch of
+// nframes (what a kernel trace shows), for tooling.
+const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route = ROUTE_AUTO);
+
 // Two-phase decoder with caller-owned scratch (must cover nframes and the
 // frames' item slots; frames that do not fit are decoded by the wave kernel).
+// stages: bitmask 1 plan, 2 parse, 4 execute, 8 hand-offs (tuning builds
+// time subsets).
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
-                     hipStream_t stream, SplitScratch *s, int stages = 15, int diag = 0);
-int launch_lz4_split_stages(int stages, int diag, const FrameDesc *d_desc, uint32_t nframes,
-                            const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
-                            hipStream_t stream);
+                     hipStream_t stream, SplitScratch *s, int route = ROUTE_AUTO, int stages = 15,
+                     int tune = 0);
 
-// Decoder selection (env ZSEEK_HIP_KERNEL = lane | split | wave; default auto).
 // Item slots of a frame in the split decoder's scratch.  An item is 8 bytes;
 // a sequence takes one (two when extended), a stored block two.  LZ4 data
 // spends >= 3 compressed bytes per sequence and typically 8-25; one slot per
@@ -105,7 +129,8 @@ __host__ __device__ __forceinline__ uint32_t slots_of(uint32_t c_size)
     return (c_size / 8 + 32 + 3) & ~3u;
 }
 
-enum : int { ENGINE_AUTO = 0, ENGINE_LANE, ENGINE_SPLIT, ENGINE_WAVE };
+// Decoder selection (env ZSEEK_HIP_KERNEL = split | wave; default auto).
+enum : int { ENGINE_AUTO = 0, ENGINE_SPLIT, ENGINE_WAVE };
 
 // Per-stage launch timing: stages [plan, parse, execute, hand-off]; marks
 // 0..4 are the boundaries, recorded as HIP events on the launch's stream
@@ -117,19 +142,13 @@ int kernel_times(double *ms, int cap);
 int lz4_engine();
 int lz4_pick_engine(uint32_t nframes);   // never ENGINE_AUTO
 
-// Execute phase with LDS-staged output (lz4_stage.hip), over the split
-// decoder's items.
-int launch_lz4_exec_stage(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                          uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
-                          const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                          int version = 1);
-
-// Execute phase v3 (seq_exec.hip): linear per-wave LDS stage, DPP scans,
-// lane-owned piece copies.
+// Execute phase (seq_exec.hip): one wave per frame, linear per-wave LDS
+// stage, DPP scans, piece descriptors.  version: tuning builds only (0 = the
+// production kernel).
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                    int version = 4);
+                    int version = 0);
 
 // Execute phase over items whose literal runs come from a literal scratch
 // laid out like the output (zstd): frame f's literals at lit + d_off[f].
@@ -177,15 +196,16 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
                        uint32_t *d_fail_at = nullptr);
 
-// Parse phase, streaming lane-per-frame (lz4_scan.hip): same outputs as
-// lz4_parse_kernel.  version 1 = the if/return fast path (A/B builds).
+// Parse phase, streaming lane-per-frame (lz4_scan.hip), for the frames
+// under max_csize compressed bytes (the short frames of config 3).
 int launch_lz4_scan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items,
                     uint32_t *nitems, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
-                    int version = 0, uint32_t max_csize = 0xFFFFFFFFu);
+                    uint32_t max_csize = 0xFFFFFFFFu);
 
 // Parse phase, streaming lane-per-frame with a one-sequence fast step
-// (lz4_lean.hip): the outputs of launch_lz4_chunk (items without padding).
+// (lz4_lean.hip), frames of [min_csize, max_csize) compressed bytes: the
+// outputs of launch_lz4_chunk (items without padding).  diag: tuning builds.
 int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t max_csize,
@@ -209,25 +229,23 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 // Env ZSEEK_PARSE=scan|chunk forces one parse for every frame.
 uint32_t chunk_parse_min(uint32_t nframes);
 
-// Lane-per-frame decoder (lz4_lane.hip) + hand-offs to the wave kernel.
-int launch_lz4_lane(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
-                    uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
-                    int diag = 0);
-
 // Wave-per-frame kernel over only the frames whose status is ST_NOT_RUN
 // (the split decoder's hand-offs).
 int launch_lz4_wave_deferred(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                              uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                              hipStream_t stream);
 
-// Wave-per-frame kernel (lz4_wave.hip): variant 0 = 4 KiB ring, 4 waves.
-int launch_lz4_wave(int variant, const FrameDesc *d_desc, uint32_t nframes,
-                    const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
-                    uint32_t *d_fail_at, hipStream_t stream);
+// Wave-per-frame kernel (lz4_wave.hip): 4 KiB LDS ring, 4 waves per workgroup.
+int launch_lz4_wave(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
+                    uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream);
 
+#ifdef ZSK_TUNING
+// Tuning builds (libzseek_tune.so, scripts/kbench.py): experimental launch
+// variants and diagnostics, never in the product library.
 int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
                               const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
                               hipStream_t stream);
+#endif
 
 const char *status_name(int32_t st);
 

@@ -89,7 +89,8 @@ EXPORTED = [
     "zseek_writer_open_full", "zseek_writer_open", "zseek_writer_close", "zseek_write",
     "zseek_writer_stats", "zseek_reader_open_full", "zseek_reader_open", "zseek_reader_close",
     "zseek_pread", "zseek_read", "zseek_reader_stats",
-    "zsk_lz4_decode_frames", "zsk_status_string", "zsk_lz4_kernel_name", "zsk_reader_frames", "zsk_reader_type",
+    "zsk_lz4_decode_frames", "zsk_lz4_decode_frames_ex", "zsk_status_string", "zsk_lz4_kernel_name",
+    "zsk_lz4_parse_kernel_name", "zsk_reader_frames", "zsk_reader_type",
     "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
     "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
     "zsk_verify_frame_checksums", "zsk_reader_set_verify_checksums",
@@ -134,11 +135,13 @@ def lib() -> C.CDLL:
     L.zsk_zstd_decode_frames.restype = C.c_int
     L.zsk_zstd_decode_frames.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_void_p]
-    L.zsk_dev_lz4_decode_variant.restype = C.c_int
-    L.zsk_dev_lz4_decode_variant.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p,
-                                             C.c_void_p, C.c_void_p, C.c_void_p]
+    L.zsk_lz4_decode_frames_ex.restype = C.c_int
+    L.zsk_lz4_decode_frames_ex.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_int]
     L.zsk_lz4_kernel_name.restype = C.c_char_p
     L.zsk_lz4_kernel_name.argtypes = [C.c_uint32]
+    L.zsk_lz4_parse_kernel_name.restype = C.c_char_p
+    L.zsk_lz4_parse_kernel_name.argtypes = [C.c_uint32, C.c_uint32]
     L.zsk_kernel_timing.restype = C.c_int
     L.zsk_kernel_timing.argtypes = [C.c_int]
     L.zsk_kernel_times.restype = C.c_int
@@ -193,6 +196,12 @@ def tools() -> C.CDLL:
 
 def status_string(status: int) -> str:
     return lib().zsk_status_string(status).decode()
+
+
+def parse_kernel_name(nframes: int, c_size: int) -> str:
+    """The parse kernel the library routes a frame of c_size compressed bytes
+    to in a batch of nframes frames (zsk_lz4_parse_kernel_name)."""
+    return lib().zsk_lz4_parse_kernel_name(nframes, c_size).decode()
 
 
 # ---------------------------------------------------------------------------
@@ -434,10 +443,9 @@ def seek_table_of(image: np.ndarray):
         r.close()
 
 
-# Decoder engines reachable through the (non-ABI) tuning hook
-# zsk_dev_lz4_decode_variant: each one a complete decoder incl. its hand-offs.
-ENGINES = {"wave": 20, "lane": 50, "split": 35, "stage": 34, "exec3": 37, "scan": 39, "exec4": 78,
-           "exec12": 77, "exec13": 79, "chunk": 80, "scanparse": 81, "scanold": 85}
+# The library's production decoders, forced for every frame through
+# zsk_lz4_decode_frames_ex (ZSK_DECODER_*): each one complete incl. hand-offs.
+DECODERS = {"auto": 0, "wave": 1, "lean": 2, "scan": 3, "chunk": 4}
 
 
 def decode_frames(desc, comp, out, status, stream: int | None = None,
@@ -447,7 +455,8 @@ def decode_frames(desc, comp, out, status, stream: int | None = None,
     desc: uint8 tensor holding N x 24-byte zsk_frame_desc_t; comp / out: uint8
     tensors; status: int32 tensor of N.  `stream` is a raw hipStream_t
     (torch.cuda.Stream.cuda_stream); None = the current torch stream.
-    `engine` forces one decoder (tests / tuning; None = the library's choice).
+    `engine` forces one production decoder (DECODERS; None = the library's
+    choice).
     """
     import torch
     n = status.numel()
@@ -462,9 +471,8 @@ def decode_frames(desc, comp, out, status, stream: int | None = None,
         rc = lib().zsk_lz4_decode_frames(desc.data_ptr(), n, comp.data_ptr(), out.data_ptr(),
                                          status.data_ptr(), stream)
     else:
-        rc = lib().zsk_dev_lz4_decode_variant(ENGINES[engine], desc.data_ptr(), n,
-                                              comp.data_ptr(), out.data_ptr(),
-                                              status.data_ptr(), stream)
+        rc = lib().zsk_lz4_decode_frames_ex(desc.data_ptr(), n, comp.data_ptr(), out.data_ptr(),
+                                            status.data_ptr(), stream, DECODERS[engine])
     if rc != 0:
         raise ZseekError("zsk_lz4_decode_frames launch failed")
 

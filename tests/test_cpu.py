@@ -229,7 +229,7 @@ def _declared_symbols():
 
 def test_library_exports_every_declared_symbol(zs):
     declared = _declared_symbols()
-    assert len(declared) == 24
+    assert len(declared) == len(set(declared)) == len(zs.EXPORTED)
     for n in ("zseek_reader_open_full", "zseek_pread", "zseek_writer_close",
               "zsk_lz4_decode_frames"):
         assert n in declared
@@ -245,7 +245,7 @@ def test_library_hides_internals(zs):
     out = subprocess.run(["nm", "-D", "--defined-only", zs.LIB_PATH], capture_output=True,
                          text=True).stdout
     funcs = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
-    assert funcs - set(zs.EXPORTED) - {"zsk_dev_lz4_decode_variant"} == set()
+    assert funcs == set(zs.EXPORTED)
 
 
 def test_null_handles(zs):
