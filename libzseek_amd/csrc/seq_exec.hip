@@ -148,18 +148,24 @@ __device__ unsigned long long g_xstats[12];   // DIAG 16: cycles per section, co
 // source and destination advancing together, a match piece's kind turning
 // from HBM to stage once its source reaches `flushed`; then the wave's pieces
 // are dealt one per lane per slot, four slots' flat 16-byte loads in flight
-// before any write.  A short literal piece near the end of the literal source
-// (the frame's last literals: 16 bytes from their start would pass the
-// frame's end mark, and the last frame's past the caller's buffer) is loaded
-// through the range-checked resource `lsp` instead, whose bytes past llen
-// read as zero.
+// before any write.  A literal run under 16 bytes whose 16-byte piece would
+// pass the end of the literal source (the frame's last literals: 16 bytes
+// from their start can pass the frame's end mark, and the last frame's the
+// end of the caller's buffer) is copied by its lane first, through the
+// range-checked resource `lsp` (bytes past llen read as zero), and gets no
+// descriptor.
 template <int DIAG>
 __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase, const Span &lsp,
                                            uint32_t llen, const uint8_t *obase, uint32_t descs,
                                            uint32_t flushed, uint32_t lane, uint32_t src, uint32_t op,
                                            uint32_t lit, uint32_t msrc, uint32_t mb, uint32_t mn)
 {
-    const uint32_t lpn = npieces(lit), np = lpn + npieces(mn);
+    const bool ltail = lit != 0 && lit < 16 && src + 16 > llen;
+    if (__ballot(ltail)) {
+        if (ltail)
+            lds_put(saddr(S, op), bload16(lsp.r, lsp.s0 + src), lit);
+    }
+    const uint32_t lpn = ltail ? 0 : npieces(lit), np = lpn + npieces(mn);
     const uint32_t inc = wave_incl_add(np);
     const uint32_t T = lane_val(inc, 63);
     if (T == 0)
@@ -184,7 +190,6 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
     for (uint32_t t0 = 0; t0 < T; t0 += 256) {
         u32x4 v[4];
         uint32_t dw[4], sx[4];
-        bool tail[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t t = t0 + 64 * j + lane;
@@ -193,11 +198,8 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
             sx[j] = (uint32_t)D;
             dw[j] = on ? (uint32_t)(D >> 32) : 0;
             const uint32_t kind = dw[j] >> 24;
-            tail[j] = on && kind == K_LIT && sx[j] + 16 > llen;
-            const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT && !tail[j] ? sx[j] : 0);
+            const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);
             v[j] = (DIAG & 1) ? (u32x4){0, 0, 0, 0} : *reinterpret_cast<const u32x4_l *>(p);
-            if (__ballot(tail[j]))
-                v[j] = tail[j] ? bload16(lsp.r, lsp.s0 + sx[j]) : v[j];
             if (t0 + 64 * j + 64 >= T)
                 break;
         }
@@ -372,7 +374,7 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // grid with next-frame prefetch; nontemporal item / literal loads; 1, 2, 5 or
 // 8 waves per workgroup instead of kXW = 4.
 template <int DIAG, uint32_t OUTB>
-__global__ __launch_bounds__(64 * kXW) void seq_exec_kernel(
+__global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,

@@ -13,11 +13,26 @@
 //                           and carries its content size, :463-518).
 //   zsk_tool_zstd_seekable  same for zstd (ZSTD_compress2, level/strategy as
 //                           compress.c:58-91, single worker).
+//   zsk_tool_open_mem       a reader over an in-memory image with a C pread
+//   zsk_tool_close_mem      callback (memcpy), opened through the
+//                           zseek_reader_open_full / close of EITHER library
+//                           (ours, or the reference build in oracle/_ref):
+//                           both share the zseek.h ABI, so the same callback
+//                           and the same timing loop serve both sides.
+//   zsk_tool_latency        per-request wall time of `count`-byte reads at
+//                           given offsets (a request loops on short reads, as
+//                           test/example.c:63-80 does).
+//   zsk_tool_read_all       wall time of reading [0, size) with one call
+//                           (looping on short reads).
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/types.h>
+#include <time.h>
 
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -199,4 +214,111 @@ ZSK_TOOL int zsk_tool_zstd_seekable(const uint8_t *in, size_t n, size_t frame_si
                         size_t c = ZSTD_compress2(cctx, dst, cap, src, len);
                         return ZSTD_isError(c) ? 0 : c;
                     });
+}
+
+// ---- in-memory readers and timing loops (bench.py latency / end-to-end) ----
+namespace {
+struct MemFile {
+    const uint8_t *p;
+    size_t n;
+};
+struct ReadFile {   // zseek_read_file_t (zseek.h:109-116)
+    void *user_data;
+    ssize_t (*pread)(void *, size_t, size_t, void *, void *);
+    ssize_t (*fsize)(void *, void *);
+};
+typedef void *(*open_full_t)(ReadFile, size_t, void *, char *);
+typedef bool (*close_t)(void *, void *, char *);
+typedef ssize_t (*pread_t)(void *, void *, size_t, size_t, void *, char *);
+
+ssize_t mem_pread(void *data, size_t size, size_t offset, void *user_data, void *)
+{
+    const MemFile *f = (const MemFile *)user_data;
+    if (offset >= f->n)
+        return 0;
+    size_t k = f->n - offset < size ? f->n - offset : size;
+    memcpy(data, f->p + offset, k);
+    return (ssize_t)k;
+}
+
+ssize_t mem_fsize(void *user_data, void *)
+{
+    return (ssize_t)((const MemFile *)user_data)->n;
+}
+
+std::mutex g_mem_mu;
+std::map<void *, MemFile *> g_mem;
+
+double now_s()
+{
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+}   // namespace
+
+ZSK_TOOL void *zsk_tool_open_mem(void *open_full, const uint8_t *img, size_t n, size_t cache_size,
+                                 char *errbuf)
+{
+    MemFile *f = new MemFile{img, n};
+    void *r = ((open_full_t)open_full)(ReadFile{f, mem_pread, mem_fsize}, cache_size, nullptr, errbuf);
+    if (!r) {
+        delete f;
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    g_mem[r] = f;
+    return r;
+}
+
+ZSK_TOOL bool zsk_tool_close_mem(void *close_fn, void *reader)
+{
+    bool ok = ((close_t)close_fn)(reader, nullptr, nullptr);
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    auto it = g_mem.find(reader);
+    if (it != g_mem.end()) {
+        delete it->second;
+        g_mem.erase(it);
+    }
+    return ok;
+}
+
+// ns_out[i] = wall time of request i; returns 0, or -1 at the first failing
+// request (its index in *failed)
+ZSK_TOOL int zsk_tool_latency(void *pread_fn, void *reader, const uint64_t *offs, size_t n,
+                              size_t count, uint8_t *buf, uint64_t *ns_out, size_t *failed)
+{
+    pread_t pr = (pread_t)pread_fn;
+    for (size_t i = 0; i < n; i++) {
+        const double t0 = now_s();
+        size_t done = 0;
+        while (done < count) {
+            ssize_t r = pr(reader, buf + done, count - done, offs[i] + done, nullptr, nullptr);
+            if (r < 0) {
+                *failed = i;
+                return -1;
+            }
+            if (r == 0)
+                break;
+            done += (size_t)r;
+        }
+        ns_out[i] = (uint64_t)((now_s() - t0) * 1e9);
+    }
+    return 0;
+}
+
+ZSK_TOOL double zsk_tool_read_all(void *pread_fn, void *reader, uint8_t *buf, size_t size,
+                                  size_t *got)
+{
+    pread_t pr = (pread_t)pread_fn;
+    const double t0 = now_s();
+    size_t done = 0;
+    while (done < size) {
+        ssize_t r = pr(reader, buf + done, size - done, done, nullptr, nullptr);
+        if (r <= 0)
+            break;
+        done += (size_t)r;
+    }
+    *got = done;
+    return now_s() - t0;
 }
