@@ -47,15 +47,22 @@ def all_gatherv(dist, slab, counts: list[int], out=None, group=None):
     """Every rank receives every rank's slab, concatenated rank-major.
 
     `slab` is this rank's 1-D uint8 tensor (len == counts[rank]); `out` (len
-    == sum(counts)) receives the result.  Implemented as one broadcast per
-    source rank issued together (RCCL groups them), so each link carries each
-    slab once.
+    == sum(counts)) receives the result.  Equal slabs: the collective
+    all-gather (RCCL's ring over xGMI); ragged slabs: one broadcast per source
+    rank issued together (RCCL groups them), so each link carries each slab
+    once.
     """
     import torch
     rank = dist.get_rank(group)
     total = sum(counts)
     if out is None:
         out = torch.empty(total, dtype=slab.dtype, device=slab.device)
+    if len(set(counts)) == 1 and hasattr(dist, "all_gather_into_tensor"):
+        try:
+            dist.all_gather_into_tensor(out, slab[: counts[rank]], group=group)
+            return out
+        except (RuntimeError, NotImplementedError):
+            pass   # a backend without it (older gloo): the broadcasts below
     starts = np.concatenate([[0], np.cumsum(counts)])
     out[starts[rank]: starts[rank + 1]].copy_(slab[: counts[rank]])
     reqs = []
@@ -72,8 +79,9 @@ def all_gatherv(dist, slab, counts: list[int], out=None, group=None):
 def to_frame_order(gathered, shards: list[Shard], d_off: np.ndarray):
     """Permute a rank-major gather back to frame order (round_robin plans).
 
-    Uniform frames use one strided view; ragged frames fall back to a
-    per-frame index copy.
+    Uniform frames use one strided view (a device transpose); ragged frames
+    one vectorised gather: a byte index built from per-frame (source,
+    destination, length) triples with repeat_interleave — no per-frame loop.
     """
     import torch
     sizes = np.diff(d_off.astype(np.int64))
@@ -82,11 +90,14 @@ def to_frame_order(gathered, shards: list[Shard], d_off: np.ndarray):
     if n and (sizes[:-1] == sizes[0]).all() and n % world == 0 and sizes[-1] == sizes[0]:
         fs = int(sizes[0])
         return gathered.view(world, n // world, fs).transpose(0, 1).reshape(-1)
+    order = np.concatenate([s.frames for s in shards]).astype(np.int64)   # gathered frame order
+    lens = sizes[order]
+    src = np.concatenate([[0], np.cumsum(lens)[:-1]])                     # offset in gathered
+    dst = d_off[:-1].astype(np.int64)[order]                               # offset in frame order
+    dev = gathered.device
+    lens_t = torch.from_numpy(lens).to(dev)
+    base = torch.repeat_interleave(torch.from_numpy(dst - src).to(dev), lens_t)
+    idx = torch.arange(gathered.numel(), device=dev) + base                # destination of each byte
     out = torch.empty_like(gathered)
-    pos = 0
-    for s in shards:
-        for i in s.frames:
-            a, b = int(d_off[i]), int(d_off[i + 1])
-            out[a:b].copy_(gathered[pos: pos + (b - a)])
-            pos += b - a
+    out[idx] = gathered
     return out

@@ -190,6 +190,16 @@ def tools() -> C.CDLL:
     T.zsk_tool_zstd_seekable.restype = C.c_int
     T.zsk_tool_zstd_seekable.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
                                          C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    T.zsk_tool_open_mem.restype = C.c_void_p
+    T.zsk_tool_open_mem.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_char_p]
+    T.zsk_tool_close_mem.restype = C.c_bool
+    T.zsk_tool_close_mem.argtypes = [C.c_void_p, C.c_void_p]
+    T.zsk_tool_latency.restype = C.c_int
+    T.zsk_tool_latency.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t,
+                                   C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t)]
+    T.zsk_tool_read_all.restype = C.c_double
+    T.zsk_tool_read_all.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                    C.POINTER(C.c_size_t)]
     _tools = T
     return T
 

@@ -79,3 +79,32 @@ def test_plan_covers_every_frame_once():
             allf = np.sort(np.concatenate([s.frames for s in shards]))
             assert (allf == np.arange(1000)).all()
             assert sum(s.out_bytes for s in shards) == 1000 * 65536
+
+
+@pytest.mark.parametrize("partition", ["contiguous", "round_robin"])
+def test_bench_spawns_ranks_harness(partition):
+    """`python bench.py --gpus 2` with no torchrun environment starts two rank
+    processes itself (torch.distributed.run child; gloo rehearsal, no GPU),
+    builds each rank's shard of a fixed total from replicated frames, gathers
+    the full range on every rank and prints one JSON line with n_gpus 2 —
+    the code path the driver's multi-GPU run takes (config 4), minus the
+    decode."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--harness-check", "--total-size", "8M", "--size", "4M", "--steps", "2",
+                        "--warmup", "1", "--partition", partition],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["decoded_bytes_total"] == 8 << 20
+    assert d["config"]["frames_per_gpu"] == 64
+    assert d["verified_bit_exact"] is True
+    assert d["reassembly"]["full_range_matches_generator"] is True
+    assert (d["reassembly"]["permute_s"] is not None) == (partition == "round_robin")
