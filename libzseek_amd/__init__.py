@@ -6,7 +6,8 @@ mirror (``libzseek_amd.zseek``) used by tests and bench.py.
 """
 from .zseek import (  # noqa: F401
     ZSEEK_LZ4, ZSEEK_ZSTD, FRAME_DESC_DTYPE, LibraryNotBuilt, Reader, Writer, ZseekError,
-    decode_frames, frame_batch, kernel_times, kernel_timing, lib, lz4_seekable, seek_table_of, status_string,
+    decode_frames, frame_batch, kernel_times, kernel_timing, lib, lz4_seekable, parse_kernel_name,
+    seek_table_of, status_string,
     synth_buffer, tools, verify_frame_checksums, with_frame_checksums, zstd_decode_frames,
     zstd_seekable,
 )
