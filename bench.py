@@ -650,22 +650,27 @@ def cpu_baseline(img, size, frame, host, zstd, with_latency):
     usable = host["usable"]
     one = min(size, 1 << 30)
     s1, b1 = rb.run(img, 1, 0, one, frame, frame, 0)
-    best = 0.0
-    for _ in range(3):
-        secs, nbytes = rb.run(img, usable, 0, size, frame, frame, 0)
-        best = max(best, nbytes / secs / 1e9)
-    res = {"value": round(best, 2), "unit": "GB/s", "cores": usable, "kind": "reference",
+
+    def best_of(threads, reps=3):
+        best = 0.0
+        for _ in range(reps):
+            secs, nbytes = rb.run(img, threads, 0, size, frame, frame, 0)
+            best = max(best, nbytes / secs / 1e9)
+        return best
+
+    runs = {usable: best_of(usable)}
+    if host["visible"] > usable:   # every visible CPU too (the cgroup quota may throttle it)
+        runs[host["visible"]] = best_of(host["visible"])
+    cores = max(runs, key=runs.get)
+    res = {"value": round(runs[cores], 2), "unit": "GB/s", "cores": cores, "kind": "reference",
            "one_thread_GBps": round(b1 / s1 / 1e9, 2),
-           "sample": (f"{'zstd' if zstd else 'LZ4'}: the whole {size >> 20} MiB image decoded by "
-                      f"{usable} reference readers (cache_size=0, {frame >> 10} KiB zseek_pread "
-                      f"calls), best of 3; 1 reader on the first {one >> 20} MiB; host "
-                      f"{host['model']}, {host['visible']} CPUs visible, affinity {host['affinity']}, "
-                      f"cgroup quota {host['cgroup_quota']}")}
-    if host["visible"] > usable:
-        secs, nbytes = rb.run(img, host["visible"], 0, size, frame, frame, 0)
-        res["all_visible_threads"] = {"threads": host["visible"],
-                                      "GBps": round(nbytes / secs / 1e9, 2),
-                                      "note": "throttled by the cgroup quota"}
+           "by_threads": {str(t): round(v, 2) for t, v in sorted(runs.items())},
+           "sample": (f"{'zstd' if zstd else 'LZ4'}: the whole {size >> 20} MiB image decoded by T "
+                      f"reference readers (cache_size=0, {frame >> 10} KiB zseek_pread calls), best of "
+                      f"3, T = {' and '.join(str(t) for t in sorted(runs))} (value: the faster); 1 "
+                      f"reader on the first {one >> 20} MiB; host {host['model']}, {host['visible']} "
+                      f"CPUs visible, affinity {host['affinity']}, cgroup CPU quota "
+                      f"{host['cgroup_quota']}")}
     if with_latency:
         import ctypes as C
         import libzseek_amd as z
