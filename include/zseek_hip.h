@@ -99,9 +99,9 @@ ZSEEK_EXPORT int zsk_lz4_decode_frames_ex(const zsk_frame_desc_t *d_desc,
 
 /* Name of the dominant HIP kernel zsk_lz4_decode_frames launches for a
  * batch of nframes frames (as it appears in a rocprofv3 kernel trace,
- * without namespace), for tooling: batches of 64 frames and more use the
- * two-phase decoder (its execute, seq_exec_kernel), smaller ones the
- * wave-per-frame decoder (env ZSEEK_HIP_KERNEL=split|wave overrides). */
+ * without namespace), for tooling: the two-phase decoder's execute,
+ * seq_exec_kernel, unless the environment forces the
+ * wave-per-frame decoder (env ZSEEK_HIP_KERNEL=wave forces it). */
 ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes);
 
 /* Name of the parse kernel the two-phase decoder runs for a frame of
@@ -150,8 +150,11 @@ typedef struct {
 ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader,
     zsk_gpu_stats_t *stats);
 
-/* Largest decoded span one batch grid covers (bytes, default 256 MiB;
- * env ZSEEK_HIP_BATCH_BYTES overrides at open). */
+/* Largest decoded span one batch grid covers (bytes, default 64 MiB; env
+ * ZSEEK_HIP_BATCH_BYTES overrides at open).  A read runs as a pipeline of
+ * such batches (the user pread of one, the upload / decode / download of
+ * the next and the copy into the caller's buffer of a third overlap); its
+ * first batch is at most 4 MiB. */
 ZSEEK_EXPORT bool zsk_reader_set_batch_bytes(zseek_reader_t *reader,
     size_t bytes);
 
@@ -178,6 +181,23 @@ ZSEEK_EXPORT int zsk_verify_frame_checksums(const zsk_frame_desc_t *d_desc,
  * mismatch".  false for a NULL reader. */
 ZSEEK_EXPORT bool zsk_reader_set_verify_checksums(zseek_reader_t *reader,
     bool on);
+
+/*
+ * The devices a reader decodes on: one decode pipeline ("lane") per entry; a
+ * multi-frame read is split into contiguous frame ranges by decoded bytes,
+ * one per lane, decoded concurrently (host destinations: each lane copies its
+ * part into the caller's buffer; zsk_pread_device: each lane copies its part
+ * into the destination, peer-to-peer from another device).  A device may
+ * repeat (several pipelines on one GPU).  Default: env ZSEEK_HIP_DEVICES
+ * ("0,1,2,3") at the first read, else ZSEEK_HIP_DEVICE, else the calling
+ * thread's current device.  false for a NULL reader or an invalid device.
+ * zsk_reader_devices writes up to @cap entries and returns the count (0
+ * before the first read has picked the default).
+ */
+ZSEEK_EXPORT bool zsk_reader_set_devices(zseek_reader_t *reader,
+    const int *devices, int n);
+ZSEEK_EXPORT int zsk_reader_devices(zseek_reader_t *reader, int *devices,
+    int cap);
 
 #ifdef __cplusplus
 }

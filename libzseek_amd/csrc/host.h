@@ -6,6 +6,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <list>
 #include <unordered_map>
 #include <vector>
@@ -89,45 +90,78 @@ struct DeviceGuard {
     DeviceGuard &operator=(const DeviceGuard &) = delete;
 };
 
-// Per-reader GPU context: one stream, device buffers and pinned staging
-// grown geometrically, created lazily at the first decode.
-struct DeviceCtx {
-    int device = -1;
+// Host copies on a small process-wide worker pool (bounce buffer -> the
+// caller's memory while the next batches read, upload and decode).  A ticket
+// counts a batch's outstanding pieces.
+struct CopyTicket {
+    std::atomic<int> left{0};
+};
+void pool_copy(void *dst, const void *src, size_t n, CopyTicket *t);
+void pool_wait(CopyTicket *t);
+
+// One batch of frames in flight: its own stream, pinned staging and device
+// buffers (grown geometrically, kept across calls), decoder scratch.
+struct Slot {
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;   // recorded after the batch's last command
+    uint8_t *h_comp = nullptr;   // pinned: the batch's compressed span (user pread target)
+    size_t h_comp_cap = 0;
+    FrameDesc *h_desc = nullptr;   // pinned
+    size_t h_desc_cap = 0;
+    int32_t *h_status = nullptr;   // pinned, per frame
+    size_t h_status_cap = 0;
+    uint32_t *h_fail = nullptr;    // pinned, per frame: output offset of a failure
+    size_t h_fail_cap = 0;
+    uint32_t *h_ck = nullptr;      // pinned: the batch's seek-table checksums
+    size_t h_ck_cap = 0;
+    uint8_t *h_out = nullptr;      // pinned bounce of decoded bytes (host destinations)
+    size_t h_out_cap = 0;
     uint8_t *d_comp = nullptr;
     size_t d_comp_cap = 0;
     uint8_t *d_out = nullptr;
     size_t d_out_cap = 0;
     FrameDesc *d_desc = nullptr;
-    size_t d_desc_cap = 0;   // frames
+    size_t d_desc_cap = 0;
     int32_t *d_status = nullptr;
     size_t d_status_cap = 0;
-    uint8_t *h_comp = nullptr;   // pinned
-    size_t h_comp_cap = 0;
-    FrameDesc *h_desc = nullptr;   // pinned
-    size_t h_desc_cap = 0;
-    int32_t *h_status = nullptr;   // pinned
-    size_t h_status_cap = 0;
-    uint32_t *d_fail = nullptr;    // per-frame output offset of a failure
+    uint32_t *d_fail = nullptr;
     size_t d_fail_cap = 0;
-    uint32_t *h_fail = nullptr;
-    size_t h_fail_cap = 0;
-    uint32_t *d_ck = nullptr;     // the batch's seek-table checksums (verification on)
+    uint32_t *d_ck = nullptr;
     size_t d_ck_cap = 0;
-    SplitScratch split;            // two-phase decoder scratch (lz4_split.hip)
-    ZstdScratch zs;                // zstd decoder scratch (zstd_decode.hip)
+    SplitScratch split;   // two-phase LZ4 decoder scratch (lz4_split.hip)
+    ZstdScratch zs;       // zstd decoder scratch (zstd_decode.hip)
+    // the batch in flight
+    size_t f0 = 0, f1 = 0;
+    uint64_t h_from = 0, h_len = 0;   // batch-span bytes copied into h_out
+    CopyTicket copies;                // h_out -> caller, still running
+
+    bool reserve(size_t comp, size_t out, size_t host_out, size_t nframes, bool ck, char *errbuf);
+    void destroy();
+    size_t device_bytes() const;
+    size_t host_bytes() const;
+};
+
+// A reader's context on one device (a "lane"): kSlots batches in flight,
+// created lazily at the first decode on that device.
+constexpr int kSlots = 3;
+struct DeviceCtx {
+    int device = -1;
+    Slot slot[kSlots];
     uint64_t batches = 0, frames_decoded = 0, bytes_decoded = 0, bytes_uploaded = 0;
 
+    DeviceCtx() = default;
+    DeviceCtx(const DeviceCtx &) = delete;
+    DeviceCtx &operator=(const DeviceCtx &) = delete;
     ~DeviceCtx();
-    bool init(char *errbuf);
-    bool reserve(size_t comp, size_t out, size_t nframes, char *errbuf);
-    size_t device_bytes() const
-    {
-        return d_comp_cap + d_out_cap + d_desc_cap * 28 + split.frames_cap * 12 + split.items_cap * 8 +
-               zs.frames_cap * 24 + zs.lit_cap + zs.items_cap * 8;
-    }
-    size_t host_bytes() const { return h_comp_cap + h_desc_cap * 28; }
+    bool init(int dev, char *errbuf);
+    size_t device_bytes() const;
+    size_t host_bytes() const;
 };
+
+// The devices a reader decodes on: env ZSEEK_HIP_DEVICES ("0,1,2,3"; a
+// device may repeat), else ZSEEK_HIP_DEVICE, else the caller's current
+// device.  Empty when no HIP device exists.
+std::vector<int> default_devices();
 
 }   // namespace zsk
 

@@ -6,6 +6,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+
 #include <hip/hip_runtime_api.h>
 
 #include "host.h"
@@ -186,60 +191,99 @@ size_t FrameCache::memory_usage() const
 }
 
 // ---------------------------------------------------------------------------
-// GPU context
+// copy pool: host memcpy on worker threads (process lifetime, never joined)
 // ---------------------------------------------------------------------------
-DeviceCtx::~DeviceCtx()
+namespace {
+constexpr size_t kCopyPiece = 4u << 20;    // bytes per task
+constexpr size_t kCopyInline = 1u << 20;   // smaller copies run on the caller's thread
+
+struct CopyTask {
+    void *dst;
+    const void *src;
+    size_t n;
+    CopyTicket *t;
+};
+
+class CopyPool {
+  public:
+    CopyPool()
+    {
+        unsigned hw = std::thread::hardware_concurrency();
+        int n = hw >= 32 ? 8 : hw >= 8 ? 4 : 2;
+        const char *env = getenv("ZSEEK_COPY_THREADS");
+        if (env && *env && atoi(env) > 0)
+            n = atoi(env);
+        for (int i = 0; i < n; i++)
+            std::thread([this] { work(); }).detach();
+    }
+    void put(const CopyTask &t)
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(t);
+        }
+        cv_.notify_one();
+    }
+    void wait(CopyTicket *t)
+    {
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [t] { return t->left.load() == 0; });
+    }
+
+  private:
+    void work()
+    {
+        for (;;) {
+            CopyTask t;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [this] { return !q_.empty(); });
+                t = q_.front();
+                q_.pop_front();
+            }
+            memcpy(t.dst, t.src, t.n);
+            if (t.t->left.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> g(mu_);
+                done_.notify_all();
+            }
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::deque<CopyTask> q_;
+};
+
+CopyPool &copy_pool()
 {
-    if (device < 0)
+    static CopyPool *p = new CopyPool();   // never destroyed: its threads outlive exit
+    return *p;
+}
+}   // namespace
+
+void pool_copy(void *dst, const void *src, size_t n, CopyTicket *t)
+{
+    if (n <= kCopyInline) {
+        memcpy(dst, src, n);
         return;
-    DeviceGuard keep;
-    (void)hipSetDevice(device);
-    if (stream)
-        (void)hipStreamSynchronize(stream);
-    (void)hipFree(d_comp);
-    (void)hipFree(d_out);
-    (void)hipFree(d_desc);
-    (void)hipFree(d_status);
-    (void)hipFree(d_fail);
-    (void)hipFree(d_ck);
-    split_scratch_free(&split);
-    zstd_scratch_free(&zs);
-    (void)hipHostFree(h_fail);
-    (void)hipHostFree(h_comp);
-    (void)hipHostFree(h_desc);
-    (void)hipHostFree(h_status);
-    if (stream)
-        (void)hipStreamDestroy(stream);
+    }
+    CopyPool &p = copy_pool();
+    const size_t pieces = (n + kCopyPiece - 1) / kCopyPiece;
+    t->left.fetch_add((int)pieces);
+    for (size_t i = 0; i < pieces; i++) {
+        const size_t o = i * kCopyPiece;
+        p.put({(uint8_t *)dst + o, (const uint8_t *)src + o, n - o < kCopyPiece ? n - o : kCopyPiece, t});
+    }
 }
 
-bool DeviceCtx::init(char *errbuf)
+void pool_wait(CopyTicket *t)
 {
-    if (device >= 0)
-        return true;
-    int dev = 0;
-    const char *env = getenv("ZSEEK_HIP_DEVICE");
-    if (env && *env) {
-        dev = atoi(env);
-    } else if (hipGetDevice(&dev) != hipSuccess) {
-        dev = 0;
-    }
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
-        set_error(errbuf, "no HIP device available");
-        return false;
-    }
-    if (dev < 0 || dev >= count || hipSetDevice(dev) != hipSuccess) {
-        set_error(errbuf, "invalid HIP device %d", dev);
-        return false;
-    }
-    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
-        set_error(errbuf, "create HIP stream failed");
-        return false;
-    }
-    device = dev;
-    return true;
+    if (t->left.load() != 0)
+        copy_pool().wait(t);
 }
 
+// ---------------------------------------------------------------------------
+// GPU context: a lane of kSlots batch slots on one device
+// ---------------------------------------------------------------------------
 namespace {
 template <typename T>
 bool grow_dev(T **p, size_t *cap, size_t want_elems)
@@ -273,22 +317,154 @@ bool grow_host(T **p, size_t *cap, size_t want_elems)
 }
 }   // namespace
 
-bool DeviceCtx::reserve(size_t comp, size_t out, size_t nframes, char *errbuf)
+bool Slot::reserve(size_t comp, size_t out, size_t host_out, size_t nframes, bool ck, char *errbuf)
 {
-    (void)hipSetDevice(device);
     if (!grow_dev(&d_comp, &d_comp_cap, comp) || !grow_dev(&d_out, &d_out_cap, out) ||
-        !grow_dev(&d_desc, &d_desc_cap, nframes) ||
-        !grow_dev(&d_status, &d_status_cap, nframes) || !grow_dev(&d_fail, &d_fail_cap, nframes) ||
-        !grow_dev(&d_ck, &d_ck_cap, nframes)) {
+        !grow_dev(&d_desc, &d_desc_cap, nframes) || !grow_dev(&d_status, &d_status_cap, nframes) ||
+        !grow_dev(&d_fail, &d_fail_cap, nframes) || (ck && !grow_dev(&d_ck, &d_ck_cap, nframes))) {
         set_error(errbuf, "allocate GPU decode buffers failed");
         return false;
     }
     if (!grow_host(&h_comp, &h_comp_cap, comp) || !grow_host(&h_desc, &h_desc_cap, nframes) ||
-        !grow_host(&h_status, &h_status_cap, nframes) || !grow_host(&h_fail, &h_fail_cap, nframes)) {
+        !grow_host(&h_status, &h_status_cap, nframes) || !grow_host(&h_fail, &h_fail_cap, nframes) ||
+        (ck && !grow_host(&h_ck, &h_ck_cap, nframes)) ||
+        (host_out && !grow_host(&h_out, &h_out_cap, host_out))) {
         set_error(errbuf, "allocate pinned staging failed");
         return false;
     }
     return true;
+}
+
+// Teardown order: the slot's stream drained (its copies too), then the zstd
+// scratch (which drains and destroys its side stream before its events: the
+// side stream's wait on this stream's event goes while this stream is
+// alive), then memory, then this stream's event and the stream itself.
+void Slot::destroy()
+{
+    if (!stream)
+        return;
+    (void)hipStreamSynchronize(stream);
+    pool_wait(&copies);
+    zstd_scratch_free(&zs);
+    split_scratch_free(&split);
+    for (void *p : {(void *)d_comp, (void *)d_out, (void *)d_desc, (void *)d_status, (void *)d_fail,
+                    (void *)d_ck})
+        if (p)
+            (void)hipFree(p);
+    for (void *p : {(void *)h_comp, (void *)h_desc, (void *)h_status, (void *)h_fail, (void *)h_ck,
+                    (void *)h_out})
+        if (p)
+            (void)hipHostFree(p);
+    if (done)
+        (void)hipEventDestroy(done);
+    (void)hipStreamDestroy(stream);
+    stream = nullptr;
+    done = nullptr;
+    h_comp = h_out = nullptr;
+    h_desc = nullptr;
+    h_status = nullptr;
+    h_fail = h_ck = nullptr;
+    d_comp = d_out = nullptr;
+    d_desc = nullptr;
+    d_status = nullptr;
+    d_fail = d_ck = nullptr;
+    h_comp_cap = h_desc_cap = h_status_cap = h_fail_cap = h_ck_cap = h_out_cap = 0;
+    d_comp_cap = d_out_cap = d_desc_cap = d_status_cap = d_fail_cap = d_ck_cap = 0;
+}
+
+size_t Slot::device_bytes() const
+{
+    return d_comp_cap + d_out_cap + d_desc_cap * sizeof(FrameDesc) + (d_status_cap + d_fail_cap + d_ck_cap) * 4 +
+           split.frames_cap * 12 + split.items_cap * 8 + zs.frames_cap * 24 + zs.lit_cap + zs.items_cap * 8;
+}
+
+size_t Slot::host_bytes() const
+{
+    return h_comp_cap + h_out_cap + h_desc_cap * sizeof(FrameDesc) + (h_status_cap + h_fail_cap + h_ck_cap) * 4;
+}
+
+DeviceCtx::~DeviceCtx()
+{
+    if (device < 0)
+        return;
+    DeviceGuard keep;
+    (void)hipSetDevice(device);
+    for (Slot &s : slot)
+        s.destroy();
+}
+
+bool DeviceCtx::init(int dev, char *errbuf)
+{
+    if (device >= 0)
+        return true;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error(errbuf, "no HIP device available");
+        return false;
+    }
+    if (dev < 0 || dev >= count || hipSetDevice(dev) != hipSuccess) {
+        set_error(errbuf, "invalid HIP device %d", dev);
+        return false;
+    }
+    for (Slot &s : slot) {
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+            set_error(errbuf, "create HIP stream failed");
+            for (Slot &t : slot)
+                t.destroy();
+            return false;
+        }
+    }
+    device = dev;
+    return true;
+}
+
+size_t DeviceCtx::device_bytes() const
+{
+    size_t n = 0;
+    for (const Slot &s : slot)
+        n += s.device_bytes();
+    return n;
+}
+
+size_t DeviceCtx::host_bytes() const
+{
+    size_t n = 0;
+    for (const Slot &s : slot)
+        n += s.host_bytes();
+    return n;
+}
+
+std::vector<int> default_devices()
+{
+    std::vector<int> out;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return out;
+    const char *list = getenv("ZSEEK_HIP_DEVICES");
+    if (list && *list) {
+        const char *p = list;
+        while (*p) {
+            char *e = nullptr;
+            long v = strtol(p, &e, 10);
+            if (e == p)
+                break;
+            out.push_back((int)v);
+            p = *e == ',' ? e + 1 : e;
+            if (*e != ',' )
+                break;
+        }
+        if (!out.empty())
+            return out;
+    }
+    int dev = 0;
+    const char *one = getenv("ZSEEK_HIP_DEVICE");
+    if (one && *one)
+        dev = atoi(one);
+    else if (hipGetDevice(&dev) != hipSuccess)
+        dev = 0;
+    out.push_back(dev);
+    return out;
 }
 
 // ---------------------------------------------------------------------------

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "lz4_dev.h"
+#include "pool.h"
 #include "zsk_internal.h"
 
 namespace zsk {
@@ -167,85 +168,6 @@ int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipS
         s->items_cap = cap;
     }
     return 0;
-}
-
-// ---- scratch for device-API calls: a bounded pool per device -----------------
-// Each set is reused in stream order: after a launch, its event is recorded on
-// the caller's stream; a later call (any stream) takes a set whose event has
-// completed, or a new set while the device has fewer than kPoolSets, or else
-// the least recently used set after making its stream wait on that event.
-// Nothing is keyed by stream, so a caller destroying its streams leaves no
-// stale entry, and the pool never grows past kPoolSets sets per device.
-namespace {
-struct PoolSet {
-    SplitScratch s;
-    hipEvent_t done = nullptr;
-    uint64_t last = 0;   // use counter at the last release (LRU)
-    bool busy = false;   // handed out, not yet released
-};
-struct DevicePool {
-    std::mutex mu;
-    std::vector<PoolSet *> sets;
-    uint64_t uses = 0;
-};
-std::mutex g_pools_mu;
-std::map<int, DevicePool *> g_pools;   // process lifetime; bounded per device
-
-DevicePool *device_pool()
-{
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> g(g_pools_mu);
-    DevicePool *&p = g_pools[dev];
-    if (!p)
-        p = new DevicePool();
-    return p;
-}
-}   // namespace
-
-SplitScratch *stream_scratch(hipStream_t stream)
-{
-    DevicePool *p = device_pool();
-    std::unique_lock<std::mutex> g(p->mu);
-    PoolSet *pick = nullptr;
-    for (PoolSet *x : p->sets)
-        if (!x->busy && hipEventQuery(x->done) == hipSuccess) {
-            pick = x;
-            break;
-        }
-    if (!pick && (int)p->sets.size() < kPoolSets) {
-        pick = new PoolSet();
-        if (hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {
-            delete pick;
-            return nullptr;
-        }
-        p->sets.push_back(pick);
-    }
-    if (!pick) {
-        // every set in use: the least recently released one, in stream order
-        for (PoolSet *x : p->sets)
-            if (!x->busy && (!pick || x->last < pick->last))
-                pick = x;
-        if (!pick)
-            return nullptr;   // kPoolSets concurrent calls on this device
-        if (hipStreamWaitEvent(stream, pick->done, 0) != hipSuccess)
-            return nullptr;
-    }
-    pick->busy = true;
-    return &pick->s;
-}
-
-void stream_scratch_done(SplitScratch *s, hipStream_t stream)
-{
-    DevicePool *p = device_pool();
-    std::lock_guard<std::mutex> g(p->mu);
-    for (PoolSet *x : p->sets)
-        if (&x->s == s) {
-            (void)hipEventRecord(x->done, stream);
-            x->last = ++p->uses;
-            x->busy = false;
-            return;
-        }
 }
 
 // ---- per-stage launch timing (zsk_kernel_timing / zsk_kernel_times) ----------
@@ -417,7 +339,8 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
         return 0;
     if (route == ROUTE_WAVE || (route == ROUTE_AUTO && lz4_pick_engine(nframes) == ENGINE_WAVE))
         return launch_lz4_wave(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
-    SplitScratch *s = stream_scratch(stream);
+    static ScratchPool<SplitScratch> pool;
+    SplitScratch *s = pool.acquire(stream);
     if (!s)
         return -1;
     // first call: room for 64 KiB frames (capped at 4 GiB of items); later
@@ -432,19 +355,20 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
         rc = launch_lz4_wave(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
     else
         rc = launch_lz4_split(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream, s, route, 15, tune);
-    stream_scratch_done(s, stream);
+    pool.release(s, stream);
     return rc;
 }
 
-// Automatic choice: the two-phase decoder (its parse per frame
-// size and batch size, chunk_parse_min) from 64 frames on; a handful of frames
-// go to the wave-per-frame kernel in one launch.
+// Automatic choice: the two-phase decoder for every batch
+// (its parse per frame size and batch size, chunk_parse_min: a single 64 KiB
+// frame takes the wave-parallel chunk parse); the wave-per-frame kernel
+// decodes only the frames the parse hands off.  Env ZSEEK_HIP_KERNEL=wave
+// forces the wave kernel for every frame.
 int lz4_pick_engine(uint32_t nframes)
 {
+    (void)nframes;
     const int e = lz4_engine();
-    if (e != ENGINE_AUTO)
-        return e;
-    return nframes >= 64 ? ENGINE_SPLIT : ENGINE_WAVE;
+    return e == ENGINE_WAVE ? ENGINE_WAVE : ENGINE_SPLIT;
 }
 
 uint32_t chunk_parse_min(uint32_t nframes)

@@ -14,6 +14,14 @@
 //   LZ4F_decompress / ZSTD_decompress*      HIP kernels over the batch (LZ4:
 //   on the CPU                              lz4_*.hip + seq_exec.hip; zstd:
 //                                           zstd_decode.hip + seq_exec.hip)
+//   serial                                  a pipeline of kSlots batches per
+//                                           device: the user pread of batch
+//                                           k+1, the upload / decode / download
+//                                           of batch k and the copy of batch
+//                                           k-1 into the caller's buffer overlap
+//   one decoder                             the range split over the reader's
+//                                           devices (ZSEEK_HIP_DEVICES), one
+//                                           pipeline ("lane") per device
 //   cache every decoded frame               cache the last cache_size frames of
 //                                           the request (same final LRU state
 //                                           as the reference's call loop)
@@ -28,35 +36,45 @@
 #include <string.h>
 #include <sys/stat.h>
 
+#include <algorithm>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
-#include <map>
 #include <new>
+#include <thread>
 #include <utility>
+#include <vector>
 
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/zseek_hip.h"
 #include "host.h"
+#include "pool.h"
 
 using namespace zsk;
 
 namespace {
 constexpr uint32_t kZstdMagic = 0xFD2FB528u;   // ref decompress.c:22
 constexpr uint32_t kLz4Magic = 0x184D2204u;    // ref decompress.c:23
-constexpr size_t kDefaultBatch = 256u << 20;
+constexpr size_t kDefaultBatch = 64u << 20;    // decoded bytes per batch
+constexpr size_t kFirstBatch = 4u << 20;       // the first batch of a request (latency)
+constexpr size_t kLaneMin = 1u << 20;          // decoded bytes per lane, at least
 }   // namespace
 
 struct zseek_reader {
     zseek_read_file_t user_file;
     zseek_compression_type_t type;
-    std::mutex lock;   // serialises decode + cache (ref uses a rwlock, :38)
+    std::mutex lock;      // serialises decode + cache (ref uses a rwlock, :38)
+    std::mutex io_lock;   // one user pread callback at a time (lanes run in threads)
     SeekTable st;
     FrameCache *cache = nullptr;   // NULL when cache_size == 0 (ref :219-227)
     std::mutex cursor_lock;        // zseek_read: cursor read, pread, advance as one step
     size_t pos = 0;                // zseek_read cursor (ref :826-835)
     size_t batch_bytes = kDefaultBatch;
     bool verify = false;   // check seek-table frame checksums (the reference never does)
-    DeviceCtx gpu;
+    std::vector<int> devices;                       // lane i decodes on devices[i]
+    std::vector<std::unique_ptr<DeviceCtx>> lanes;  // created at first use
 };
 
 // ---------------------------------------------------------------------------
@@ -162,122 +180,14 @@ extern "C" ZSEEK_EXPORT bool zseek_reader_close(zseek_reader_t *reader, void *ca
     if (!reader)
         return true;   // ref decompress.c:362-363
     delete reader->cache;
-    delete reader;
+    delete reader;     // lanes: streams drained, scratch and buffers freed
     return true;
 }
 
 // ---------------------------------------------------------------------------
-// GPU batch decode: frames [f0, f1) -> gpu.d_out (frame i at d_off[i]-d_off[f0])
+// error wording
 // ---------------------------------------------------------------------------
 namespace {
-
-struct BatchResult {
-    size_t first_bad;   // == f1 when every frame decoded
-    int32_t status;
-    uint32_t fail_at;   // output offset (within the frame) of the failure
-};
-
-bool read_span(zseek_reader *r, void *dst, size_t len, uint64_t off, void *call_data,
-               char *errbuf)
-{
-    ssize_t got = r->user_file.pread(dst, len, off, r->user_file.user_data, call_data);
-    if (got != (ssize_t)len) {
-        // ref decompress.c:735-741
-        set_error(errbuf, got >= 0 ? "unexpected EOF" : "read file failed");
-        return false;
-    }
-    return true;
-}
-
-bool gpu_decode(zseek_reader *r, size_t f0, size_t f1, void *call_data, char *errbuf,
-                BatchResult *res)
-{
-    DeviceCtx &g = r->gpu;
-    if (!g.init(errbuf))
-        return false;
-    const SeekTable &st = r->st;
-    const size_t n = f1 - f0;
-    const uint64_t c0 = st.c_off[f0], csz = st.c_off[f1] - c0;
-    const uint64_t d0 = st.d_off[f0], dsz = st.d_off[f1] - d0;
-    if (!g.reserve(csz, dsz, n, errbuf))
-        return false;
-    if (csz && !read_span(r, g.h_comp, csz, c0, call_data, errbuf))
-        return false;
-    for (size_t i = 0; i < n; i++) {
-        FrameDesc &d = g.h_desc[i];
-        d.c_off = st.c_off[f0 + i] - c0;
-        d.d_off = st.d_off[f0 + i] - d0;
-        d.c_size = (uint32_t)st.csize(f0 + i);
-        d.d_size = (uint32_t)st.dsize(f0 + i);
-    }
-    (void)hipSetDevice(g.device);
-    hipError_t e = hipSuccess;
-    if (csz)
-        e = hipMemcpyAsync(g.d_comp, g.h_comp, csz, hipMemcpyHostToDevice, g.stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(g.d_desc, g.h_desc, n * sizeof(FrameDesc), hipMemcpyHostToDevice,
-                           g.stream);
-    if (e == hipSuccess)
-        e = hipMemsetD32Async((hipDeviceptr_t)g.d_status, ST_NOT_RUN, n, g.stream);
-    if (r->type == ZSEEK_ZSTD) {
-        // zstd: plan + decode (zstd_decode.hip); a failure's output offset is
-        // its block's start (the frame's end for the end-of-frame checks)
-        if (e == hipSuccess)
-            e = hipMemsetD32Async((hipDeviceptr_t)g.d_fail, 0, n, g.stream);
-        if (e == hipSuccess && zstd_decode_frames(g.d_desc, (uint32_t)n, g.d_comp, g.d_out,
-                                                  g.d_status, &g.zs, g.stream, g.d_fail) != 0)
-            e = hipErrorLaunchFailure;
-    }
-    const int engine = r->type == ZSEEK_ZSTD ? -1 : lz4_pick_engine((uint32_t)n);
-    if (e == hipSuccess && engine == ENGINE_WAVE &&
-        launch_lz4_wave(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail, g.stream) != 0)
-        e = hipErrorLaunchFailure;
-    if (e == hipSuccess && engine == ENGINE_SPLIT &&
-        split_scratch_reserve(&g.split, (uint32_t)n, split_items_needed(g.h_desc, (uint32_t)n),
-                              g.stream) != 0)
-        e = hipErrorOutOfMemory;
-    if (e == hipSuccess && engine == ENGINE_SPLIT &&
-        launch_lz4_split(g.d_desc, (uint32_t)n, g.d_comp, g.d_out, g.d_status, g.d_fail,
-                         g.stream, &g.split) != 0)
-        e = hipErrorLaunchFailure;
-    // seek-table checksums (descriptor bit 7) when asked for: XXH64 low 32
-    // bits of every decoded frame, on the GPU (frame_check.hip)
-    if (e == hipSuccess && r->verify && st.checksum_flag) {
-        e = hipMemcpyAsync(g.d_ck, st.checksum.data() + f0, n * sizeof(uint32_t),
-                           hipMemcpyHostToDevice, g.stream);
-        if (e == hipSuccess &&
-            launch_frame_checksums(g.d_desc, (uint32_t)n, g.d_out, g.d_ck, g.d_status, g.stream) != 0)
-            e = hipErrorLaunchFailure;
-    }
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(g.h_status, g.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost,
-                           g.stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(g.h_fail, g.d_fail, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           g.stream);
-    if (e == hipSuccess)
-        e = hipStreamSynchronize(g.stream);
-    if (e != hipSuccess) {
-        set_error(errbuf, "GPU decode failed: %s", hipGetErrorString(e));
-        return false;
-    }
-    g.batches++;
-    g.frames_decoded += n;
-    g.bytes_decoded += dsz;
-    g.bytes_uploaded += csz;
-    res->first_bad = f1;
-    res->status = ST_OK;
-    res->fail_at = 0;
-    for (size_t i = 0; i < n; i++) {
-        if (g.h_status[i] != ST_OK) {
-            res->first_bad = f0 + i;
-            res->status = g.h_status[i];
-            res->fail_at = g.h_fail[i];
-            break;
-        }
-    }
-    return true;
-}
 
 // LZ4F_decompress (liblz4 1.9.3) as the reference's no-cache read drives it
 // (decompress.c:614-669): a block's data is decoded only once the request
@@ -330,12 +240,11 @@ bool zstd_partial_ok(int32_t st, uint64_t fail_at, uint64_t end_in_frame)
 // when the block was decoded straight into the destination (room >= max
 // block size) and ERROR_decompressionFailed when it went through its
 // temporary buffer; the room depends on which buffer the block landed in.
-void frame_error(zseek_reader *r, const BatchResult &br, size_t frame, size_t offset_in_frame,
+void frame_error(zseek_reader *r, int32_t st, uint32_t fail_at, size_t frame, size_t offset_in_frame,
                  size_t count, char *errbuf)
 {
-    const int32_t st = br.status;
     const uint64_t dsize = r->st.dsize(frame);
-    const uint64_t at = br.fail_at;
+    const uint64_t at = fail_at;
     const char *prefix;
     uint64_t room;
     if (r->cache) {
@@ -370,52 +279,301 @@ void frame_error(zseek_reader *r, const BatchResult &br, size_t frame, size_t of
     set_error(errbuf, "%s: %s", prefix, name);
 }
 
-bool copy_out(DeviceCtx &g, void *dst, uint64_t src_off, size_t len, bool device_dst,
-              char *errbuf)
+// ---------------------------------------------------------------------------
+// the batch pipeline of one lane (device)
+// ---------------------------------------------------------------------------
+struct CacheItem {
+    size_t frame;
+    uint8_t *data;   // malloc'd, owned until inserted
+    size_t len;
+};
+
+// One lane's share of a request: frames [fa, fb); bytes [offset, end) of the
+// decoded range go to buf at (x - offset).
+struct LaneJob {
+    zseek_reader *r = nullptr;
+    DeviceCtx *g = nullptr;
+    size_t fa = 0, fb = 0;
+    uint64_t offset = 0, end = 0;
+    uint8_t *buf = nullptr;
+    bool device_dst = false;
+    int dst_dev = -1;
+    void *call_data = nullptr;
+    size_t cache_cap = 0;   // keep the last cache_cap good frames' bytes
+    // results
+    bool io_failed = false;   // pread / HIP failure (err holds the text)
+    char err[ZSEEK_ERRBUF_SIZE] = {0};
+    size_t first_bad = SIZE_MAX;   // first failed frame, if any
+    int32_t status = ST_OK;
+    uint32_t fail_at = 0;
+    uint64_t good_end = 0;   // the lane's bytes before good_end are in buf
+    std::deque<CacheItem> cached;
+};
+
+void free_items(std::deque<CacheItem> &q)
 {
-    if (!len)
-        return true;
-    hipError_t e = hipMemcpyAsync(dst, g.d_out + src_off, len,
-                                  device_dst ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
-                                  g.stream);
-    if (e == hipSuccess)
-        e = hipStreamSynchronize(g.stream);
-    if (e != hipSuccess) {
-        set_error(errbuf, "copy decoded data failed: %s", hipGetErrorString(e));
+    for (CacheItem &c : q)
+        free(c.data);
+    q.clear();
+}
+
+size_t batch_end(const SeekTable &st, size_t f, size_t fb, size_t limit)
+{
+    size_t g = f + 1;
+    while (g < fb && st.d_off[g + 1] - st.d_off[f] <= limit)
+        g++;
+    return g;
+}
+
+// Read, upload, decode and queue the download of frames [f0, f1) on slot s.
+bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
+{
+    zseek_reader *r = J.r;
+    DeviceCtx &g = *J.g;
+    const SeekTable &st = r->st;
+    const size_t n = f1 - f0;
+    const uint64_t c0 = st.c_off[f0], csz = st.c_off[f1] - c0;
+    const uint64_t d0 = st.d_off[f0], dsz = st.d_off[f1] - d0;
+    // the decoded bytes the host needs: the request's part of the batch
+    // (host destination), and the frames the cache may keep (its last
+    // cache_cap frames)
+    const uint64_t lo = std::max<uint64_t>(J.offset, d0), hi = std::min<uint64_t>(J.end, st.d_off[f1]);
+    uint64_t h_lo = UINT64_MAX, h_hi = 0;
+    if (!J.device_dst && hi > lo) {
+        h_lo = lo;
+        h_hi = hi;
+    }
+    if (J.cache_cap) {
+        const size_t cf = f1 - std::min(n, J.cache_cap);
+        h_lo = std::min<uint64_t>(h_lo, st.d_off[cf]);
+        h_hi = std::max<uint64_t>(h_hi, st.d_off[f1]);
+    }
+    if (h_hi <= h_lo)
+        h_lo = h_hi = d0;
+    const bool ck = r->verify && st.checksum_flag;
+    (void)hipSetDevice(g.device);
+    if (!s.reserve(csz, dsz, h_hi - h_lo, n, ck, J.err)) {
+        J.io_failed = true;
         return false;
     }
+    if (csz) {
+        std::lock_guard<std::mutex> io(r->io_lock);
+        ssize_t got = r->user_file.pread(s.h_comp, csz, c0, r->user_file.user_data, J.call_data);
+        if (got != (ssize_t)csz) {
+            // ref decompress.c:735-741
+            set_error(J.err, got >= 0 ? "unexpected EOF" : "read file failed");
+            J.io_failed = true;
+            return false;
+        }
+    }
+    for (size_t i = 0; i < n; i++) {
+        FrameDesc &d = s.h_desc[i];
+        d.c_off = st.c_off[f0 + i] - c0;
+        d.d_off = st.d_off[f0 + i] - d0;
+        d.c_size = (uint32_t)st.csize(f0 + i);
+        d.d_size = (uint32_t)st.dsize(f0 + i);
+    }
+    s.f0 = f0;
+    s.f1 = f1;
+    s.h_from = h_lo - d0;
+    s.h_len = h_hi - h_lo;
+    hipError_t e = hipSuccess;
+    if (csz)
+        e = hipMemcpyAsync(s.d_comp, s.h_comp, csz, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(s.d_desc, s.h_desc, n * sizeof(FrameDesc), hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+        e = hipMemsetD32Async((hipDeviceptr_t)s.d_status, ST_NOT_RUN, n, s.stream);
+    if (e == hipSuccess)
+        e = hipMemsetD32Async((hipDeviceptr_t)s.d_fail, 0, n, s.stream);
+    if (e == hipSuccess && r->type == ZSEEK_ZSTD &&
+        zstd_decode_frames(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream,
+                           s.d_fail) != 0)
+        e = hipErrorLaunchFailure;
+    if (e == hipSuccess && r->type == ZSEEK_LZ4) {
+        if (lz4_pick_engine((uint32_t)n) == ENGINE_WAVE) {
+            if (launch_lz4_wave(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, s.d_fail, s.stream) != 0)
+                e = hipErrorLaunchFailure;
+        } else if (split_scratch_reserve(&s.split, (uint32_t)n, split_items_needed(s.h_desc, (uint32_t)n),
+                                         s.stream) != 0) {
+            e = hipErrorOutOfMemory;
+        } else if (launch_lz4_split(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, s.d_fail,
+                                    s.stream, &s.split) != 0) {
+            e = hipErrorLaunchFailure;
+        }
+    }
+    // seek-table checksums (descriptor bit 7) when asked for: XXH64 low 32
+    // bits of every decoded frame, on the GPU (frame_check.hip)
+    if (e == hipSuccess && ck) {
+        memcpy(s.h_ck, st.checksum.data() + f0, n * sizeof(uint32_t));
+        e = hipMemcpyAsync(s.d_ck, s.h_ck, n * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream);
+        if (e == hipSuccess &&
+            launch_frame_checksums(s.d_desc, (uint32_t)n, s.d_out, s.d_ck, s.d_status, s.stream) != 0)
+            e = hipErrorLaunchFailure;
+    }
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(s.h_status, s.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(s.h_fail, s.d_fail, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream);
+    // decoded bytes out: straight into a device destination (a peer copy from
+    // another lane's device), or into the slot's pinned bounce once the host
+    // copies of its previous batch are done
+    if (e == hipSuccess && J.device_dst && hi > lo) {
+        if (J.dst_dev == g.device)
+            e = hipMemcpyAsync(J.buf + (lo - J.offset), s.d_out + (lo - d0), hi - lo,
+                               hipMemcpyDeviceToDevice, s.stream);
+        else
+            e = hipMemcpyPeerAsync(J.buf + (lo - J.offset), J.dst_dev, s.d_out + (lo - d0), g.device,
+                                   hi - lo, s.stream);
+    }
+    if (e == hipSuccess && s.h_len) {
+        pool_wait(&s.copies);
+        e = hipMemcpyAsync(s.h_out, s.d_out + s.h_from, s.h_len, hipMemcpyDeviceToHost, s.stream);
+    }
+    if (e == hipSuccess)
+        e = hipEventRecord(s.done, s.stream);
+    if (e != hipSuccess) {
+        set_error(J.err, "GPU decode failed: %s", hipGetErrorString(e));
+        J.io_failed = true;
+        (void)hipStreamSynchronize(s.stream);
+        return false;
+    }
+    g.batches++;
+    g.frames_decoded += n;
+    g.bytes_decoded += dsz;
+    g.bytes_uploaded += csz;
     return true;
 }
 
-// Insert frames [a, b) of the current batch (batch starts at frame f0) into
-// the cache, MRU last.
-bool cache_frames(zseek_reader *r, size_t f0, size_t a, size_t b, char *errbuf)
+// Wait for slot s's batch; hand its bytes to the caller (host: pool copies
+// from the bounce) and its last good frames to the cache candidates.  false
+// when a frame of the batch failed (the lane stops there).
+bool finish(LaneJob &J, Slot &s)
 {
+    zseek_reader *r = J.r;
     const SeekTable &st = r->st;
-    for (size_t i = a; i < b; i++) {
-        size_t len = st.dsize(i);
-        uint8_t *p = (uint8_t *)malloc(len ? len : 1);
-        if (!p) {
-            set_error_errno(errbuf, "allocate decompressed buffer", errno);
-            return false;
+    hipError_t e = hipEventSynchronize(s.done);
+    if (e != hipSuccess) {
+        set_error(J.err, "GPU decode failed: %s", hipGetErrorString(e));
+        J.io_failed = true;
+        return false;
+    }
+    const size_t f0 = s.f0, f1 = s.f1, n = f1 - f0;
+    const uint64_t d0 = st.d_off[f0];
+    size_t bad = f1;
+    for (size_t i = 0; i < n; i++)
+        if (s.h_status[i] != ST_OK) {
+            bad = f0 + i;
+            break;
         }
-        if (!copy_out(r->gpu, p, st.d_off[i] - st.d_off[f0], len, false, errbuf)) {
-            free(p);
-            return false;
-        }
-        if (!r->cache->insert(i, p, len)) {
-            free(p);
-            set_error(errbuf, "frame caching failed");
-            return false;
+    uint64_t good_end = st.d_off[bad];
+    if (bad < f1) {
+        J.first_bad = bad;
+        J.status = s.h_status[bad - f0];
+        J.fail_at = s.h_fail[bad - f0];
+        // Without a cache the reference decodes a frame only as far as the
+        // request reaches (lz4_partial_ok, zstd_partial_ok).
+        const uint64_t end_in = J.end - st.d_off[bad];
+        if (!r->cache && (r->type == ZSEEK_LZ4 ? lz4_partial_ok(J.status, J.fail_at, end_in)
+                                               : zstd_partial_ok(J.status, J.fail_at, end_in)))
+            good_end = J.end;
+    }
+    const uint64_t lo = std::max<uint64_t>(J.offset, d0);
+    const uint64_t hi = std::min<uint64_t>(J.end, good_end);
+    if (!J.device_dst && hi > lo)
+        pool_copy(J.buf + (lo - J.offset), s.h_out + (lo - d0 - s.h_from), hi - lo, &s.copies);
+    J.good_end = std::max<uint64_t>(J.good_end, std::min<uint64_t>(J.end, good_end));
+    if (J.cache_cap) {
+        // the last cache_cap good frames of the batch, in frame order
+        const size_t a = bad - std::min(bad - f0, J.cache_cap);
+        for (size_t i = a; i < bad; i++) {
+            const size_t len = st.dsize(i);
+            uint8_t *p = (uint8_t *)malloc(len ? len : 1);
+            if (!p) {
+                set_error_errno(J.err, "allocate decompressed buffer", errno);
+                J.io_failed = true;
+                return false;
+            }
+            const uint64_t x = st.d_off[i] - d0;
+            if (x >= s.h_from && x + len <= s.h_from + s.h_len) {
+                memcpy(p, s.h_out + (x - s.h_from), len);
+            } else if (len && hipMemcpy(p, s.d_out + x, len, hipMemcpyDeviceToHost) != hipSuccess) {
+                free(p);
+                set_error(J.err, "copy decoded data failed");
+                J.io_failed = true;
+                return false;
+            }
+            J.cached.push_back({i, p, len});
+            if (J.cached.size() > J.cache_cap) {
+                free(J.cached.front().data);
+                J.cached.pop_front();
+            }
         }
     }
+    return bad == f1;
+}
+
+// The batch loop of one lane: up to kSlots batches in flight, finished in
+// order; the first batch is small so a request's first bytes come early.
+void run_lane(LaneJob &J)
+{
+    DeviceGuard keep;
+    DeviceCtx &g = *J.g;
+    (void)hipSetDevice(g.device);
+    J.good_end = std::max<uint64_t>(J.offset, J.r->st.d_off[J.fa]);
+    std::deque<int> inflight;
+    size_t f = J.fa;
+    int next = 0;
+    bool stop = false;
+    size_t limit = std::min(kFirstBatch, J.r->batch_bytes);
+    for (;;) {
+        if (!stop && f < J.fb && (int)inflight.size() < kSlots) {
+            const size_t gend = batch_end(J.r->st, f, J.fb, limit);
+            limit = J.r->batch_bytes;
+            if (!submit(J, g.slot[next], f, gend)) {
+                stop = true;
+                continue;
+            }
+            inflight.push_back(next);
+            next = (next + 1) % kSlots;
+            f = gend;
+            continue;
+        }
+        if (inflight.empty())
+            break;
+        Slot &s = g.slot[inflight.front()];
+        inflight.pop_front();
+        if (stop) {   // a failure before this batch: drain it, keep nothing
+            (void)hipEventSynchronize(s.done);
+            continue;
+        }
+        if (!finish(J, s))
+            stop = true;
+    }
+    for (Slot &s : g.slot)
+        pool_wait(&s.copies);
+}
+
+bool ensure_lanes(zseek_reader *r, char *errbuf)
+{
+    if (r->devices.empty())
+        r->devices = default_devices();
+    if (r->devices.empty()) {
+        set_error(errbuf, "no HIP device available");
+        return false;
+    }
+    while (r->lanes.size() < r->devices.size())
+        r->lanes.emplace_back(new DeviceCtx());
+    for (size_t i = 0; i < r->devices.size(); i++)
+        if (!r->lanes[i]->init(r->devices[i], errbuf))
+            return false;
     return true;
 }
 
 // Range read: [offset, offset+count) into buf (host or device memory), both
 // codecs (ref decompress.c:685-804 LZ4, :377-574 zstd).
 ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, void *call_data,
-                  char *errbuf, bool device_dst)
+                     char *errbuf, bool device_dst)
 {
     const SeekTable &st = r->st;
     int64_t fi = st.frame_of(offset);
@@ -426,22 +584,42 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
     const size_t f_first = (size_t)fi;
     const uint64_t end = offset + count < st.decompressed_size() ? offset + count
                                                                  : st.decompressed_size();
-
     // single-frame request with a cache: the reference's cached path
-    // (decompress.c:699-796), GPU-decoded on a miss
+    // (decompress.c:699-796), GPU-decoded on a miss (one batch of one frame,
+    // one synchronisation)
     if (r->cache && (count == 0 || (size_t)st.frame_of(end - 1) == f_first)) {
         size_t len = 0;
         const uint8_t *data = r->cache->find(f_first, &len);
         if (!data) {
-            BatchResult br;
-            if (!gpu_decode(r, f_first, f_first + 1, call_data, errbuf, &br))
+            if (!ensure_lanes(r, errbuf))
                 return -1;
-            if (br.first_bad != f_first + 1) {
-                frame_error(r, br, f_first, offset - st.d_off[f_first], count, errbuf);
+            LaneJob J;
+            J.r = r;
+            J.g = r->lanes[0].get();
+            J.fa = f_first;
+            J.fb = f_first + 1;
+            J.offset = J.end = st.d_off[f_first + 1];   // nothing to copy: the cache serves it
+            J.device_dst = true;
+            J.call_data = call_data;
+            J.cache_cap = 1;
+            run_lane(J);
+            if (J.io_failed) {
+                set_error(errbuf, "%s", J.err);
+                free_items(J.cached);
                 return -1;
             }
-            if (!cache_frames(r, f_first, f_first, f_first + 1, errbuf))
+            if (J.first_bad != SIZE_MAX || J.cached.empty()) {
+                frame_error(r, J.status, J.fail_at, f_first, offset - st.d_off[f_first], count, errbuf);
+                free_items(J.cached);
                 return -1;
+            }
+            CacheItem c = J.cached.back();
+            J.cached.pop_back();
+            if (!r->cache->insert(c.frame, c.data, c.len)) {
+                free(c.data);
+                set_error(errbuf, "frame caching failed");
+                return -1;
+            }
             data = r->cache->find(f_first, &len);
         }
         size_t rel = offset - st.d_off[f_first];
@@ -458,53 +636,95 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
     }
     if (count == 0)
         return 0;
+    if (!ensure_lanes(r, errbuf))
+        return -1;
 
-    // multi-frame (or no-cache) request: batches of whole frames, one grid each
+    // multi-frame (or no-cache) request: lanes of whole frames, split by
+    // decoded bytes over the reader's devices
     const size_t f_last = (size_t)st.frame_of(end - 1);
-    size_t done = 0;
-    size_t f = f_first;
-    while (f <= f_last) {
-        // grow the batch up to batch_bytes of decoded data (at least 1 frame)
-        size_t g_end = f + 1;
-        while (g_end <= f_last && st.d_off[g_end + 1] - st.d_off[f] <= r->batch_bytes)
-            g_end++;
-        BatchResult br;
-        if (!gpu_decode(r, f, g_end, call_data, errbuf, &br))
-            return done ? (ssize_t)done : -1;
-        const uint64_t lo = offset > st.d_off[f] ? offset : st.d_off[f];
-        uint64_t good_end = br.first_bad < g_end ? st.d_off[br.first_bad] : st.d_off[g_end];
-        // Without a cache the reference decodes a frame only as far as the
-        // request reaches (lz4_partial_ok, zstd_partial_ok).
-        if (br.first_bad < g_end && !r->cache &&
-            (r->type == ZSEEK_LZ4 ? lz4_partial_ok(br.status, br.fail_at, end - st.d_off[br.first_bad])
-                                  : zstd_partial_ok(br.status, br.fail_at, end - st.d_off[br.first_bad])))
-            good_end = end;
-        const uint64_t hi = end < good_end ? end : good_end;
-        if (hi > lo) {
-            if (!copy_out(r->gpu, (uint8_t *)buf + (lo - offset), lo - st.d_off[f], hi - lo,
-                          device_dst, errbuf))
-                return done ? (ssize_t)done : -1;
-            done += hi - lo;
-        }
-        if (br.first_bad < g_end && good_end < end) {
-            if (done)
-                return (ssize_t)done;   // short read up to the corrupt frame
-            frame_error(r, br, br.first_bad, offset - st.d_off[br.first_bad], count, errbuf);
-            return -1;
-        }
-        // the cache ends as a reference caller's looping frame by frame over
-        // the range would leave it: the range's last `capacity` frames, MRU
-        // last, inserted batch by batch before the batch buffer is reused
-        if (r->cache) {
-            const size_t cap = r->cache->capacity();
-            const size_t keep_from = f_last + 1 > cap ? f_last + 1 - cap : 0;
-            const size_t a = keep_from > f ? keep_from : f;
-            if (a < g_end && !cache_frames(r, f, a, g_end, errbuf))
-                return (ssize_t)done;
-        }
-        f = g_end;
+    const size_t nfr = f_last + 1 - f_first;
+    size_t L = r->lanes.size();
+    // a lane gets at least one full batch (and 1 MiB)
+    const size_t per_lane = std::max<size_t>(r->batch_bytes, kLaneMin);
+    L = std::min<size_t>(L, std::max<size_t>(1, (end - offset) / per_lane));
+    L = std::min(L, nfr);
+    int dst_dev = -1;
+    if (device_dst) {
+        hipPointerAttribute_t pa;
+        dst_dev = hipPointerGetAttributes(&pa, buf) == hipSuccess ? pa.device : r->lanes[0]->device;
     }
-    return (ssize_t)done;
+    std::vector<LaneJob> jobs(L);
+    size_t f = f_first;
+    for (size_t i = 0; i < L; i++) {
+        LaneJob &J = jobs[i];
+        J.r = r;
+        J.g = r->lanes[i].get();
+        J.fa = f;
+        if (i + 1 == L) {
+            J.fb = f_last + 1;
+        } else {
+            const uint64_t cut = offset + (end - offset) * (i + 1) / L;
+            J.fb = std::max((size_t)st.frame_of(cut), f + 1);
+        }
+        f = J.fb;
+        J.offset = offset;
+        J.end = end;
+        J.buf = (uint8_t *)buf;
+        J.device_dst = device_dst;
+        J.dst_dev = dst_dev;
+        J.call_data = call_data;
+        J.cache_cap = r->cache ? r->cache->capacity() : 0;
+    }
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < L; i++)
+        th.emplace_back(run_lane, std::ref(jobs[i]));
+    run_lane(jobs[0]);
+    for (auto &t : th)
+        t.join();
+
+    // the contiguous prefix the lanes delivered, up to the first failure
+    ssize_t done = 0;
+    size_t stop_lane = L;
+    for (size_t i = 0; i < L; i++) {
+        LaneJob &J = jobs[i];
+        done = (ssize_t)(J.good_end - offset);
+        if (J.io_failed || J.first_bad != SIZE_MAX) {
+            stop_lane = i;
+            break;
+        }
+    }
+    // the cache ends as a reference caller's looping frame by frame over the
+    // delivered range would leave it: its last `capacity` good frames, MRU last
+    if (r->cache) {
+        std::deque<CacheItem> keep;
+        for (size_t i = 0; i < L; i++) {
+            if (i <= stop_lane || stop_lane == L) {
+                for (CacheItem &c : jobs[i].cached)
+                    keep.push_back(c);
+                jobs[i].cached.clear();
+            } else {
+                free_items(jobs[i].cached);
+            }
+        }
+        while (keep.size() > r->cache->capacity()) {
+            free(keep.front().data);
+            keep.pop_front();
+        }
+        for (CacheItem &c : keep)
+            if (!r->cache->insert(c.frame, c.data, c.len))
+                free(c.data);
+    }
+    if (stop_lane < L && done == 0) {
+        LaneJob &J = jobs[stop_lane];
+        if (J.io_failed)
+            set_error(errbuf, "%s", J.err);
+        else
+            frame_error(r, J.status, J.fail_at, J.first_bad,
+                        offset > st.d_off[J.first_bad] ? offset - st.d_off[J.first_bad] : 0, count,
+                        errbuf);
+        return -1;
+    }
+    return done;
 }
 
 }   // namespace
@@ -557,7 +777,9 @@ extern "C" ZSEEK_EXPORT bool zseek_reader_stats(zseek_reader_t *reader,
     stats->decompressed_size = reader->st.decompressed_size();
     stats->cache_memory = reader->cache ? reader->cache->memory_usage() : 0;
     stats->cached_frames = reader->cache ? reader->cache->entries() : 0;
-    size_t buffered = reader->gpu.host_bytes();
+    size_t buffered = 0;
+    for (auto &l : reader->lanes)
+        buffered += l->host_bytes();
     stats->buffer_size = buffered;
     return true;
 }
@@ -611,20 +833,21 @@ extern "C" ZSEEK_EXPORT int zsk_dev_lz4_decode_variant(int variant, const zsk_fr
 }
 #endif
 
+// The device API's zstd scratch: a bounded stream-ordered pool (pool.h).
 extern "C" ZSEEK_EXPORT int zsk_zstd_decode_frames(const zsk_frame_desc_t *d_desc,
                                                    uint32_t nframes, const void *d_comp,
                                                    void *d_out, int32_t *d_status, void *stream)
 {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, ZstdScratch> cache;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> g(mu);
-    ZstdScratch &s = cache[{dev, static_cast<hipStream_t>(stream)}];
-    return zsk::zstd_decode_frames(reinterpret_cast<const FrameDesc *>(d_desc), nframes,
-                                   static_cast<const uint8_t *>(d_comp),
-                                   static_cast<uint8_t *>(d_out), d_status, &s,
-                                   static_cast<hipStream_t>(stream));
+    static ScratchPool<ZstdScratch> pool;
+    hipStream_t hs = static_cast<hipStream_t>(stream);
+    ZstdScratch *s = pool.acquire(hs);
+    if (!s)
+        return -1;
+    const int rc = zsk::zstd_decode_frames(reinterpret_cast<const FrameDesc *>(d_desc), nframes,
+                                           static_cast<const uint8_t *>(d_comp),
+                                           static_cast<uint8_t *>(d_out), d_status, s, hs);
+    pool.release(s, hs);
+    return rc;
 }
 
 extern "C" ZSEEK_EXPORT int zsk_kernel_timing(int on)
@@ -676,13 +899,15 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader, zsk_gp
     if (!reader || !s)
         return false;
     std::lock_guard<std::mutex> guard(reader->lock);
-    const DeviceCtx &g = reader->gpu;
-    s->batches = g.batches;
-    s->frames_decoded = g.frames_decoded;
-    s->bytes_decoded = g.bytes_decoded;
-    s->bytes_uploaded = g.bytes_uploaded;
-    s->device_memory = g.device_bytes();
-    s->device = g.device;
+    memset(s, 0, sizeof(*s));
+    s->device = reader->lanes.empty() ? -1 : reader->lanes[0]->device;
+    for (auto &l : reader->lanes) {
+        s->batches += l->batches;
+        s->frames_decoded += l->frames_decoded;
+        s->bytes_decoded += l->bytes_decoded;
+        s->bytes_uploaded += l->bytes_uploaded;
+        s->device_memory += l->device_bytes();
+    }
     return true;
 }
 
@@ -703,4 +928,36 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_set_verify_checksums(zseek_reader_t *rea
     std::lock_guard<std::mutex> guard(reader->lock);
     reader->verify = on;
     return true;
+}
+
+// Devices a reader decodes on (zseek_hip.h): one lane per entry, a device may
+// repeat (several pipelines on one GPU).  Takes effect at the next read.
+extern "C" ZSEEK_EXPORT bool zsk_reader_set_devices(zseek_reader_t *reader, const int *devices,
+                                                    int n)
+{
+    if (!reader || n < 0 || (n > 0 && !devices))
+        return false;
+    int count = 0;
+    if (n > 0 && hipGetDeviceCount(&count) != hipSuccess)
+        return false;
+    for (int i = 0; i < n; i++)
+        if (devices[i] < 0 || devices[i] >= count)
+            return false;
+    std::lock_guard<std::mutex> guard(reader->lock);
+    reader->lanes.clear();   // drains and frees the old lanes
+    reader->devices.assign(devices, devices + n);
+    return true;
+}
+
+// The devices a reader decodes on: up to cap entries into devices (NULL:
+// count only); returns the count (0 before the first read picks the default).
+extern "C" ZSEEK_EXPORT int zsk_reader_devices(zseek_reader_t *reader, int *devices, int cap)
+{
+    if (!reader)
+        return -1;
+    std::lock_guard<std::mutex> guard(reader->lock);
+    const int n = (int)reader->devices.size();
+    for (int i = 0; devices && i < n && i < cap; i++)
+        devices[i] = reader->devices[i];
+    return n;
 }

@@ -91,14 +91,6 @@ uint64_t split_items_needed(const FrameDesc *h_desc, uint32_t n);
 int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipStream_t stream);
 void split_scratch_free(SplitScratch *s);
 
-// Scratch for device-API calls (no reader): a small pool per device of
-// scratch sets, each reused in stream order (an event recorded after the
-// launches that use it; a later call on another stream waits on that event
-// instead of allocating).  Bounded: kPoolSets sets per device.
-constexpr int kPoolSets = 4;
-SplitScratch *stream_scratch(hipStream_t stream);
-void stream_scratch_done(SplitScratch *s, hipStream_t stream);
-
 // Parse routing of the two-phase decoder: frames of >= chunk_min compressed
 // bytes take lz4_chunk_kernel, of [lean_min, chunk_min) lz4_lean_kernel,
 // shorter ones lz4_scan_kernel.

@@ -2111,69 +2111,42 @@ int grow(T **p, uint64_t &cap, uint64_t want, uint64_t unit)
     return 0;
 }
 
-// The Huffman side stream and its two events come from a process-wide pool
-// and are never destroyed: a reader's teardown with the runtime still holding
-// an event's last record (on the reader's own stream, destroyed right after)
-// corrupted the host heap now and then.  A released set is drained and its
-// events re-recorded on its own stream, so nothing in the pool refers to a
-// stream that may go away.
-struct SideSet {
-    int dev;
-    hipStream_t side;
-    hipEvent_t ev_tab, ev_huf;
-};
-std::mutex g_side_mu;
-std::vector<SideSet> g_side_pool;
-
-int side_acquire(ZstdScratch *s)
+// The Huffman kernel's side stream and its two events belong to the scratch.
+// Teardown (zstd_scratch_free) drains the side stream and destroys it before
+// its events and before the caller's stream goes: the side stream's wait on
+// an event recorded on the caller's stream is released while that stream is
+// still alive.
+int side_create(ZstdScratch *s)
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess)
-        return -1;
-    {
-        std::lock_guard<std::mutex> lk(g_side_mu);
-        for (size_t i = 0; i < g_side_pool.size(); i++)
-            if (g_side_pool[i].dev == dev) {
-                s->side_dev = dev;
-                s->side = g_side_pool[i].side;
-                s->ev_tab = g_side_pool[i].ev_tab;
-                s->ev_huf = g_side_pool[i].ev_huf;
-                g_side_pool.erase(g_side_pool.begin() + i);
-                return 0;
-            }
-    }
-    SideSet x = {dev, nullptr, nullptr, nullptr};
     // the side stream at the lowest priority: the sequence kernel, the longer
     // of the two, gets the CUs' LDS first (10.9 -> 10.6 ms per launch at
     // config 5; launching the sequence kernel first made no difference)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (hipStreamCreateWithPriority(&x.side, hipStreamNonBlocking, lo) != hipSuccess ||
-        hipEventCreateWithFlags(&x.ev_tab, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&x.ev_huf, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetDevice(&s->side_dev);
+    if (hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_tab, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_huf, hipEventDisableTiming) != hipSuccess) {
         // partly created, nothing recorded on it yet
-        if (x.ev_tab)
-            (void)hipEventDestroy(x.ev_tab);
-        if (x.side)
-            (void)hipStreamDestroy(x.side);
+        if (s->ev_tab)
+            (void)hipEventDestroy(s->ev_tab);
+        if (s->side)
+            (void)hipStreamDestroy(s->side);
+        s->side = nullptr;
+        s->ev_tab = s->ev_huf = nullptr;
         return -1;
     }
-    s->side_dev = dev;
-    s->side = x.side;
-    s->ev_tab = x.ev_tab;
-    s->ev_huf = x.ev_huf;
     return 0;
 }
 
-void side_release(ZstdScratch *s)
+void side_destroy(ZstdScratch *s)
 {
     if (!s->side)
         return;
-    (void)hipEventRecord(s->ev_tab, s->side);
-    (void)hipEventRecord(s->ev_huf, s->side);
     (void)hipStreamSynchronize(s->side);
-    std::lock_guard<std::mutex> lk(g_side_mu);
-    g_side_pool.push_back({s->side_dev, s->side, s->ev_tab, s->ev_huf});
+    (void)hipStreamDestroy(s->side);
+    (void)hipEventDestroy(s->ev_tab);
+    (void)hipEventDestroy(s->ev_huf);
     s->side = nullptr;
     s->ev_tab = s->ev_huf = nullptr;
 }
@@ -2183,7 +2156,7 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
                          uint64_t blocks, hipStream_t stream)
 {
     (void)stream;
-    if (!s->side && side_acquire(s) != 0)
+    if (!s->side && side_create(s) != 0)
         return -1;
     if (frames + 1 > s->frames_cap) {
         const uint32_t cap = frames + 1 < 4096 ? 4096 : frames + 1;
@@ -2224,7 +2197,7 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
 
 void zstd_scratch_free(ZstdScratch *s)
 {
-    side_release(s);   // drains the side stream before anything goes
+    side_destroy(s);   // drains the side stream before anything goes
     for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
                     (void *)s->nitems, (void *)s->ck, (void *)s->stop, (void *)s->lit, (void *)s->items,
                     (void *)s->ops, (void *)s->hjobs, (void *)s->slots, (void *)s->hbad, (void *)s->d_total})
@@ -2309,13 +2282,17 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                     fprintf(stderr, " %d:%u", i, z[i]);
             fprintf(stderr, "  global %u lds %u\n", z[16], z[17]);
         }
-        if (hipEventRecord(s->ev_huf, hs) != hipSuccess)
+        if (hipEventRecord(s->ev_huf, hs) != hipSuccess) {
+            (void)hipStreamSynchronize(hs);   // the kernel may still write lit / hbad
             return -1;
+        }
     }
     seq();
     if (nj) {
-        if (hipStreamWaitEvent(stream, s->ev_huf, 0) != hipSuccess)
+        if (hipStreamWaitEvent(stream, s->ev_huf, 0) != hipSuccess) {
+            (void)hipStreamSynchronize(s->side);
             return -1;
+        }
         hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, nframes, s->ops,
                            s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at);
     }

@@ -94,6 +94,7 @@ EXPORTED = [
     "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
     "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
     "zsk_verify_frame_checksums", "zsk_reader_set_verify_checksums",
+    "zsk_reader_set_devices", "zsk_reader_devices",
 ]
 
 _lib = None
@@ -164,6 +165,10 @@ def lib() -> C.CDLL:
                                              C.c_void_p, C.c_void_p]
     L.zsk_reader_set_verify_checksums.restype = C.c_bool
     L.zsk_reader_set_verify_checksums.argtypes = [C.c_void_p, C.c_bool]
+    L.zsk_reader_set_devices.restype = C.c_bool
+    L.zsk_reader_set_devices.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    L.zsk_reader_devices.restype = C.c_int
+    L.zsk_reader_devices.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
     _lib = L
     return L
 
@@ -400,6 +405,18 @@ class Reader:
 
     def set_batch_bytes(self, n: int) -> None:
         lib().zsk_reader_set_batch_bytes(self._h, n)
+
+    def set_devices(self, devices) -> None:
+        """zsk_reader_set_devices: one decode lane per entry (may repeat)."""
+        arr = (C.c_int * len(devices))(*devices)
+        if not lib().zsk_reader_set_devices(self._h, arr, len(devices)):
+            raise ZseekError("invalid device list")
+
+    def devices(self) -> list:
+        n = lib().zsk_reader_devices(self._h, None, 0)
+        arr = (C.c_int * max(n, 1))()
+        lib().zsk_reader_devices(self._h, arr, n)
+        return list(arr[:n])
 
     def set_verify_checksums(self, on: bool = True) -> None:
         """zsk_reader_set_verify_checksums: check seek-table frame checksums."""

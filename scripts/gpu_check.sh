@@ -1,8 +1,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out/g1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/g1/pytest.log 2>&1; rc=$?
-tail -5 gpurun_out/g1/pytest.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-e2e > gpurun_out/g1/bench.json 2> gpurun_out/g1/bench.err && cat gpurun_out/g1/bench.json
+O=gpurun_out/check
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest.log 2>&1; rc=$?
+grep -E "passed|failed|error" $O/pytest.log | tail -5
+[ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error\|error" $O/pytest.log | head -120; exit $rc; }
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/bench.json 2> $O/bench.err && cat $O/bench.json
