@@ -285,6 +285,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         return 0;
     if (s->frames_cap < nframes || !s->rec_base || !s->redo)
         return -1;
+    (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
     uint64_t *total_dev = nullptr;
     (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
     stage_mark(0, stream);

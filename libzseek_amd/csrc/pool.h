@@ -42,6 +42,10 @@ class ScratchPool {
         for (size_t i = 0; !pick && i < d->sets.size(); i++)
             if (!d->sets[i]->busy && hipEventQuery(d->sets[i]->done) == hipSuccess)
                 pick = d->sets[i];
+        // hipEventQuery's hipErrorNotReady stays the thread's last error,
+        // which the launchers' hipGetLastError checks would take for a
+        // launch failure
+        (void)hipGetLastError();
         if (!pick && (int)d->sets.size() < kPoolSets) {
             pick = new Set();
             if (hipEventCreateWithFlags(&pick->done, hipEventDisableTiming) != hipSuccess) {

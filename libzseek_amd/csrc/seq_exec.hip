@@ -195,7 +195,10 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
             const uint32_t t = t0 + 64 * j + lane;
             const bool on = t < T;
             const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
-            sx[j] = (uint32_t)D;
+            // an idle lane loads the literal source's first 16 bytes (its kind
+            // reads as K_LIT: a stale source offset there could be a match's
+            // output offset, far past a big frame's compressed bytes)
+            sx[j] = on ? (uint32_t)D : 0;
             dw[j] = on ? (uint32_t)(D >> 32) : 0;
             const uint32_t kind = dw[j] >> 24;
             const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);

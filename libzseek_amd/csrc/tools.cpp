@@ -191,6 +191,39 @@ ZSK_TOOL int zsk_tool_lz4_seekable(const uint8_t *in, size_t n, size_t frame_siz
                     });
 }
 
+// A seekable LZ4 image whose frames use LZ4F options the reference writer
+// never sets (compress.c:203-207 fixes max64KB, autoFlush, nothing else) but
+// its reader accepts through LZ4F_decompress (decompress.c:752-773): block
+// size id 4..7, linked / independent blocks, content checksum, block
+// checksums, content size, dictID.  One LZ4F_compressFrame per frame (which
+// makes a frame that fits one block independent, as liblz4 does).
+ZSK_TOOL int zsk_tool_lz4_seekable_ex(const uint8_t *in, size_t n, size_t frame_size, int level,
+                                      int bsid, int independent, int content_checksum,
+                                      int block_checksum, int content_size, unsigned dict_id,
+                                      int threads, uint8_t *out, size_t out_cap, size_t *out_len)
+{
+    auto prefs = [=](size_t len) {
+        LZ4F_preferences_t p = lz4_prefs(level, content_size ? len : 0);
+        p.frameInfo.blockSizeID = (LZ4F_blockSizeID_t)bsid;
+        p.frameInfo.blockMode = independent ? LZ4F_blockIndependent : LZ4F_blockLinked;
+        p.frameInfo.contentChecksumFlag = content_checksum ? LZ4F_contentChecksumEnabled
+                                                           : LZ4F_noContentChecksum;
+        p.frameInfo.blockChecksumFlag = block_checksum ? LZ4F_blockChecksumEnabled : LZ4F_noBlockChecksum;
+        p.frameInfo.dictID = dict_id;
+        return p;
+    };
+    LZ4F_preferences_t pb = prefs(frame_size);
+    size_t slot = LZ4F_compressFrameBound(frame_size, &pb);
+    if (slot * ((n + frame_size - 1) / frame_size) + 8 + 8 * ((n + frame_size - 1) / frame_size) + 9 > out_cap)
+        return -1;
+    return seekable(in, n, frame_size, threads, slot, out, out_cap, out_len,
+                    [prefs](uint8_t *dst, size_t cap, const uint8_t *src, size_t len, bool) -> size_t {
+                        LZ4F_preferences_t p = prefs(len);
+                        size_t c = LZ4F_compressFrame(dst, cap, src, len, &p);
+                        return LZ4F_isError(c) ? 0 : c;
+                    });
+}
+
 ZSK_TOOL size_t zsk_tool_zstd_seekable_bound(size_t n, size_t frame_size)
 {
     size_t nf = frame_size ? (n + frame_size - 1) / frame_size : 0;

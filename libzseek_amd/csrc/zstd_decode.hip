@@ -2315,6 +2315,7 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 {
     if (nframes == 0)
         return 0;
+    (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
     if (zstd_scratch_reserve(s, nframes, 0, 0, 0, stream) != 0)
         return -1;
     stage_mark(0, stream);

@@ -195,6 +195,10 @@ def tools() -> C.CDLL:
     T.zsk_tool_zstd_seekable.restype = C.c_int
     T.zsk_tool_zstd_seekable.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
                                          C.c_int, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    T.zsk_tool_lz4_seekable_ex.restype = C.c_int
+    T.zsk_tool_lz4_seekable_ex.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
+                                           C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint, C.c_int,
+                                           C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
     T.zsk_tool_open_mem.restype = C.c_void_p
     T.zsk_tool_open_mem.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_char_p]
     T.zsk_tool_close_mem.restype = C.c_bool
@@ -237,6 +241,27 @@ def lz4_seekable(data: np.ndarray, frame_size: int, level: int = 0, threads: int
     n = C.c_size_t(0)
     if T.zsk_tool_lz4_seekable(data.ctypes.data, data.size, frame_size, level, threads,
                                out.ctypes.data, cap, C.byref(n)) != 0:
+        raise ZseekError("lz4 seekable compression failed")
+    return out[: n.value]
+
+
+def lz4_seekable_ex(data: np.ndarray, frame_size: int, *, level: int = 0, bsid: int = 4,
+                    independent: bool = False, content_checksum: bool = False,
+                    block_checksum: bool = False, content_size: bool = False, dict_id: int = 0,
+                    threads: int = 16) -> np.ndarray:
+    """Seekable LZ4 image with LZ4F frame options the reference writer never
+    sets but its reader accepts (block size id 4..7, linked / independent
+    blocks, content / block checksums, content size, dictID)."""
+    T = tools()
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    nf = max(1, -(-data.size // frame_size))
+    cap = nf * (frame_size + frame_size // 64 + (1 << 16)) + 8 * nf + 64
+    out = np.empty(cap, np.uint8)
+    n = C.c_size_t(0)
+    if T.zsk_tool_lz4_seekable_ex(data.ctypes.data, data.size, frame_size, level, bsid,
+                                  int(independent), int(content_checksum), int(block_checksum),
+                                  int(content_size), dict_id, threads, out.ctypes.data, cap,
+                                  C.byref(n)) != 0:
         raise ZseekError("lz4 seekable compression failed")
     return out[: n.value]
 

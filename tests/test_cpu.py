@@ -13,9 +13,16 @@ import pytest
 
 from conftest import GOLDEN, ROOT, golden_file, sha
 
+# LZ4F-option fixtures: frames the reference writer never makes (checksums,
+# dictID, linked / bigger blocks) that its reader accepts, read by it
+LZ4F = ["lz4f_content_checksum", "lz4f_block_checksum_linked", "lz4f_dictid_1m_blocks",
+        "lz4f_all_flags_256k"]
 LZ4 = [n for n in ["lz4_64k_direct", "lz4_64k_buffered", "lz4_4k_direct", "lz4_1m_direct",
                    "lz4_1m_buffered", "lz4_odd_frames", "lz4_zeros", "lz4_random",
-                   "lz4_periodic", "lz4_text_hc", "lz4_single_byte"]]
+                   "lz4_periodic", "lz4_text_hc", "lz4_single_byte"]] + LZ4F
+LZ4F_CORRUPT = ["lz4f_content_checksum__content_checksum",
+                "lz4f_block_checksum_linked__block_checksum",
+                "lz4f_all_flags_256k__content_checksum", "lz4f_all_flags_256k__block_checksum"]
 ZSTD = ["zstd_64k_direct", "zstd_64k_buffered"]
 
 
@@ -98,7 +105,7 @@ def _oracle_error(oracle, img, cache, off, cnt):
 @pytest.mark.parametrize("case", ["block_byte", "block_size_huge", "first_token_offset",
                                   "frame_magic", "flg_version", "flg_reserved", "bd_reserved",
                                   "bd_blocksize", "header_checksum", "1m_block4_offset0",
-                                  "1m_block4_size_huge"])
+                                  "1m_block4_size_huge"] + LZ4F_CORRUPT)
 def test_oracle_errors_match_reference(oracle, golden, case):
     """Every corruption fixture: the restatement's result (error string, or the
     bytes a partial no-cache read gets) equals the reference's.  1m_block4_offset0
@@ -307,7 +314,7 @@ def test_open_errors_match_reference(zs, golden, case):
     assert str(e.value) == rec["open_error"]
 
 
-@pytest.mark.parametrize("name", [n for n in LZ4 if n != "lz4_text_hc"])
+@pytest.mark.parametrize("name", [n for n in LZ4 if n != "lz4_text_hc" and n not in LZ4F])
 def test_writer_byte_identical_to_reference(zs, golden, payloads, name):
     entry = golden["files"][name]
     data = payloads[name]
