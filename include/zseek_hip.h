@@ -183,6 +183,16 @@ ZSEEK_EXPORT bool zsk_reader_set_verify_checksums(zseek_reader_t *reader,
     bool on);
 
 /*
+ * Allow up to @n concurrent calls of the reader's pread callback (on
+ * disjoint ranges of >= 4 MiB of one batch's compressed span).  Default 1,
+ * the reference's contract: it calls pread under the reader's lock, one call
+ * at a time, and its default FILE* callback is not safe to call concurrently.
+ * Only for callbacks that are (an in-memory image, pread(2) on a descriptor).
+ * Env ZSEEK_IO_THREADS at open.  false for a NULL reader or n outside 1..64.
+ */
+ZSEEK_EXPORT bool zsk_reader_set_io_threads(zseek_reader_t *reader, int n);
+
+/*
  * The devices a reader decodes on: one decode pipeline ("lane") per entry; a
  * multi-frame read is split into contiguous frame ranges by decoded bytes,
  * one per lane, decoded concurrently (host destinations: each lane copies its

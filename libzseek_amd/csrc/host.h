@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <functional>
 #include <list>
 #include <unordered_map>
 #include <vector>
@@ -97,6 +98,7 @@ struct CopyTicket {
     std::atomic<int> left{0};
 };
 void pool_copy(void *dst, const void *src, size_t n, CopyTicket *t);
+void pool_run(std::function<void()> fn, CopyTicket *t);   // any task, same ticket rules
 void pool_wait(CopyTicket *t);
 
 // One batch of frames in flight: its own stream, pinned staging and device

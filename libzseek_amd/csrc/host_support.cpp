@@ -8,6 +8,7 @@
 
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <thread>
 
@@ -202,6 +203,7 @@ struct CopyTask {
     const void *src;
     size_t n;
     CopyTicket *t;
+    std::function<void()> fn;   // a task to run instead of the copy
 };
 
 class CopyPool {
@@ -241,7 +243,10 @@ class CopyPool {
                 t = q_.front();
                 q_.pop_front();
             }
-            memcpy(t.dst, t.src, t.n);
+            if (t.fn)
+                t.fn();
+            else
+                memcpy(t.dst, t.src, t.n);
             if (t.t->left.fetch_sub(1) == 1) {
                 std::lock_guard<std::mutex> g(mu_);
                 done_.notify_all();
@@ -271,8 +276,14 @@ void pool_copy(void *dst, const void *src, size_t n, CopyTicket *t)
     t->left.fetch_add((int)pieces);
     for (size_t i = 0; i < pieces; i++) {
         const size_t o = i * kCopyPiece;
-        p.put({(uint8_t *)dst + o, (const uint8_t *)src + o, n - o < kCopyPiece ? n - o : kCopyPiece, t});
+        p.put({(uint8_t *)dst + o, (const uint8_t *)src + o, n - o < kCopyPiece ? n - o : kCopyPiece, t, {}});
     }
+}
+
+void pool_run(std::function<void()> fn, CopyTicket *t)
+{
+    t->left.fetch_add(1);
+    copy_pool().put({nullptr, nullptr, 0, t, std::move(fn)});
 }
 
 void pool_wait(CopyTicket *t)

@@ -72,6 +72,7 @@ struct zseek_reader {
     std::mutex cursor_lock;        // zseek_read: cursor read, pread, advance as one step
     size_t pos = 0;                // zseek_read cursor (ref :826-835)
     size_t batch_bytes = kDefaultBatch;
+    int io_threads = 1;    // > 1: the caller allows concurrent pread callbacks
     bool verify = false;   // check seek-table frame checksums (the reference never does)
     std::vector<int> devices;                       // lane i decodes on devices[i]
     std::vector<std::unique_ptr<DeviceCtx>> lanes;  // created at first use
@@ -156,6 +157,9 @@ extern "C" ZSEEK_EXPORT zseek_reader_t *zseek_reader_open_full(zseek_read_file_t
     }
     const char *vck = getenv("ZSEEK_VERIFY_CHECKSUMS");
     r->verify = vck && *vck && strcmp(vck, "0") != 0;
+    const char *io = getenv("ZSEEK_IO_THREADS");
+    if (io && *io && atoi(io) > 1)
+        r->io_threads = atoi(io) > 64 ? 64 : atoi(io);
     const char *env = getenv("ZSEEK_HIP_BATCH_BYTES");
     if (env && *env) {
         size_t b = strtoull(env, nullptr, 0);
@@ -325,6 +329,48 @@ size_t batch_end(const SeekTable &st, size_t f, size_t fb, size_t limit)
     return g;
 }
 
+// The batch's compressed span through the user's pread callback: one call
+// at a time (the reference's contract: it calls pread under the reader's
+// lock), or, where the caller allowed it (zsk_reader_set_io_threads), up to
+// io_threads concurrent calls on disjoint pieces of >= 4 MiB.
+bool read_span(LaneJob &J, uint8_t *dst, uint64_t len, uint64_t off)
+{
+    zseek_reader *r = J.r;
+    const uint64_t kPiece = 4u << 20;
+    const int parts = (int)std::min<uint64_t>((uint64_t)r->io_threads, len / kPiece);
+    if (parts <= 1) {
+        std::lock_guard<std::mutex> io(r->io_lock);
+        ssize_t got = r->user_file.pread(dst, len, off, r->user_file.user_data, J.call_data);
+        if (got != (ssize_t)len) {
+            // ref decompress.c:735-741
+            set_error(J.err, got >= 0 ? "unexpected EOF" : "read file failed");
+            return false;
+        }
+        return true;
+    }
+    std::vector<ssize_t> got(parts, 0);
+    CopyTicket t;
+    const uint64_t per = (len / parts + 4095) & ~4095ull;
+    for (int i = 0; i < parts; i++) {
+        const uint64_t a = std::min<uint64_t>(len, per * i), b = std::min<uint64_t>(len, per * (i + 1));
+        pool_run([&, i, a, b] {
+            got[i] = b > a ? r->user_file.pread(dst + a, b - a, off + a, r->user_file.user_data, J.call_data)
+                           : 0;
+            if (got[i] == (ssize_t)(b - a))
+                got[i] = 0;   // complete
+            else if (got[i] >= 0)
+                got[i] = 1;   // short: EOF
+        }, &t);
+    }
+    pool_wait(&t);
+    for (int i = 0; i < parts; i++)
+        if (got[i] != 0) {
+            set_error(J.err, got[i] > 0 ? "unexpected EOF" : "read file failed");
+            return false;
+        }
+    return true;
+}
+
 // Read, upload, decode and queue the download of frames [f0, f1) on slot s.
 bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
 {
@@ -356,15 +402,9 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         J.io_failed = true;
         return false;
     }
-    if (csz) {
-        std::lock_guard<std::mutex> io(r->io_lock);
-        ssize_t got = r->user_file.pread(s.h_comp, csz, c0, r->user_file.user_data, J.call_data);
-        if (got != (ssize_t)csz) {
-            // ref decompress.c:735-741
-            set_error(J.err, got >= 0 ? "unexpected EOF" : "read file failed");
-            J.io_failed = true;
-            return false;
-        }
+    if (csz && !read_span(J, s.h_comp, csz, c0)) {
+        J.io_failed = true;
+        return false;
     }
     for (size_t i = 0; i < n; i++) {
         FrameDesc &d = s.h_desc[i];
@@ -917,6 +957,17 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_set_batch_bytes(zseek_reader_t *reader, 
         return false;
     std::lock_guard<std::mutex> guard(reader->lock);
     reader->batch_bytes = bytes;
+    return true;
+}
+
+// Concurrent pread callbacks (zseek_hip.h): an opt-in beyond the reference's
+// contract, for callbacks that are safe to call from several threads.
+extern "C" ZSEEK_EXPORT bool zsk_reader_set_io_threads(zseek_reader_t *reader, int n)
+{
+    if (!reader || n < 1 || n > 64)
+        return false;
+    std::lock_guard<std::mutex> guard(reader->lock);
+    reader->io_threads = n;
     return true;
 }
 

@@ -94,7 +94,7 @@ EXPORTED = [
     "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
     "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
     "zsk_verify_frame_checksums", "zsk_reader_set_verify_checksums",
-    "zsk_reader_set_devices", "zsk_reader_devices",
+    "zsk_reader_set_devices", "zsk_reader_devices", "zsk_reader_set_io_threads",
 ]
 
 _lib = None
@@ -167,6 +167,8 @@ def lib() -> C.CDLL:
     L.zsk_reader_set_verify_checksums.argtypes = [C.c_void_p, C.c_bool]
     L.zsk_reader_set_devices.restype = C.c_bool
     L.zsk_reader_set_devices.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    L.zsk_reader_set_io_threads.restype = C.c_bool
+    L.zsk_reader_set_io_threads.argtypes = [C.c_void_p, C.c_int]
     L.zsk_reader_devices.restype = C.c_int
     L.zsk_reader_devices.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
     _lib = L
@@ -436,6 +438,12 @@ class Reader:
         arr = (C.c_int * len(devices))(*devices)
         if not lib().zsk_reader_set_devices(self._h, arr, len(devices)):
             raise ZseekError("invalid device list")
+
+    def set_io_threads(self, n: int) -> None:
+        """zsk_reader_set_io_threads: concurrent pread callbacks (this class's
+        in-memory callback is safe for it)."""
+        if not lib().zsk_reader_set_io_threads(self._h, n):
+            raise ZseekError("invalid io thread count")
 
     def devices(self) -> list:
         n = lib().zsk_reader_devices(self._h, None, 0)

@@ -179,3 +179,20 @@ def test_single_frame_reads_one_batch_each(gpu, zs, synth_img):
                 b0 = r.gpu_stats()["batches"]
                 assert r.pread(4096, off) == data[off: off + 4096].tobytes()
                 assert r.gpu_stats()["batches"] - b0 <= 1
+
+
+@pytest.mark.parametrize("io", [2, 4, 8])
+def test_parallel_pread_callbacks(gpu, zs, io):
+    """zsk_reader_set_io_threads: a batch's compressed span read by concurrent
+    pread calls on disjoint pieces (the in-memory callback is safe for it):
+    every byte exact, multi-batch, ragged, and a read past the end."""
+    data = zs.synth_buffer(40 << 20)
+    img = zs.lz4_seekable(data, FRAME)
+    with zs.Reader(img, 0) as r:
+        r.set_io_threads(io)
+        r.set_batch_bytes(24 << 20)
+        assert r.pread(len(data), 0) == data.tobytes()
+        assert r.pread(len(data), 12345) == data[12345:].tobytes()
+    with zs.Reader(img, 0) as r:
+        with pytest.raises(zs.ZseekError):
+            r.set_io_threads(0)
