@@ -270,6 +270,14 @@ def main():
         dev = torch.device("cpu")
         if world > 1:
             dist.init_process_group("gloo")
+    elif os.environ.get("ZSEEK_BENCH_SHARE_GPU") == "1":
+        # rehearsal of the multi-rank GPU path on a one-GPU box: every rank
+        # decodes on device 0, the collective runs over gloo (RCCL refuses
+        # two ranks on one device); never the measured configuration
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(0)
+        if world > 1:
+            dist.init_process_group("gloo")
     else:
         dev = torch.device("cuda", local)
         if world > 1:
