@@ -568,7 +568,8 @@ def reassemble(dist, torch, out, sh, world, rank, dev, args, base_dev, harness):
             "received_GBps_per_rank": round(recv / float(t[0]) / 1e9, 2),
             "method": ("all_gather_into_tensor" if len(set(counts)) == 1 else
                        "grouped broadcasts (all-gatherv)") +
-                      (" over gloo (rehearsal)" if harness else " over RCCL/xGMI"),
+                      (" over gloo (rehearsal)" if harness or dist.get_backend() == "gloo"
+                       else " over RCCL/xGMI"),
             "full_range_matches_generator": ok}
 
 
