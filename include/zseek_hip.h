@@ -85,7 +85,9 @@ ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
  * zsk_lz4_decode_frames with one of the library's production decoders forced
  * for every frame (testing, tooling): ZSK_DECODER_AUTO is the library's own
  * choice (= zsk_lz4_decode_frames); WAVE the wave-per-frame decoder; LEAN,
- * SCAN and CHUNK the two-phase decoder with that parse kernel for every frame.
+ * SCAN and CHUNK the two-phase decoder with that parse kernel for every frame;
+ * BLOCK the two-phase decoder's block route (one parse lane per LZ4 block of
+ * each multi-block frame, the chunk parse for the rest) at any batch size.
  * Returns -1 for an unknown decoder.
  */
 #define ZSK_DECODER_AUTO 0
@@ -93,6 +95,7 @@ ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
 #define ZSK_DECODER_LEAN 2
 #define ZSK_DECODER_SCAN 3
 #define ZSK_DECODER_CHUNK 4
+#define ZSK_DECODER_BLOCK 5
 ZSEEK_EXPORT int zsk_lz4_decode_frames_ex(const zsk_frame_desc_t *d_desc,
     uint32_t nframes, const void *d_comp, void *d_out, int32_t *d_status,
     void *stream, int decoder);

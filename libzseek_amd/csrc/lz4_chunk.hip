@@ -379,7 +379,9 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
-    uint32_t min_csize)
+    uint32_t min_csize, uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
+    const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, const uint32_t *__restrict__ njobs,
+    uint32_t min_jobs)
 {
     __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
     __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
@@ -391,6 +393,40 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
     const FrameDesc d = desc[f];
     if (uni(d.c_size) < min_csize)
         return;   // lz4_scan_kernel's frame
+    if (bfirst) {
+        // block route: the frame's jobs (lane j: job j) are its parse when
+        // every one reached its next header with every rule met, each block
+        // but the last decoding to exactly the maximum block size (so the
+        // speculative offsets were the real ones) and the last ending at
+        // dSize; otherwise this kernel parses the frame and the execute reads
+        // its items from rec_base (the job list is dropped)
+        const uint32_t j0 = uni(bfirst[f]);
+        if (j0 != kNoJob) {
+            const uint32_t nb = uni(bcount[f]);
+            bool bad = uni(*njobs) < min_jobs || nb == 0 || nb > 64;
+            uint32_t k = 0;
+            if (!bad && lane < nb) {
+                const BlockJob J = jobs[j0 + lane];
+                const BlockRes R = jres[j0 + lane];
+                const uint32_t mb = 1u << (8 + 2 * (J.info & 0xFF));
+                const uint32_t end = lane + 1 == nb ? d.d_size : J.bop + mb;
+                k = R.n;
+                bad = J.f != f || R.st != ST_OK || R.op != end || R.n == 0;
+            }
+            if (__ballot(bad) == 0) {
+                const uint32_t total = wave_incl_add(k);
+                if (lane == 63) {
+                    status[f] = ST_OK;
+                    nitems[f] = total;
+                    if (fail_at)
+                        fail_at[f] = 0;
+                }
+                return;
+            }
+            if (lane == 0)
+                bfirst[f] = kNoJob;
+        }
+    }
     const uint64_t rb0 = rec_base[f];
     const uint32_t cap = slots_of(d.c_size);
     const uint32_t clen = d.c_size, dlen = d.d_size;
@@ -543,13 +579,16 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
 
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
-                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize)
+                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
+                     SplitScratch *blk, uint32_t min_jobs)
 {
     if (nframes == 0)
         return 0;
     hipLaunchKernelGGL(lz4_chunk_kernel, dim3((nframes + kCW - 1) / kCW), dim3(64 * kCW), 0, stream,
                        d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
-                       min_csize);
+                       min_csize, blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr,
+                       blk ? blk->jobs : nullptr, blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr,
+                       min_jobs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

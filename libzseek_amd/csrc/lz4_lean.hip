@@ -77,6 +77,7 @@ struct Lane {
     uint32_t mlim;                     // min(oend - LASTLITERALS, dlen): a match's end bound
     uint32_t tok, lsrc, nlit;          // sequence whose offset is pending (P_OFF, slow step)
     uint32_t acc, moff;                // partial extension sum (P_LEXT / P_MEXT), offset (P_MEXT)
+    uint32_t stop;                     // block route: the header that ends the job (else ~0)
     uint32_t ib, k, cap;               // item 0 at irs byte 8*ib; k emitted, cap slots
     uint32_t kf;                       // items [0, kf) written to HBM (a multiple of 16)
     // the sub-step's item store: slots k0, k0+1 (nk = 0: none)
@@ -453,6 +454,10 @@ __device__ __forceinline__ void slow(Lane &L)
         return;
     }
     if (L.ph == P_BHDR) {
+        if (L.ip == L.stop) {   // block route: the job's block parsed
+            finish(L, ST_OK);
+            return;
+        }
         L.fail_op = L.op;
         if (L.clen - L.ip < 4) {
             finish(L, ST_TRUNCATED);
@@ -611,12 +616,16 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
 // 4 = sub-step outcome counters (printed), 8 / 16 = a 4- / 1-deep fill pipeline
 // (default 2: at ~1,400 cycles per sub-step, 4 sub-steps cover the loads)
 // D: fill pipeline depth (slots of up to 64 bytes, retired every other sub-step)
-template <int DIAG, int D>
+// BLK: the block route -- lane t parses job t of `jobs` (one LZ4 block from
+// its header at the job's speculative output offset, every liblz4 rule, up
+// to the next header) into the job's slots and result; n = the job slots.
+template <int DIAG, int D, bool BLK>
 __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))) void lz4_lean_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
-    uint32_t max_csize, uint32_t min_csize)
+    uint32_t max_csize, uint32_t min_csize, const BlockJob *__restrict__ jobs, BlockRes *__restrict__ jres,
+    const uint32_t *__restrict__ njobs)
 {
     __shared__ __attribute__((aligned(16))) uint8_t rings[kLW * 64 * kStride];
     __shared__ __attribute__((aligned(16))) uint64_t tabs[kLW * (kFlush + 1)];
@@ -624,23 +633,37 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     const uint32_t tab = (uint32_t)(uintptr_t)(tabs) + (threadIdx.x >> 6) * 8 * (kFlush + 1);
     const uint32_t f = blockIdx.x * (64 * kLW) + threadIdx.x;
     FrameDesc d = {0, 0, 0, 0};
-    if (f < n)
-        d = desc[f];
-    // frames of max_csize bytes and more belong to lz4_chunk_kernel, frames
-    // under min_csize to lz4_scan_kernel
-    const bool act = f < n && d.c_size < max_csize && d.c_size >= min_csize;
+    BlockJob J = {kNoJob, 0, 0, 0, 0, 0, 0, 0};
+    bool act;
+    if (BLK) {
+        // min_csize: the job minimum (fewer planned: the chunk parse takes
+        // the frames)
+        const uint32_t nj = uni(*njobs);
+        if (nj >= min_csize && f < nj && f < n)
+            J = jobs[f];
+        act = J.f != kNoJob;
+        if (act)
+            d = desc[J.f];
+    } else {
+        if (f < n)
+            d = desc[f];
+        // frames of max_csize bytes and more belong to lz4_chunk_kernel,
+        // frames under min_csize to lz4_scan_kernel
+        act = f < n && d.c_size < max_csize && d.c_size >= min_csize;
+    }
     uint64_t rb0 = 0;
     uint32_t cap = 0;
     if (act) {
-        rb0 = rec_base[f];
-        cap = slots_of(d.c_size);
+        rb0 = rec_base[BLK ? J.f : f] + J.slot_off * (uint32_t)BLK;
+        cap = BLK ? J.slot_cap : slots_of(d.c_size);
     }
     const uint64_t clo = uni64(wave_min64(act ? d.c_off : ~0ull));
     const uint64_t chi = uni64(wave_max64(act ? d.c_off + d.c_size : 0ull));
     const uint64_t ilo = uni64(wave_min64(act ? rb0 : ~0ull));
     const uint64_t ihi = uni64(wave_max64(act ? rb0 + cap : 0ull));
+    const uint64_t work = BLK ? (uint64_t)(J.stop - J.hpos) : (uint64_t)d.c_size;
     const uint32_t steps = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(wave_max64(act ? (uint64_t)d.c_size : 0ull) * 2 + 64 * D + 1024));
+        (int)(uint32_t)(wave_max64(act ? work : 0ull) * 2 + 64 * D + 1024));
     if (clo == ~0ull)
         return;   // no frame in this wave (inactive lanes stay: flushes take all 64)
     Lane L;
@@ -665,6 +688,7 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     L.iend = L.oend = L.floor_ = L.bop = L.mlim = 0;
     L.tok = L.lsrc = L.nlit = L.acc = L.moff = 0;
     L.k = L.kf = 0;
+    L.stop = 0xFFFFFFFFu;
     L.cap = cap;
     L.ia = L.ibw = L.ia2 = L.ib2 = L.nk = 0;
     for (int i = 0; i < 6; i++)
@@ -672,6 +696,24 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     if (!act || cspan >= 0x7FFFFF00ull || ispan >= 0x7FFFFF00ull || d.c_size > kItemPos ||
         rb0 + cap > capacity) {
         finish(L, ST_NOT_RUN);
+    } else if (BLK) {
+        // the job's block: its header's 128 bytes synchronously, the frame
+        // header's fields from the plan
+        L.ip = J.hpos;
+        L.op = J.bop;
+        L.stop = J.stop;
+        L.bsid = J.info & 0xFF;
+        L.indep = (J.info >> 8) & 1;
+        L.max_block = 1u << (8 + 2 * L.bsid);
+        L.fill = (L.cx0 + J.hpos) & ~31u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t fx = L.fill;
+            const u32x4 a = bload16(L.cin, fx), b = bload16(L.cin, fx + 16);
+            ring_put(L, fx, a, b, true);
+            L.fill += 32;
+        }
+        L.avail = L.fill;
     } else {
         // frame header: the first 128 bytes, synchronously
 #pragma unroll
@@ -736,6 +778,10 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     if (!act)
         return;
+    if (BLK) {
+        jres[f] = BlockRes{L.k, L.op, L.st, 0};
+        return;
+    }
     status[f] = L.st;
     nitems[f] = L.k;
     if (fail_at)
@@ -753,9 +799,10 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
         return 0;
     const uint32_t per = 64 * kLW;
     const dim3 grid((nframes + per - 1) / per), block(per);
-#define ZSK_LEAN(D, P)                                                                                  \
-    hipLaunchKernelGGL((lz4_lean_kernel<D, P>), grid, block, 0, stream, d_desc, nframes, d_comp, rec_base, \
-                       capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize)
+#define ZSK_LEAN(D, P)                                                                                         \
+    hipLaunchKernelGGL((lz4_lean_kernel<D, P, false>), grid, block, 0, stream, d_desc, nframes, d_comp, rec_base, \
+                       capacity, items, nitems, d_status, d_fail_at, max_csize, min_csize, nullptr, nullptr,       \
+                       nullptr)
 #ifdef ZSK_TUNING
     if (diag & 4) {
         unsigned long long z[6] = {0};
@@ -780,6 +827,21 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 #endif
         ZSK_LEAN(0, 2);
 #undef ZSK_LEAN
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_lz4_lean_blocks(const FrameDesc *d_desc, const uint8_t *d_comp, const uint64_t *rec_base,
+                           uint64_t capacity, uint64_t *items, const SplitScratch *s, uint32_t lanes,
+                           uint32_t min_jobs, hipStream_t stream)
+{
+    if (lanes == 0)
+        return 0;
+    if (lanes > s->jobs_cap || !s->jobs || !s->jres || !s->njobs)
+        return -1;
+    const uint32_t per = 64 * kLW;
+    hipLaunchKernelGGL((lz4_lean_kernel<0, 2, true>), dim3((lanes + per - 1) / per), dim3(per), 0, stream,
+                       d_desc, lanes, d_comp, rec_base, capacity, items, nullptr, nullptr, nullptr, 0u,
+                       min_jobs, s->jobs, s->jres, s->njobs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

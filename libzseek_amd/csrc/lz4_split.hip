@@ -98,6 +98,103 @@ __global__ __launch_bounds__(1024) void lz4_plan_kernel(const FrameDesc *__restr
         *total = part[t];
 }
 
+// ---- block route plan ---------------------------------------------------------
+// Lane per frame: a frame of > 64 KiB decoded and >= min_csize compressed
+// bytes whose header passes every check lz4_lean_kernel's hdr_status makes
+// (no checksum flags; content size, when present, equal to the seek table's
+// dSize) and whose block headers chain to an end mark at exactly c_size, with
+// at most kMaxBlockJobs blocks and a dSize those blocks can hold, gets one job
+// per block (reserved with one atomic, written in block order).  Every other
+// frame keeps kNoJob and the chunk parse decodes it as before; a reservation
+// past the job slots marks the slots it got as no job.
+__device__ __forceinline__ uint32_t xxh32_short(const uint8_t *c, uint32_t p, uint32_t n)
+{
+    uint32_t acc = 0x165667B1u + n, i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const uint32_t w = c[p + i] | c[p + i + 1] << 8 | c[p + i + 2] << 16 | (uint32_t)c[p + i + 3] << 24;
+        acc += w * 0xC2B2AE3Du;
+        acc = ((acc << 17) | (acc >> 15)) * 0x27D4EB2Fu;
+    }
+    for (; i < n; i++) {
+        acc += c[p + i] * 0x165667B1u;
+        acc = ((acc << 11) | (acc >> 21)) * 0x9E3779B1u;
+    }
+    acc ^= acc >> 15;
+    acc *= 0x85EBCA77u;
+    acc ^= acc >> 13;
+    acc *= 0xC2B2AE3Du;
+    acc ^= acc >> 16;
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void lz4_block_plan_kernel(const FrameDesc *__restrict__ desc, uint32_t n,
+                                                              const uint8_t *__restrict__ comp, uint32_t min_csize,
+                                                              uint32_t *__restrict__ bfirst,
+                                                              uint32_t *__restrict__ bcount,
+                                                              uint32_t *__restrict__ njobs,
+                                                              BlockJob *__restrict__ jobs, uint32_t jobs_cap)
+{
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    if (f >= n)
+        return;
+    const FrameDesc d = desc[f];
+    bfirst[f] = kNoJob;
+    bcount[f] = 0;
+    const uint32_t clen = d.c_size;
+    if (d.d_size <= 65536 || clen < min_csize || clen < 15 || clen > 0x3FFFFFFFu)   // item positions: 30 bits
+        return;
+    const uint8_t *c = comp + d.c_off;
+    auto r32 = [&](uint32_t p) -> uint32_t {
+        return c[p] | c[p + 1] << 8 | c[p + 2] << 16 | (uint32_t)c[p + 3] << 24;
+    };
+    if (r32(0) != kLz4Magic)
+        return;
+    const uint32_t flg = c[4], bd = c[5];
+    if ((flg & 0xC0) != 0x40 || (flg & 0x16) || (bd & 0x8F) || ((bd >> 4) & 7) < 4)
+        return;
+    const uint32_t csz = (flg >> 3) & 1, dictid = flg & 1;
+    const uint32_t hdr = 7 + 8 * csz + 4 * dictid;
+    if (clen < hdr + 4 || ((xxh32_short(c, 4, hdr - 5) >> 8) & 0xFF) != c[hdr - 1])
+        return;
+    if (csz && (r32(6) != d.d_size || r32(10) != 0))
+        return;
+    const uint32_t bsid = (bd >> 4) & 7, max_block = 1u << (8 + 2 * bsid);
+    uint32_t p = hdr, nb = 0;
+    for (;;) {
+        if (clen - p < 4)
+            return;
+        const uint32_t h = r32(p);
+        if (h == 0) {
+            if (clen - p != 4)
+                return;
+            break;
+        }
+        const uint32_t sz = h & 0x7FFFFFFFu;
+        if (sz == 0 || sz > max_block || sz > clen - p - 8 || ++nb > kMaxBlockJobs)
+            return;
+        p += 4 + sz;
+    }
+    if ((uint64_t)(nb - 1) * max_block >= d.d_size || (uint64_t)nb * max_block < d.d_size)
+        return;
+    const uint32_t base = atomicAdd(njobs, nb);
+    if (base >= jobs_cap || nb > jobs_cap - base) {
+        for (uint32_t i = base; i < jobs_cap && i - base < nb; i++)
+            jobs[i].f = kNoJob;
+        return;
+    }
+    const uint32_t info = bsid | ((flg >> 5) & 1) << 8;
+    p = hdr;
+    for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t q = p + 4 + (r32(p) & 0x7FFFFFFFu);
+        const uint32_t so = j ? (p >> 3) & ~3u : 0;
+        const uint32_t se = j + 1 < nb ? (q >> 3) & ~3u : slots_of(clen);
+        jobs[base + j] = BlockJob{f, p, q, so, se - so, info, j * max_block, 0};
+        p = q;
+    }
+    bfirst[f] = base;
+    bcount[f] = nb;
+}
+
 }   // namespace
 
 // ---- host side ---------------------------------------------------------------
@@ -129,8 +226,76 @@ void split_scratch_free(SplitScratch *s)
         (void)hipHostFree(s->total);
     if (s->redo)
         (void)hipFree(s->redo);
+    if (s->bfirst)
+        (void)hipFree(s->bfirst);
+    if (s->bcount)
+        (void)hipFree(s->bcount);
+    if (s->njobs)
+        (void)hipFree(s->njobs);
+    if (s->jobs)
+        (void)hipFree(s->jobs);
+    if (s->jres)
+        (void)hipFree(s->jres);
     *s = SplitScratch();
 }
+
+namespace {
+// block route scratch for (frames, jobs); stream-ordered like the rest
+int block_scratch_reserve(SplitScratch *s, uint32_t frames, uint32_t jobs, hipStream_t stream)
+{
+    if (!s->njobs && hipMalloc((void **)&s->njobs, sizeof(uint32_t)) != hipSuccess)
+        return -1;
+    if (frames > s->bframes_cap) {
+        const uint32_t cap = frames < 1024 ? 1024 : frames;
+        (void)hipStreamSynchronize(stream);
+        if (s->bfirst)
+            (void)hipFree(s->bfirst);
+        if (s->bcount)
+            (void)hipFree(s->bcount);
+        s->bfirst = s->bcount = nullptr;
+        s->bframes_cap = 0;
+        if (hipMalloc((void **)&s->bfirst, (size_t)cap * 4) != hipSuccess ||
+            hipMalloc((void **)&s->bcount, (size_t)cap * 4) != hipSuccess)
+            return -1;
+        s->bframes_cap = cap;
+    }
+    if (jobs > s->jobs_cap) {
+        (void)hipStreamSynchronize(stream);
+        if (s->jobs)
+            (void)hipFree(s->jobs);
+        if (s->jres)
+            (void)hipFree(s->jres);
+        s->jobs = nullptr;
+        s->jres = nullptr;
+        s->jobs_cap = 0;
+        if (hipMalloc((void **)&s->jobs, (size_t)jobs * sizeof(BlockJob)) != hipSuccess ||
+            hipMalloc((void **)&s->jres, (size_t)jobs * sizeof(BlockRes)) != hipSuccess)
+            return -1;
+        s->jobs_cap = jobs;
+    }
+    return 0;
+}
+
+// The block route for a batch: on (AUTO) for >= 1024 frames and < 32768 --
+// the batches whose big frames take the chunk parse (config 3: 4,096 frames
+// of 1 MiB, 16 blocks each) -- with frames of >= chunk_min compressed bytes,
+// used on the device only when >= 16,384 jobs were planned (fewer leave the
+// lean parse's lanes idle and the chunk parse wins); ROUTE_BLOCK forces it
+// for every frame and any job count.
+struct BlockRoute {
+    bool on;
+    uint32_t min_csize, min_jobs;
+};
+BlockRoute block_route(uint32_t nframes, int route, const ParseRoute &r)
+{
+    if (route == ROUTE_BLOCK)
+        return {true, 0, 1};
+    if (route != ROUTE_AUTO || nframes < 1024 || nframes >= 32768 || r.chunk_min == 0xFFFFFFFFu)
+        return {false, 0, 0};
+    return {true, r.chunk_min, 16384};
+}
+constexpr uint32_t kJobsCapMax = 1u << 21;
+}   // namespace
 
 int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipStream_t stream)
 {
@@ -260,7 +425,8 @@ ParseRoute parse_route(uint32_t nframes, int route)
     switch (route) {
     case ROUTE_LEAN: return {0xFFFFFFFFu, 0};
     case ROUTE_SCAN: return {0xFFFFFFFFu, 0xFFFFFFFFu};
-    case ROUTE_CHUNK: return {0, 0};
+    case ROUTE_CHUNK:
+    case ROUTE_BLOCK: return {0, 0};
     default: break;
     }
     const uint32_t cmin = chunk_parse_min(nframes);
@@ -288,6 +454,13 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
     uint64_t *total_dev = nullptr;
     (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
+    const ParseRoute r = parse_route(nframes, route);
+    BlockRoute br = block_route(nframes, route, r);
+    const uint64_t jw = (uint64_t)nframes * kMaxBlockJobs;
+    const uint32_t jlanes = (uint32_t)(jw < kJobsCapMax ? jw : kJobsCapMax);
+    if (br.on && block_scratch_reserve(s, nframes, jlanes, stream) != 0)
+        br.on = false;   // no room: the chunk parse takes the frames as before
+    SplitScratch *blk = br.on ? s : nullptr;
     stage_mark(0, stream);
     if (stages & 1) {
         (void)hipMemsetAsync(s->redo, 0, sizeof(uint32_t), stream);
@@ -295,12 +468,21 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                            d_desc, nframes, s->rec_base, total_dev, s->redo);
         hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
                            s->rec_base, total_dev, s->redo);
+        if (blk) {
+            (void)hipMemsetAsync(s->njobs, 0, sizeof(uint32_t), stream);
+            hipLaunchKernelGGL(lz4_block_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
+                               nframes, d_comp, br.min_csize, s->bfirst, s->bcount, s->njobs, s->jobs, jlanes);
+        }
     }
     stage_mark(1, stream);
     // parse: each kernel takes the frames of its compressed-size range and
-    // skips the others (launched only when the range is not empty)
-    const ParseRoute r = parse_route(nframes, route);
+    // skips the others (launched only when the range is not empty); block
+    // route jobs before the chunk parse, which accepts or re-parses their
+    // frames
     if (stages & 2) {
+        if (blk)
+            launch_lz4_lean_blocks(d_desc, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items, s, jlanes,
+                                   br.min_jobs, stream);
         if (r.chunk_min > r.lean_min)
             launch_lz4_lean(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
                             s->nitems, d_status, d_fail_at, stream, r.chunk_min, tune & 0xFF, r.lean_min);
@@ -309,12 +491,12 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                             s->nitems, d_status, d_fail_at, stream, r.lean_min < r.chunk_min ? r.lean_min : r.chunk_min);
         if (r.chunk_min != 0xFFFFFFFFu)
             launch_lz4_chunk(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                             s->nitems, d_status, d_fail_at, stream, r.chunk_min);
+                             s->nitems, d_status, d_fail_at, stream, r.chunk_min, blk, br.min_jobs);
     }
     stage_mark(2, stream);
     if (stages & 4)
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                        stream, (tune >> 8) & 0xFFF);
+                        stream, (tune >> 8) & 0xFFF, blk);
     stage_mark(3, stream);
     if (hipGetLastError() != hipSuccess) {
         stage_mark(4, stream);

@@ -376,12 +376,18 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // deal step; O(1) readiness pre-tests before the binary search; a persistent
 // grid with next-frame prefetch; nontemporal item / literal loads; 1, 2, 5 or
 // 8 waves per workgroup instead of kXW = 4.
-template <int DIAG, uint32_t OUTB>
+// SEG (the LZ4 block route): a frame with a job list (bfirst[f] != kNoJob)
+// has its items job by job -- job j's jres[j].n items at rec_base[f] +
+// jobs[j].slot_off -- read in block order as one sequence (a batch never
+// spans two jobs; the stage and output state carry over).
+template <int DIAG, uint32_t OUTB, bool SEG>
 __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
-    const int32_t *__restrict__ status, const uint8_t *__restrict__ lit)
+    const int32_t *__restrict__ status, const uint8_t *__restrict__ lit,
+    const uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
+    const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * x_wave(OUTB)];
     const uint32_t lane = threadIdx.x & 63;
@@ -397,11 +403,14 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
     if (fst == ST_NOT_RUN)
         return;
     const FrameDesc d = desc[f];
-    const uint32_t nit = uni(nitems[f]);
-    const uint64_t *it = items + rec_base[f];
-    // the frame's items as a buffer resource: loads past nit return 0
-    const __amdgpu_buffer_rsrc_t irs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)it, 0, (int)(nit * 8), kRsrcDw3);
+    uint32_t nit = uni(nitems[f]);
+    const uint64_t rb0 = rec_base[f];
+    uint32_t j0 = kNoJob, nseg = 1;
+    if (SEG) {
+        j0 = uni(bfirst[f]);
+        if (j0 != kNoJob)
+            nseg = uni(bcount[f]);
+    }
     Out O;
     O.o = out + d.d_off;
     O.dlen = d.d_size;
@@ -418,9 +427,6 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
     S.cb = 0xFFFFFFFFu;      // chunk -1 at index 0: chunk 0 starts at index 16
     uint32_t produced = 0;   // frame bytes decoded
     uint32_t fc = 0;         // output chunks [0, fc) are in HBM
-    uint64_t cur = lane < nit ? it[lane] : 0;
-    __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
-    uint32_t b = 0;
     uint64_t tsec[4] = {0, 0, 0, 0};
     uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tmark = (DIAG & 16) ? __builtin_readcyclecounter() : 0;
@@ -431,6 +437,20 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
         tsec[i] += tn - tmark;                                        \
         tmark = tn;                                                   \
     }
+    for (uint32_t sg = 0; sg < nseg; sg++) {
+    uint64_t ib = rb0;
+    if (SEG && j0 != kNoJob) {
+        ib += jobs[j0 + sg].slot_off;
+        nit = uni(jres[j0 + sg].n);
+    }
+    const uint64_t *it = items + ib;
+    // the items as a buffer resource: loads past nit return 0
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)it, 0, (int)(nit * 8), kRsrcDw3);
+    uint64_t cur = lane < nit ? it[lane] : 0;
+    __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
+    uint32_t b = 0;
+    const bool last_seg = sg + 1 == nseg;
     while (b < nit) {
         const uint64_t nxt =
             __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, 8 * (b + 64 + lane), 0, 0));
@@ -573,7 +593,7 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
             cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
         }
         // flush complete chunks (the frame's last chunk exactly)
-        const bool last = b + nb >= nit;
+        const bool last = last_seg && b + nb >= nit;
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
         if (!(DIAG & 34))
             flush_chunks4<DIAG>(S, O, fc, end_c, lane);
@@ -592,6 +612,7 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
         b += nb;
         ZSK_T(3)
     }
+    }
 #undef ZSK_T
     if ((DIAG & 16) && lane == 0)
         for (int i = 0; i < 4; i++)
@@ -608,14 +629,20 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                    int version)
+                    int version, const SplitScratch *blk)
 {
     if (nframes == 0)
         return 0;
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
-#define ZSK_X(D)                                                                                   \
-    hipLaunchKernelGGL((seq_exec_kernel<D, 4096>), grid, block, 0, stream, d_desc, nframes, d_comp, \
-                       d_out, rec_base, items, nitems, d_status, nullptr)
+    if (blk) {   // the block route (production kernel only)
+        hipLaunchKernelGGL((seq_exec_kernel<0, 4096, true>), grid, block, 0, stream, d_desc, nframes, d_comp,
+                           d_out, rec_base, items, nitems, d_status, nullptr, blk->bfirst, blk->bcount,
+                           blk->jobs, blk->jres);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+#define ZSK_X(D)                                                                                          \
+    hipLaunchKernelGGL((seq_exec_kernel<D, 4096, false>), grid, block, 0, stream, d_desc, nframes, d_comp, \
+                       d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr)
 #ifdef ZSK_TUNING
     switch (version) {
     case 0x101: ZSK_X(1); break;
@@ -653,8 +680,9 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL((seq_exec_kernel<0, 4096>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
-                       stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit);
+    hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
+                       stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit, nullptr,
+                       nullptr, nullptr, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

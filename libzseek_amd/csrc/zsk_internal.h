@@ -64,7 +64,9 @@ const char *lz4_kernel_name(uint32_t nframes);
 // Production decoders a batch can be forced through (tests; ROUTE_AUTO is the
 // library's own choice).  LEAN / SCAN / CHUNK: the two-phase decoder with that
 // parse for every frame.
-enum : int { ROUTE_AUTO = 0, ROUTE_WAVE = 1, ROUTE_LEAN = 2, ROUTE_SCAN = 3, ROUTE_CHUNK = 4 };
+// BLOCK: every multi-block-capable frame through the block route below (any
+// batch size, no job minimum).
+enum : int { ROUTE_AUTO = 0, ROUTE_WAVE = 1, ROUTE_LEAN = 2, ROUTE_SCAN = 3, ROUTE_CHUNK = 4, ROUTE_BLOCK = 5 };
 
 // Launch the LZ4 frame decoder over nframes frames (asynchronous on stream).
 // d_fail_at (optional) receives, per frame, the output offset of the block
@@ -75,6 +77,33 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
 
 // Scratch of the two-phase decoder (lz4_split.hip): per-frame item slot
 // offsets and counts, and the items themselves (one u32 per LZ4 sequence).
+// Block route (big multi-block frames): the block plan walks
+// each eligible frame's block headers and gives every LZ4 block a job; the
+// lean parse takes one lane per job at the output offset the block would
+// start at if every block before it decodes to the frame's maximum block size
+// (what LZ4F writers produce); the chunk parse accepts a frame whose jobs all
+// parsed cleanly at those offsets and re-parses any other; the execute reads
+// an accepted frame's items block by block.
+struct BlockJob {
+    uint32_t f;          // frame, or kNoJob: a slot no lane parses
+    uint32_t hpos;       // block header, frame-relative
+    uint32_t stop;       // the next header (hpos + 4 + block size)
+    uint32_t slot_off;   // the job's item slots, relative to rec_base[f]
+    uint32_t slot_cap;
+    uint32_t info;       // block size id | independent blocks << 8
+    uint32_t bop;        // speculative output offset (job index x max block)
+    uint32_t pad;
+};
+struct BlockRes {
+    uint32_t n;    // items
+    uint32_t op;   // output offset the block ended at
+    int32_t st;    // ST_OK: parsed up to `stop`, every rule checked
+    uint32_t pad;
+};
+static_assert(sizeof(BlockJob) == 32 && sizeof(BlockRes) == 16, "block job layout");
+constexpr uint32_t kNoJob = 0xFFFFFFFFu;
+constexpr uint32_t kMaxBlockJobs = 64;   // blocks per frame the route takes
+
 struct SplitScratch {
     uint64_t *rec_base = nullptr;   // [frames_cap]
     uint32_t *nitems = nullptr;     // [frames_cap]
@@ -83,6 +112,13 @@ struct SplitScratch {
     uint32_t *redo = nullptr;      // device flag: frames out of order, slots by scan
     uint32_t frames_cap = 0;
     uint64_t items_cap = 0;
+    // block route (allocated on first use)
+    uint32_t *bfirst = nullptr;     // [bframes_cap] first job of frame f, or kNoJob
+    uint32_t *bcount = nullptr;     // [bframes_cap]
+    uint32_t *njobs = nullptr;      // device counter
+    BlockJob *jobs = nullptr;       // [jobs_cap]
+    BlockRes *jres = nullptr;       // [jobs_cap]
+    uint32_t bframes_cap = 0, jobs_cap = 0;
 };
 
 // Item slots frame descriptors need (host-side mirror of the plan kernel).
@@ -137,10 +173,12 @@ int lz4_pick_engine(uint32_t nframes);   // never ENGINE_AUTO
 // Execute phase (seq_exec.hip): one wave per frame, linear per-wave LDS
 // stage, DPP scans, piece descriptors.  version: tuning builds only (0 = the
 // production kernel).
+// With `blk` (the block route's scratch), frames with a job list read their
+// items job by job.
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                    int version = 0);
+                    int version = 0, const SplitScratch *blk = nullptr);
 
 // Execute phase over items whose literal runs come from a literal scratch
 // laid out like the output (zstd): frame f's literals at lit + d_off[f].
@@ -206,13 +244,22 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 // (its direct item stores beat the lean kernel's line flush on short frames:
 // 4 KiB frames 5.68 vs 6.71 ms per launch, config 3)
 constexpr uint32_t kLeanMinCsize = 12288;
+// Block route parse: lane per job of s->jobs (the first *s->njobs), all
+// lanes idle when fewer than min_jobs jobs were planned.
+int launch_lz4_lean_blocks(const FrameDesc *d_desc, const uint8_t *d_comp, const uint64_t *rec_base,
+                           uint64_t capacity, uint64_t *items, const SplitScratch *s, uint32_t lanes,
+                           uint32_t min_jobs, hipStream_t stream);
 
 // Parse phase, one wave per frame, chunk-parallel (lz4_chunk.hip): the same
 // outputs as launch_lz4_scan for the frames of min_csize compressed bytes and
 // more (other frames are left to lz4_scan_kernel), items without padding.
+// With `blk`: a frame with a job list is accepted from its jobs' results
+// (when at least min_jobs were planned and every job parsed cleanly at its
+// speculative offset) or parsed here, its job list dropped.
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
-                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize);
+                     int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
+                     SplitScratch *blk = nullptr, uint32_t min_jobs = 0);
 // Frames of at least chunk_parse_min(nframes) compressed bytes go to the
 // chunk parse: with >= 32768 frames the lane-per-frame scan has a lane for
 // every frame it needs and wins on 64 KiB frames (2.07 vs 4.18 ms parse at
