@@ -286,11 +286,16 @@ struct BlockRoute {
     bool on;
     uint32_t min_csize, min_jobs;
 };
+// Env ZSEEK_BLOCK_ROUTE=0 turns the automatic choice off (A/B runs).
 BlockRoute block_route(uint32_t nframes, int route, const ParseRoute &r)
 {
+    static const bool off = [] {
+        const char *v = getenv("ZSEEK_BLOCK_ROUTE");
+        return v && !strcmp(v, "0");
+    }();
     if (route == ROUTE_BLOCK)
         return {true, 0, 1};
-    if (route != ROUTE_AUTO || nframes < 1024 || nframes >= 32768 || r.chunk_min == 0xFFFFFFFFu)
+    if (off || route != ROUTE_AUTO || nframes < 1024 || nframes >= 32768 || r.chunk_min == 0xFFFFFFFFu)
         return {false, 0, 0};
     return {true, r.chunk_min, 16384};
 }
@@ -438,6 +443,11 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route)
     if (lz4_pick_engine(nframes) == ENGINE_WAVE && route == ROUTE_AUTO)
         return "lz4_wave_kernel";
     const ParseRoute r = parse_route(nframes, route);
+    // (block route: frames of > 64 KiB decoded; named for the compressed
+    // sizes those frames have)
+    const BlockRoute br = block_route(nframes, route, r);
+    if (br.on && c_size >= br.min_csize && c_size >= 65536)
+        return "lz4_lean_kernel (block route)";
     if (c_size >= r.chunk_min)
         return "lz4_chunk_kernel";
     return c_size >= r.lean_min ? "lz4_lean_kernel" : "lz4_scan_kernel";

@@ -376,12 +376,96 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // deal step; O(1) readiness pre-tests before the binary search; a persistent
 // grid with next-frame prefetch; nontemporal item / literal loads; 1, 2, 5 or
 // 8 waves per workgroup instead of kXW = 4.
+// Item addressing of the execute: contiguous items (JobMap<false>), or the
+// block route's job segments (JobMap<true>, below).
+template <bool SEG>
+struct JobMap {
+    __device__ __forceinline__ uint32_t init(const uint32_t *, const uint32_t *, const BlockJob *,
+                                             const BlockRes *, uint32_t, const uint32_t *, uint32_t, uint32_t,
+                                             uint32_t &)
+    {
+        return 0;
+    }
+    __device__ __forceinline__ uint32_t addr(uint32_t i0, uint32_t lane, uint32_t) const
+    {
+        return 8 * (i0 + lane);
+    }
+};
+
+template <>
+struct JobMap<true> {
+    uint32_t jtab = 0;   // LDS: entry j = {job j's first item index, its slot offset - that index}
+    uint32_t nseg = 0;   // jobs (0: contiguous items)
+    // cursor: the job of the window's first index, the next job's first
+    // index, both offsets (uniform)
+    uint32_t cs = 0, s_next = 0xFFFFFFFFu, d_cur = 0, d_next = 0;
+
+    // the table from frame f's jobs; returns the frame's item count (their
+    // total), span = the item slots its resource must cover
+    __device__ __forceinline__ uint32_t init(const uint32_t *bfirst, const uint32_t *bcount, const BlockJob *jobs,
+                                             const BlockRes *jres, uint32_t f, const uint32_t *nitems,
+                                             uint32_t tab, uint32_t lane, uint32_t &span)
+    {
+        const uint32_t j0 = uni(bfirst[f]);
+        if (j0 == kNoJob) {
+            span = uni(nitems[f]);
+            return span;
+        }
+        jtab = tab;
+        nseg = uni(bcount[f]);
+        uint32_t so = 0, nj = 0;
+        if (lane < nseg) {
+            so = jobs[j0 + lane].slot_off;
+            nj = jres[j0 + lane].n;
+        }
+        const uint32_t inc = wave_incl_add(nj);
+        if (lane <= nseg)
+            *lp<uint64_t>(jtab + 8 * lane) =
+                lane < nseg ? ((uint64_t)(so - (inc - nj)) << 32) | (inc - nj) : 0xFFFFFFFFull;
+        span = uni(lane_val(so + nj, (int)nseg - 1));
+        wave_lds_sync();
+        const uint64_t e0 = *lp<uint64_t>(jtab), e1 = *lp<uint64_t>(jtab + 8);
+        d_cur = uni((uint32_t)(e0 >> 32));
+        s_next = uni((uint32_t)e1);
+        d_next = uni((uint32_t)(e1 >> 32));
+        return uni(lane_val(inc, 63));
+    }
+
+    // byte offset of item index i = i0 + lane (past nit: out of range); i0
+    // never decreases
+    __device__ __forceinline__ uint32_t addr(uint32_t i0, uint32_t lane, uint32_t nit)
+    {
+        const uint32_t i = i0 + lane;
+        if (nseg == 0)
+            return 8 * i;
+        while (s_next <= i0) {   // the window starts in a later job
+            cs++;
+            d_cur = d_next;
+            const uint64_t e = *lp<uint64_t>(jtab + 8 * (cs + 1));
+            s_next = uni((uint32_t)e);
+            d_next = uni((uint32_t)(e >> 32));
+        }
+        uint32_t d = d_cur;
+        for (uint32_t k = cs + 1, sk = s_next, dk = d_next; sk <= i0 + 63;) {   // jobs starting inside it
+            d = i >= sk ? dk : d;
+            const uint64_t e = *lp<uint64_t>(jtab + 8 * (++k));
+            sk = uni((uint32_t)e);
+            dk = uni((uint32_t)(e >> 32));
+        }
+        return i < nit ? 8 * (i + d) : 0x7FFFFFF0u;
+    }
+};
+
 // SEG (the LZ4 block route): a frame with a job list (bfirst[f] != kNoJob)
 // has its items job by job -- job j's jres[j].n items at rec_base[f] +
-// jobs[j].slot_off -- read in block order as one sequence (a batch never
-// spans two jobs; the stage and output state carry over).
+// jobs[j].slot_off -- read in block order as one sequence: lane j holds job
+// j's first item index in that sequence and its slot offset (a 512-byte LDS
+// table per wave), and each lane maps the item index it loads onto its job's
+// slots with a uniform job cursor, so batches run across jobs unchanged.
+// (SEG runs at 4 waves per SIMD: its batches have <= 32,767 frames -- config
+// 3's 4,096 fill 4 per SIMD -- and the job cursor's registers fit no spill)
 template <int DIAG, uint32_t OUTB, bool SEG>
-__global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) void seq_exec_kernel(
+__global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 4 : 5))) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
@@ -389,7 +473,7 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
     const uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
     const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * x_wave(OUTB)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * x_wave(OUTB) + (SEG ? kXW * 8 * 65 : 0)];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t f = uni(blockIdx.x * kXW + w);
@@ -403,14 +487,15 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
     if (fst == ST_NOT_RUN)
         return;
     const FrameDesc d = desc[f];
-    uint32_t nit = uni(nitems[f]);
-    const uint64_t rb0 = rec_base[f];
-    uint32_t j0 = kNoJob, nseg = 1;
-    if (SEG) {
-        j0 = uni(bfirst[f]);
-        if (j0 != kNoJob)
-            nseg = uni(bcount[f]);
-    }
+    JobMap<SEG> J;
+    uint32_t ispan = 0;   // item slots the resource covers (SEG)
+    const uint32_t nit = SEG ? J.init(bfirst, bcount, jobs, jres, f, nitems,
+                                      (uint32_t)(uintptr_t)(lds + kXW * x_wave(OUTB)) + w * 8 * 65, lane, ispan)
+                             : uni(nitems[f]);
+    const uint64_t *it = items + rec_base[f];
+    // the frame's items as a buffer resource: loads past nit return 0
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)it, 0, (int)((SEG ? ispan : nit) * 8), kRsrcDw3);
     Out O;
     O.o = out + d.d_off;
     O.dlen = d.d_size;
@@ -427,6 +512,13 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
     S.cb = 0xFFFFFFFFu;      // chunk -1 at index 0: chunk 0 starts at index 16
     uint32_t produced = 0;   // frame bytes decoded
     uint32_t fc = 0;         // output chunks [0, fc) are in HBM
+    uint64_t cur;
+    if constexpr (SEG)
+        cur = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, J.addr(0, lane, nit), 0, 0));
+    else
+        cur = lane < nit ? it[lane] : 0;
+    __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
+    uint32_t b = 0;
     uint64_t tsec[4] = {0, 0, 0, 0};
     uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tmark = (DIAG & 16) ? __builtin_readcyclecounter() : 0;
@@ -437,23 +529,9 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
         tsec[i] += tn - tmark;                                        \
         tmark = tn;                                                   \
     }
-    for (uint32_t sg = 0; sg < nseg; sg++) {
-    uint64_t ib = rb0;
-    if (SEG && j0 != kNoJob) {
-        ib += jobs[j0 + sg].slot_off;
-        nit = uni(jres[j0 + sg].n);
-    }
-    const uint64_t *it = items + ib;
-    // the items as a buffer resource: loads past nit return 0
-    const __amdgpu_buffer_rsrc_t irs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)it, 0, (int)(nit * 8), kRsrcDw3);
-    uint64_t cur = lane < nit ? it[lane] : 0;
-    __builtin_amdgcn_s_waitcnt(0);   // cur in registers before the loop: its waits then leave nxt in flight
-    uint32_t b = 0;
-    const bool last_seg = sg + 1 == nseg;
     while (b < nit) {
         const uint64_t nxt =
-            __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, 8 * (b + 64 + lane), 0, 0));
+            __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, J.addr(b + 64, lane, nit), 0, 0));
         const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
         const uint32_t w0n = dpp_next(w0, 0), w1n = dpp_next(w1, 0);
         const uint32_t w0p = dpp_prev(w0, 0);
@@ -593,7 +671,7 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
             cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
         }
         // flush complete chunks (the frame's last chunk exactly)
-        const bool last = last_seg && b + nb >= nit;
+        const bool last = b + nb >= nit;
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
         if (!(DIAG & 34))
             flush_chunks4<DIAG>(S, O, fc, end_c, lane);
@@ -612,7 +690,6 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
         b += nb;
         ZSK_T(3)
     }
-    }
 #undef ZSK_T
     if ((DIAG & 16) && lane == 0)
         for (int i = 0; i < 4; i++)
@@ -624,6 +701,21 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(5))) v
 
 }   // namespace
 
+#ifdef ZSK_EXEC_SEG_TU
+// seq_exec_seg.hip: the block route's instantiation, compiled on its own (in
+// one module with the production kernel it cost that kernel a VGPR spill)
+int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                        const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
+                        const int32_t *d_status, hipStream_t stream, const SplitScratch *blk)
+{
+    if (nframes == 0)
+        return 0;
+    hipLaunchKernelGGL((seq_exec_kernel<0, 4096, true>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0, stream,
+                       d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status, nullptr, blk->bfirst,
+                       blk->bcount, blk->jobs, blk->jres);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#else
 // version: 0 = the production kernel; tuning builds add diagnostics
 // (DIAG bits above) as 0x100 | DIAG.
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
@@ -633,13 +725,9 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 {
     if (nframes == 0)
         return 0;
+    if (blk)   // the block route (production kernel only)
+        return launch_seq_exec_seg(d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status, stream, blk);
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
-    if (blk) {   // the block route (production kernel only)
-        hipLaunchKernelGGL((seq_exec_kernel<0, 4096, true>), grid, block, 0, stream, d_desc, nframes, d_comp,
-                           d_out, rec_base, items, nitems, d_status, nullptr, blk->bfirst, blk->bcount,
-                           blk->jobs, blk->jres);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
 #define ZSK_X(D)                                                                                          \
     hipLaunchKernelGGL((seq_exec_kernel<D, 4096, false>), grid, block, 0, stream, d_desc, nframes, d_comp, \
                        d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr)
@@ -685,5 +773,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
                        nullptr, nullptr, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#endif
 
 }   // namespace zsk

@@ -179,6 +179,9 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
                     int version = 0, const SplitScratch *blk = nullptr);
+int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                        const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
+                        const int32_t *d_status, hipStream_t stream, const SplitScratch *blk);
 
 // Execute phase over items whose literal runs come from a literal scratch
 // laid out like the output (zstd): frame f's literals at lit + d_off[f].
