@@ -419,9 +419,10 @@ struct JobMap<true> {
             nj = jres[j0 + lane].n;
         }
         const uint32_t inc = wave_incl_add(nj);
-        if (lane <= nseg)
-            *lp<uint64_t>(jtab + 8 * lane) =
-                lane < nseg ? ((uint64_t)(so - (inc - nj)) << 32) | (inc - nj) : 0xFFFFFFFFull;
+        if (lane < nseg)
+            *lp<uint64_t>(jtab + 8 * lane) = ((uint64_t)(so - (inc - nj)) << 32) | (inc - nj);
+        if (lane == 0)   // the end entry (index 64 for 64 jobs: no lane of its own)
+            *lp<uint64_t>(jtab + 8 * nseg) = 0xFFFFFFFFull;
         span = uni(lane_val(so + nj, (int)nseg - 1));
         wave_lds_sync();
         const uint64_t e0 = *lp<uint64_t>(jtab), e1 = *lp<uint64_t>(jtab + 8);
