@@ -205,10 +205,14 @@ struct ZstdScratch {
     uint8_t *hjobs = nullptr;      // Huffman stream jobs, 4 per block, 32 B each
     uint8_t *slots = nullptr;      // per-block decoding tables (kZSlot bytes each)
     uint8_t *hbad = nullptr;       // per Huffman stream: 1 = corrupt
-    uint64_t *d_total = nullptr;   // [0] item total, [1] output extent, [2] blocks
+    // [0] item total, [1] output extent, [2] blocks, [3] -, [4 + k] blk_base
+    // at chunk boundary k (zstd_decode.hip: the decode runs in chunks)
+    uint64_t *d_total = nullptr;
     uint64_t *total = nullptr;     // pinned host copy of d_total
     hipStream_t side = nullptr;    // the Huffman kernel's stream (beside the sequence replay)
-    hipEvent_t ev_tab = nullptr, ev_huf = nullptr;
+    hipStream_t sq = nullptr;      // the sequence kernel's stream
+    static constexpr int kChunks = 8;   // most chunks a decode runs in
+    hipEvent_t ev_f[kChunks] = {}, ev_s[kChunks] = {}, ev_h[kChunks] = {};   // per chunk: frame / seq / Huffman done
     int side_dev = -1;   // the device the side set belongs to (pooled, zstd_decode.hip)
     uint32_t frames_cap = 0;
     uint64_t lit_cap = 0, items_cap = 0, blocks_cap = 0, ops_cap = 0;

@@ -1186,11 +1186,11 @@ __global__ __launch_bounds__(64 * kZW) __attribute__((amdgpu_waves_per_eu(4))) v
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ lit, uint64_t lit_cap, const uint64_t *__restrict__ rec_base,
     uint64_t capacity, const uint64_t *__restrict__ blk_base, uint8_t *__restrict__ ops,
-    uint8_t *__restrict__ slots, uint8_t *__restrict__ jobs)
+    uint8_t *__restrict__ slots, uint8_t *__restrict__ jobs, uint32_t f0)
 {
     __shared__ ZLds lds[kZW];
     const uint32_t w = threadIdx.x >> 6;
-    const uint32_t f = uni(blockIdx.x * kZW + w);
+    const uint32_t f = uni(f0 + blockIdx.x * kZW + w);   // frames [f0, n)
     if (f >= n)
         return;
     ZLds &L = lds[w];
@@ -1736,7 +1736,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
     const uint8_t *__restrict__ slots, uint32_t *__restrict__ stop,
     const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
-    int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at)
+    int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at, uint32_t f0)
 {
     __shared__ uint32_t codes[89];
     __shared__ __attribute__((aligned(16))) uint16_t ftab[CELLS ? LANES * CELLS : 8];
@@ -1744,7 +1744,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
     __syncthreads();
     const uint32_t lane = threadIdx.x;
-    const uint32_t f = blockIdx.x * LANES + lane;
+    const uint32_t f = f0 + blockIdx.x * LANES + lane;   // frames [f0, n)
     const bool act = lane < LANES && f < n;
     FrameDesc d = {0, 0, 0, 0};
     if (act)
@@ -1973,9 +1973,9 @@ __global__ __launch_bounds__(256) void zstd_lit_fix_kernel(uint32_t n, const uin
                                                            const uint32_t *__restrict__ stop,
                                                            int32_t *__restrict__ status,
                                                            uint32_t *__restrict__ nitems,
-                                                           uint32_t *__restrict__ fail_at)
+                                                           uint32_t *__restrict__ fail_at, uint32_t f0)
 {
-    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t f = f0 + blockIdx.x * 256 + threadIdx.x;   // frames [f0, n)
     if (f >= n)
         return;
     const ZOp *op = reinterpret_cast<const ZOp *>(ops) + op_base(blk_base, f);
@@ -2093,6 +2093,15 @@ __global__ __launch_bounds__(256) void zstd_check_kernel(const FrameDesc *__rest
 
 }   // namespace
 
+// blk_base at the decode's chunk boundaries (zstd_chunks) -> out[0..k]
+__global__ void zstd_bounds_kernel(const uint64_t *__restrict__ blk_base, uint32_t n, uint32_t k,
+                                   uint64_t *__restrict__ out)
+{
+    const uint32_t c = threadIdx.x;
+    if (c <= k)
+        out[c] = blk_base[(uint64_t)n * c / k];
+}
+
 // ---- host side -----------------------------------------------------------------------------------
 
 namespace {
@@ -2116,39 +2125,56 @@ int grow(T **p, uint64_t &cap, uint64_t want, uint64_t unit)
 // its events and before the caller's stream goes: the side stream's wait on
 // an event recorded on the caller's stream is released while that stream is
 // still alive.
+void side_destroy(ZstdScratch *s)
+{
+    for (hipStream_t *q : {&s->side, &s->sq})
+        if (*q) {
+            (void)hipStreamSynchronize(*q);
+            (void)hipStreamDestroy(*q);
+            *q = nullptr;
+        }
+    for (int c = 0; c < ZstdScratch::kChunks; c++)
+        for (hipEvent_t *e : {&s->ev_f[c], &s->ev_s[c], &s->ev_h[c]})
+            if (*e) {
+                (void)hipEventDestroy(*e);
+                *e = nullptr;
+            }
+}
+
 int side_create(ZstdScratch *s)
 {
-    // the side stream at the lowest priority: the sequence kernel, the longer
-    // of the two, gets the CUs' LDS first (10.9 -> 10.6 ms per launch at
-    // config 5; launching the sequence kernel first made no difference)
+    // the Huffman stream at the lowest priority: the sequence kernel, the
+    // longer of the two, gets the CUs' LDS first (10.9 -> 10.6 ms per launch
+    // at config 5; launching the sequence kernel first made no difference)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     (void)hipGetDevice(&s->side_dev);
-    if (hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, lo) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_tab, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_huf, hipEventDisableTiming) != hipSuccess) {
-        // partly created, nothing recorded on it yet
-        if (s->ev_tab)
-            (void)hipEventDestroy(s->ev_tab);
-        if (s->side)
-            (void)hipStreamDestroy(s->side);
-        s->side = nullptr;
-        s->ev_tab = s->ev_huf = nullptr;
+    bool ok = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, lo) == hipSuccess &&
+              hipStreamCreateWithFlags(&s->sq, hipStreamNonBlocking) == hipSuccess;
+    for (int c = 0; ok && c < ZstdScratch::kChunks; c++)
+        ok = hipEventCreateWithFlags(&s->ev_f[c], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&s->ev_s[c], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&s->ev_h[c], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {   // partly created, nothing recorded on it yet
+        side_destroy(s);
         return -1;
     }
     return 0;
 }
 
-void side_destroy(ZstdScratch *s)
+// Chunks a decode of n frames runs in (frames [n c / k, n (c + 1) / k)): the
+// frame kernel of chunk c + 1 and the execute of chunk c - 1 run beside the
+// sequence and Huffman kernels of chunk c, which leave most of each CU's
+// issue slots idle.  Env ZSEEK_ZSTD_CHUNKS (A/B runs).
+uint32_t zstd_chunks(uint32_t n)
 {
-    if (!s->side)
-        return;
-    (void)hipStreamSynchronize(s->side);
-    (void)hipStreamDestroy(s->side);
-    (void)hipEventDestroy(s->ev_tab);
-    (void)hipEventDestroy(s->ev_huf);
-    s->side = nullptr;
-    s->ev_tab = s->ev_huf = nullptr;
+    static const int forced = getenv("ZSEEK_ZSTD_CHUNKS") ? atoi(getenv("ZSEEK_ZSTD_CHUNKS")) : 0;
+    uint32_t k = n >= 16384 ? 4 : n >= 4096 ? 2 : 1;
+    if (forced > 0)
+        k = (uint32_t)forced;
+    if (k > (uint32_t)ZstdScratch::kChunks)
+        k = ZstdScratch::kChunks;
+    return k > n ? (n ? n : 1) : k;
 }
 }   // namespace
 
@@ -2176,8 +2202,9 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
             hipMalloc((void **)&s->nitems, sizeof(uint32_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->ck, sizeof(uint64_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->stop, sizeof(uint32_t) * cap) != hipSuccess ||
-            hipMalloc((void **)&s->d_total, 4 * sizeof(uint64_t)) != hipSuccess ||
-            hipHostMalloc((void **)&s->total, 4 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
+            hipMalloc((void **)&s->d_total, (5 + ZstdScratch::kChunks) * sizeof(uint64_t)) != hipSuccess ||
+            hipHostMalloc((void **)&s->total, (5 + ZstdScratch::kChunks) * sizeof(uint64_t), hipHostMallocDefault) !=
+                hipSuccess)
             return -1;
         s->total[0] = s->total[1] = s->total[2] = 0;
         s->frames_cap = cap;
@@ -2222,16 +2249,22 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                        nframes, d_comp, s->bound, s->bblk, reinterpret_cast<unsigned long long *>(s->d_total + 1));
     hipLaunchKernelGGL(zstd_scan_kernel, dim3(1), dim3(1024), 0, stream, s->bound, s->bblk, nframes,
                        s->rec_base, s->blk_base, s->d_total);
+    const uint32_t k = zstd_chunks(nframes);
+    hipLaunchKernelGGL(zstd_bounds_kernel, dim3(1), dim3(64), 0, stream, s->blk_base, nframes, k, s->d_total + 4);
     if (hipGetLastError() != hipSuccess)
         return -1;
-    return hipMemcpyAsync(s->total, s->d_total, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) ==
+    return hipMemcpyAsync(s->total, s->d_total, (5 + k) * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) ==
                    hipSuccess
                ? 0
                : -1;
 }
 
-// Frame kernel -> Huffman kernel -> sequence kernel -> execute -> checksums,
-// back to back on the stream.  s must hold the last plan of these frames.
+// Frame kernel -> Huffman kernel beside the sequence kernel -> literal fix-up
+// -> execute -> checksums, in zstd_chunks(n) chunks of frames pipelined over
+// three streams: the caller's stream runs every chunk's frame kernel, then
+// each chunk's fix-up, execute and checksums once its sequence (s->sq) and
+// Huffman (s->side) kernels are done; those start on a chunk as soon as its
+// frame kernel is.  s must hold the last plan of these frames.
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
                        uint32_t *d_fail_at)
@@ -2241,67 +2274,88 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     const uint64_t blocks = s->total[2];
     if (blocks > s->blocks_cap)
         return -1;
-    const uint32_t nj = (uint32_t)(4 * blocks);
-    if (nj && hipMemsetAsync(s->hjobs, 0, (size_t)nj * sizeof(HufJob), stream) != hipSuccess)
+    const uint32_t K = zstd_chunks(nframes);
+    static const bool serial = getenv("ZSEEK_ZSTD_SERIAL") != nullptr;   // diagnostics: one stream
+    hipStream_t const hs = serial ? stream : s->side, qs = serial ? stream : s->sq;
+    static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
+    if (blocks && hipMemsetAsync(s->hjobs, 0, (size_t)(4 * blocks) * sizeof(HufJob), stream) != hipSuccess)
         return -1;
-    hipLaunchKernelGGL(zstd_frame_kernel, dim3((nframes + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc,
-                       nframes, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops,
-                       s->slots, s->hjobs);
-    // the Huffman streams decode on a side stream beside the sequence replay
-    // (neither reads the other's output); zstd_lit_fix_kernel joins them
-    auto seq = [&] {
-        hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells>), dim3((nframes + kSeqLanes - 1) / kSeqLanes),
-                           dim3(64), 0, stream, d_desc, nframes, d_comp, s->ops, s->blk_base, s->slots, s->stop,
-                           s->rec_base, s->items, s->nitems, d_status, s->ck, d_fail_at);
+    auto drain = [&] {   // an enqueue failed: nothing may still write the scratch
+        (void)hipStreamSynchronize(stream);
+        (void)hipStreamSynchronize(s->side);
+        (void)hipStreamSynchronize(s->sq);
+        return -1;
     };
-    if (nj) {
-        if (hipEventRecord(s->ev_tab, stream) != hipSuccess || hipStreamWaitEvent(s->side, s->ev_tab, 0) != hipSuccess)
-            return -1;
-        static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
-        const dim3 g((nj + 63) / 64), b(64);
-        static const bool serial = getenv("ZSEEK_ZSTD_SERIAL") != nullptr;   // diagnostics: one stream
-        hipStream_t const hs = serial ? stream : s->side;
-        if (diag) {
-            unsigned int z[32] = {};
-            (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+    auto bnd = [&](uint32_t c) { return (uint32_t)((uint64_t)nframes * c / K); };
+    for (uint32_t c = 0; c < K; c++) {
+        const uint32_t f0 = bnd(c), f1 = bnd(c + 1), m = f1 - f0;
+        if (m == 0)
+            continue;
+        const uint64_t b0 = s->total[4 + c], b1 = s->total[5 + c];
+        hipLaunchKernelGGL(zstd_frame_kernel, dim3((m + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc, f1,
+                           d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops, s->slots,
+                           s->hjobs, f0);
+        if (hipEventRecord(s->ev_f[c], stream) != hipSuccess || hipStreamWaitEvent(qs, s->ev_f[c], 0) != hipSuccess)
+            return drain();
+        // the Huffman streams decode beside the sequence replay (neither reads
+        // the other's output); zstd_lit_fix_kernel joins them
+        const uint32_t nj = (uint32_t)(4 * (b1 - b0));
+        if (nj) {
+            if (hipStreamWaitEvent(hs, s->ev_f[c], 0) != hipSuccess)
+                return drain();
+            if (diag) {
+                unsigned int z[32] = {};
+                (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, hs);
+            }
+            const uint8_t *jb = s->hjobs + 4 * b0 * sizeof(HufJob);
+            uint8_t *hb = s->hbad + 4 * b0;
+            const dim3 g((nj + 63) / 64), b(64);
+            switch (diag) {
+            case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
+            case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
+            case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
+            case 7: hipLaunchKernelGGL(zstd_huf_kernel<7>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
+            default: hipLaunchKernelGGL(zstd_huf_kernel<8>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
+            }
+            if (diag) {
+                unsigned int z[32] = {};
+                (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_hdiag), sizeof(z), 0, hipMemcpyDeviceToHost, hs);
+                (void)hipStreamSynchronize(hs);
+                fprintf(stderr, "huf diag %d (chunk %u): lgmax", diag, c);
+                for (int i = 0; i < 16; i++)
+                    if (z[i])
+                        fprintf(stderr, " %d:%u", i, z[i]);
+                fprintf(stderr, "  global %u lds %u\n", z[16], z[17]);
+            }
+            if (hipEventRecord(s->ev_h[c], hs) != hipSuccess)
+                return drain();
         }
-        switch (diag) {
-        case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        case 7: hipLaunchKernelGGL(zstd_huf_kernel<7>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        default: hipLaunchKernelGGL(zstd_huf_kernel<8>, g, b, 0, hs, s->hjobs, nj, d_comp, s->slots, s->lit, s->hbad); break;
-        }
-        if (diag) {
-            unsigned int z[32] = {};
-            (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_hdiag), sizeof(z), 0, hipMemcpyDeviceToHost, hs);
-            (void)hipStreamSynchronize(hs);
-            fprintf(stderr, "huf diag %d: lgmax", diag);
-            for (int i = 0; i < 16; i++)
-                if (z[i])
-                    fprintf(stderr, " %d:%u", i, z[i]);
-            fprintf(stderr, "  global %u lds %u\n", z[16], z[17]);
-        }
-        if (hipEventRecord(s->ev_huf, hs) != hipSuccess) {
-            (void)hipStreamSynchronize(hs);   // the kernel may still write lit / hbad
-            return -1;
-        }
-    }
-    seq();
-    if (nj) {
-        if (hipStreamWaitEvent(stream, s->ev_huf, 0) != hipSuccess) {
-            (void)hipStreamSynchronize(s->side);
-            return -1;
-        }
-        hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, nframes, s->ops,
-                           s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at);
+        hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
+                           qs, d_desc, f1, d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items,
+                           s->nitems, d_status, s->ck, d_fail_at, f0);
+        if (hipEventRecord(s->ev_s[c], qs) != hipSuccess)
+            return drain();
     }
     stage_mark(2, stream);
-    const int rc = launch_seq_exec_lit(d_desc, nframes, s->lit, d_out, s->rec_base, s->items,
-                                       s->nitems, d_status, stream);
+    int rc = 0;
+    for (uint32_t c = 0; c < K; c++) {
+        const uint32_t f0 = bnd(c), f1 = bnd(c + 1), m = f1 - f0;
+        if (m == 0)
+            continue;
+        const uint64_t b0 = s->total[4 + c], b1 = s->total[5 + c];
+        if (hipStreamWaitEvent(stream, s->ev_s[c], 0) != hipSuccess ||
+            (b1 > b0 && hipStreamWaitEvent(stream, s->ev_h[c], 0) != hipSuccess))
+            return drain();
+        if (b1 > b0)
+            hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, f1, s->ops,
+                               s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at, f0);
+        if (launch_seq_exec_lit(d_desc + f0, m, s->lit, d_out, s->rec_base + f0, s->items, s->nitems + f0,
+                                d_status + f0, stream) != 0)
+            rc = -1;
+        hipLaunchKernelGGL(zstd_check_kernel, dim3((m + 3) / 4), dim3(256), 0, stream, d_desc + f0, m, d_out,
+                           s->ck + f0, d_status + f0, d_fail_at ? d_fail_at + f0 : nullptr);
+    }
     stage_mark(3, stream);
-    hipLaunchKernelGGL(zstd_check_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes,
-                       d_out, s->ck, d_status, d_fail_at);
     stage_mark(4, stream);
     return rc == 0 && hipGetLastError() == hipSuccess ? 0 : -1;
 }
