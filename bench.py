@@ -412,10 +412,14 @@ def main():
     stages, kname = None, None
     if stage_ms is not None and n_timed:
         avg_c = comp_bytes / max(nfr, 1)
-        parse_k = ("zstd_frame_kernel + zstd_huf_kernel + zstd_seq_kernel" if zstd
+        parse_k = ("zstd_frame_kernel (every chunk; each chunk's sequence and Huffman kernels start "
+                   "beside the later chunks' frame kernels)" if zstd
                    else z.parse_kernel_name(min(nfr, CHUNK_FRAMES), int(avg_c)))
-        names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel", "parse": parse_k,
-                  "execute": "seq_exec_kernel", "hand-off": "zstd_check_kernel"} if zstd else
+        # zstd: the decode runs in frame chunks over three streams, so after the
+        # frame kernels the caller's stream measures the rest together
+        names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel + zstd_bounds_kernel", "parse": parse_k,
+                  "execute": "rest of the chunks: zstd_seq_kernel | zstd_huf_kernel, zstd_lit_fix_kernel, "
+                             "seq_exec_kernel, zstd_check_kernel", "hand-off": "-"} if zstd else
                  {"plan": "lz4_plan_direct_kernel", "parse": parse_k,
                   "execute": "seq_exec_kernel", "hand-off": "lz4_wave_kernel<4096, 4, true>"})
         launches = 1 if zstd else (nfr + CHUNK_FRAMES - 1) // CHUNK_FRAMES
