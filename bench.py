@@ -51,7 +51,13 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH
 METRIC = "decompressed GB/s whole-node + achieved %HBM-read, LZ4 64KiB frames"
 METRIC_ZSTD = "decompressed GB/s whole-node, zstd 64KiB frames (config 5)"
 GiB = 1 << 30
-CHUNK_FRAMES = 65536     # frames per decode launch in a strong-scaling step
+CHUNK_BYTES = 4 * GiB    # decoded bytes per decode launch (config 4's 64 GiB steps: several)
+
+
+def chunk_frames(frame):
+    """frames per decode launch: one launch for the 4 GiB configs (2, 3), 4 GiB
+    launches for bigger per-rank workloads"""
+    return max(65536, CHUNK_BYTES // frame)
 
 
 def log(*a):
@@ -234,9 +240,9 @@ class Shard:
             yield a, b, sel
 
 
-def decode_launches(z, torch, desc_dev, n, comp, out, status, zstd):
-    """One step: every frame of the rank, launches of <= CHUNK_FRAMES frames
-    (LZ4) back to back on the current stream; zstd: one launch."""
+def decode_launches(z, torch, desc_dev, n, comp, out, status, zstd, per):
+    """One step: every frame of the rank, launches of <= per frames (LZ4)
+    back to back on the current stream; zstd: one launch."""
     L = z.lib()
     stream = torch.cuda.current_stream().cuda_stream
     if zstd:
@@ -244,8 +250,8 @@ def decode_launches(z, torch, desc_dev, n, comp, out, status, zstd):
                                     status.data_ptr(), stream) != 0:
             raise SystemExit("zsk_zstd_decode_frames launch failed")
         return
-    for s in range(0, n, CHUNK_FRAMES):
-        m = min(CHUNK_FRAMES, n - s)
+    for s in range(0, n, per):
+        m = min(per, n - s)
         if L.zsk_lz4_decode_frames(desc_dev.data_ptr() + 24 * s, m, comp.data_ptr(), out.data_ptr(),
                                    status.data_ptr() + 4 * s, stream) != 0:
             raise SystemExit("zsk_lz4_decode_frames launch failed")
@@ -322,7 +328,7 @@ def main():
         if harness:   # rehearsal: the expected bytes stand in for the decode
             fill_expected(torch, out, sh, base_dev, args.frame)
         else:
-            decode_launches(z, torch, desc_dev, nfr, comp, out, status, zstd)
+            decode_launches(z, torch, desc_dev, nfr, comp, out, status, zstd, chunk_frames(args.frame))
 
     def sync():
         if not harness:
@@ -414,7 +420,7 @@ def main():
         avg_c = comp_bytes / max(nfr, 1)
         parse_k = ("zstd_frame_kernel (every chunk; each chunk's sequence and Huffman kernels start "
                    "beside the later chunks' frame kernels)" if zstd
-                   else z.parse_kernel_name(min(nfr, CHUNK_FRAMES), int(avg_c)))
+                   else z.parse_kernel_name(min(nfr, chunk_frames(args.frame)), int(avg_c)))
         # zstd: the decode runs in frame chunks over three streams, so after the
         # frame kernels the caller's stream measures the rest together
         names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel + zstd_bounds_kernel", "parse": parse_k,
@@ -422,7 +428,7 @@ def main():
                              "seq_exec_kernel, zstd_check_kernel", "hand-off": "-"} if zstd else
                  {"plan": "lz4_plan_direct_kernel", "parse": parse_k,
                   "execute": "seq_exec_kernel", "hand-off": "lz4_wave_kernel<4096, 4, true>"})
-        launches = 1 if zstd else (nfr + CHUNK_FRAMES - 1) // CHUNK_FRAMES
+        launches = 1 if zstd else (nfr + chunk_frames(args.frame) - 1) // chunk_frames(args.frame)
         # kernel_times averages per launch; a step is `launches` launches
         stages = {k: {"kernel": names[k], "avg_ms": round(v * launches, 4)} for k, v in stage_ms.items()}
         kname = "zstd_seq_kernel" if zstd else names[max(("parse", "execute"), key=lambda k: stage_ms[k])]

@@ -53,6 +53,10 @@ def part(name):
     return None
 
 
+# dispatches per decode launch: the plan kernel runs once per launch (the
+# zstd decode dispatches its frame / Huffman / sequence / execute / check
+# kernels once per chunk)
+PLAN = "zstd_plan_kernel" if ZSTD else "lz4_plan_direct_kernel"
 stats = one("trace/*/*_kernel_stats.csv")
 shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
 kern = {}
@@ -62,6 +66,9 @@ for row in csv.DictReader(open(stats)):
         nm = row["Name"].replace("(anonymous namespace)::", "").split("(")[0]
         kern[k] = {"name": nm, "avg_ns": float(row["AverageNs"]),
                    "calls": int(row["Calls"])}
+plan_calls = kern.get(PLAN, {}).get("calls", 1)
+for k, v in kern.items():
+    v["per_launch"] = round(v["calls"] / plan_calls, 3)
 counters = {}
 for name in ("fetch", "write"):
     f = one(f"pmc_{name}/*/*_counter_collection.csv")
@@ -71,8 +78,10 @@ for name in ("fetch", "write"):
         if k:
             counters.setdefault((k, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
 per = {}
+# per launch: the median dispatch x dispatches per launch (in the PMC pass)
+plan_n = {c: len(v) for (k, c), v in counters.items() if k == PLAN}
 for (k, c), v in counters.items():
-    per.setdefault(k, {})[c] = statistics.median(v) * 1024
+    per.setdefault(k, {})[c] = statistics.median(v) * 1024 * len(v) / max(plan_n.get(c, len(v)), 1)
 fetch = sum(d.get("FETCH_SIZE", 0.0) for d in per.values())
 write = sum(d.get("WRITE_SIZE", 0.0) for d in per.values())
 alg = bench["roofline"]["algorithmic_bytes_per_launch"]
@@ -82,7 +91,7 @@ out = {
     "workload": bench["config"]["workload"],
     "launch_kernels": {k: {**kern.get(k, {}), "fetch_bytes_raw": per.get(k, {}).get("FETCH_SIZE"),
                            "write_bytes": per.get(k, {}).get("WRITE_SIZE")} for k in sorted(set(kern) | set(per))},
-    "launch_avg_ns_rocprof": sum(v["avg_ns"] for v in kern.values()),
+    "launch_avg_ns_rocprof": sum(v["avg_ns"] * v["per_launch"] for v in kern.values()),
     "bench_avg_launch_ms": bench["roofline"]["avg_launch_ms"],
     "fetch_size_bytes_raw": fetch,
     "fetch_bytes_corrected_x2": 2 * fetch,
