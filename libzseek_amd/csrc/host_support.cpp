@@ -354,8 +354,16 @@ void Slot::destroy()
 {
     if (!stream)
         return;
+    // every stream drained, then every stream destroyed before any event
+    // recorded on it (the slot's event and the zstd chunk events are recorded
+    // on this stream; round 2 saw the host heap corrupted when events went
+    // first), then the memory
     (void)hipStreamSynchronize(stream);
     pool_wait(&copies);
+    zstd_scratch_drop_streams(&zs);
+    (void)hipStreamDestroy(stream);
+    if (done)
+        (void)hipEventDestroy(done);
     zstd_scratch_free(&zs);
     split_scratch_free(&split);
     for (void *p : {(void *)d_comp, (void *)d_out, (void *)d_desc, (void *)d_status, (void *)d_fail,
@@ -366,9 +374,6 @@ void Slot::destroy()
                     (void *)h_out})
         if (p)
             (void)hipHostFree(p);
-    if (done)
-        (void)hipEventDestroy(done);
-    (void)hipStreamDestroy(stream);
     stream = nullptr;
     done = nullptr;
     h_comp = h_out = nullptr;

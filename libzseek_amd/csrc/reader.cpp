@@ -398,6 +398,9 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         h_lo = h_hi = d0;
     const bool ck = r->verify && st.checksum_flag;
     (void)hipSetDevice(g.device);
+    // the host copies of this slot's previous batch read its pinned bounce,
+    // which reserve() may reallocate
+    pool_wait(&s.copies);
     if (!s.reserve(csz, dsz, h_hi - h_lo, n, ck, J.err)) {
         J.io_failed = true;
         return false;

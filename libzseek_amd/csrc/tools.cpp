@@ -27,8 +27,11 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <sys/types.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <map>
@@ -354,4 +357,37 @@ ZSK_TOOL double zsk_tool_read_all(void *pread_fn, void *reader, uint8_t *buf, si
     }
     *got = done;
     return now_s() - t0;
+}
+
+// ---- crash diagnostics (test sessions) -------------------------------------
+// A native backtrace on SIGSEGV / SIGBUS / SIGABRT to stderr, then the handler
+// that was installed before (Python's faulthandler prints the Python stack).
+// Offsets into libzseek.so resolve with addr2line against the built library.
+namespace {
+struct sigaction g_prev[32];
+
+void crash_bt(int sig)
+{
+    void *f[64];
+    const int n = backtrace(f, 64);
+    static const char m[] = "\n*** native backtrace ***\n";
+    (void)!write(2, m, sizeof m - 1);
+    backtrace_symbols_fd(f, n, 2);
+    sigaction(sig, &g_prev[sig], nullptr);
+    raise(sig);
+}
+}   // namespace
+
+ZSK_TOOL int zsk_tool_install_backtrace(void)
+{
+    void *f[2];
+    (void)backtrace(f, 2);   // loads the unwinder now, not inside a signal
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_handler = crash_bt;
+    sa.sa_flags = SA_NODEFER;
+    for (int sig : {SIGSEGV, SIGBUS, SIGABRT})
+        if (sigaction(sig, &sa, &g_prev[sig]) != 0)
+            return -1;
+    return 0;
 }

@@ -220,6 +220,9 @@ struct ZstdScratch {
 int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, uint64_t items,
                          uint64_t blocks, hipStream_t stream);
 void zstd_scratch_free(ZstdScratch *s);
+// drain and destroy the scratch's own streams (its events stay until
+// zstd_scratch_free): lets an owner destroy every stream before any event
+void zstd_scratch_drop_streams(ZstdScratch *s);
 int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      ZstdScratch *s, hipStream_t stream);
 // d_fail_at (optional): per failed frame, the output offset of its failing

@@ -2125,7 +2125,7 @@ int grow(T **p, uint64_t &cap, uint64_t want, uint64_t unit)
 // its events and before the caller's stream goes: the side stream's wait on
 // an event recorded on the caller's stream is released while that stream is
 // still alive.
-void side_destroy(ZstdScratch *s)
+void drop_streams(ZstdScratch *s)
 {
     for (hipStream_t *q : {&s->side, &s->sq})
         if (*q) {
@@ -2133,6 +2133,12 @@ void side_destroy(ZstdScratch *s)
             (void)hipStreamDestroy(*q);
             *q = nullptr;
         }
+}
+
+// streams first, then the events recorded on them
+void side_destroy(ZstdScratch *s)
+{
+    drop_streams(s);
     for (int c = 0; c < ZstdScratch::kChunks; c++)
         for (hipEvent_t *e : {&s->ev_f[c], &s->ev_s[c], &s->ev_h[c]})
             if (*e) {
@@ -2152,9 +2158,8 @@ int side_create(ZstdScratch *s)
     bool ok = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, lo) == hipSuccess &&
               hipStreamCreateWithFlags(&s->sq, hipStreamNonBlocking) == hipSuccess;
     for (int c = 0; ok && c < ZstdScratch::kChunks; c++)
-        ok = hipEventCreateWithFlags(&s->ev_f[c], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&s->ev_s[c], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&s->ev_h[c], hipEventDisableTiming) == hipSuccess;
+        for (hipEvent_t *e : {&s->ev_f[c], &s->ev_s[c], &s->ev_h[c]})
+            ok = ok && (*e || hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess);
     if (!ok) {   // partly created, nothing recorded on it yet
         side_destroy(s);
         return -1;
@@ -2220,6 +2225,11 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
     }
     // op lists: 4 per block + 4 per frame
     return grow(&s->ops, s->ops_cap, blocks + frames, 4 * sizeof(ZOp));
+}
+
+void zstd_scratch_drop_streams(ZstdScratch *s)
+{
+    drop_streams(s);
 }
 
 void zstd_scratch_free(ZstdScratch *s)

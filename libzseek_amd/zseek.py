@@ -183,6 +183,8 @@ def tools() -> C.CDLL:
     if not os.path.exists(TOOLS_PATH):
         raise LibraryNotBuilt(f"{TOOLS_PATH} not built")
     T = C.CDLL(TOOLS_PATH)
+    T.zsk_tool_install_backtrace.restype = C.c_int
+    T.zsk_tool_install_backtrace.argtypes = []
     T.zsk_tool_synth.restype = None
     T.zsk_tool_synth.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
     T.zsk_tool_gen.restype = None

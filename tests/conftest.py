@@ -96,4 +96,8 @@ def gpu():
     if not gpu_available():
         pytest.fail("GPU test selected but no HIP device is visible")
     import torch
+    # a crash in native code prints its native stack too (then pytest's own
+    # Python traceback)
+    from libzseek_amd import zseek
+    zseek.tools().zsk_tool_install_backtrace()
     return torch.device("cuda", 0)
