@@ -1726,7 +1726,11 @@ __device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 // CU) 11.4 and 12.8 ms per launch against 10.6; the LL / ML code tables
 // computed (packed constants and selects) instead of read from LDS, 11.05;
 // 24 or 20 frames per wave (four or five single-wave workgroups per CU, one
-// per SIMD) the same as 32.
+// per SIMD) the same as 32.  Round 3, under the 4-chunk pipeline (other
+// chunks' kernels beside it): tables from the slot (no LDS) 10.96 ms per
+// launch at 32 frames per wave, 11.42 at 64, against 10.34 as here; the
+// sequence loop made branch-free (repeat offsets, checks, window unpack)
+// 11 % more wave cycles (its window wait no longer clear of the stores).
 constexpr uint32_t kSeqLanes = 32;
 constexpr uint32_t kSeqCells = 800;   // u16 cells per frame (768 + copy slack)
 
@@ -2340,6 +2344,20 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             if (hipEventRecord(s->ev_h[c], hs) != hipSuccess)
                 return drain();
         }
+#ifdef ZSK_TUNING
+        // A/B (tuning builds): ZSEEK_ZSTD_SEQ=1 tables from the slot (no LDS),
+        // 64 frames per wave; 2: the same, 32 frames per wave
+        static const int seqv = getenv("ZSEEK_ZSTD_SEQ") ? atoi(getenv("ZSEEK_ZSTD_SEQ")) : 0;
+        if (seqv == 1)
+            hipLaunchKernelGGL((zstd_seq_kernel<64, 0>), dim3((m + 63) / 64), dim3(64), 0, qs, d_desc, f1, d_comp,
+                               s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems, d_status,
+                               s->ck, d_fail_at, f0);
+        else if (seqv == 2)
+            hipLaunchKernelGGL((zstd_seq_kernel<32, 0>), dim3((m + 31) / 32), dim3(64), 0, qs, d_desc, f1, d_comp,
+                               s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems, d_status,
+                               s->ck, d_fail_at, f0);
+        else
+#endif
         hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
                            qs, d_desc, f1, d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items,
                            s->nitems, d_status, s->ck, d_fail_at, f0);

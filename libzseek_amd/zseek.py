@@ -17,7 +17,9 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libzseek.so")
+# ZSEEK_AMD_LIB: a tuning build (libzseek_tune.so, same exports plus A/B
+# variants) for scripts/ A/B runs; the product library otherwise
+LIB_PATH = os.environ.get("ZSEEK_AMD_LIB") or os.path.join(HERE, "lib", "libzseek.so")
 TOOLS_PATH = os.path.join(HERE, "lib", "libzseek_tools.so")
 
 ERRBUF = 80
