@@ -1402,7 +1402,7 @@ __device__ __forceinline__ int32_t br_left(const BRd &b)
 // a time, aligned.
 constexpr uint32_t kHufLdsCells = 2048;
 
-template <int G, int F, int DIAG, typename Tab>
+template <int G, int F, int DIAG, int B = 4, typename Tab>
 __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *out, uint64_t dst, uint32_t cnt,
                                            uint32_t lim)
 {
@@ -1451,7 +1451,7 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
             *reinterpret_cast<u32x4 *>(out + at) = v;
     };
     // to a 128-byte boundary of the output, a step at a time
-    while (i + 16 <= lim && ((dst + i) & 63)) {
+    while (i + 16 <= lim && ((dst + i) & (16 * B - 1))) {
         const u32x4 v = step16();
         put16(i, v);
         i += 16;
@@ -1461,15 +1461,15 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     // partial lines in L2 to be evicted (and merged in HBM) under this
     // kernel's write load (5.2 -> 3.9 ms; no stores at all: 1.9 ms; 8 steps
     // need more than the 128 VGPRs four waves per SIMD leave: spills)
-    while (i + 64 <= lim) {
-        u32x4 v[4];
+    while (i + 16 * B <= lim) {
+        u32x4 v[B];
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < B; k++)
             v[k] = step16();
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < B; k++)
             put16(i + 16 * k, v[k]);
-        i += 64;
+        i += 16 * B;
     }
     while (i + 16 <= lim) {
         const u32x4 v = step16();
@@ -1488,8 +1488,10 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
 
 __device__ unsigned int g_hdiag[32];   // diagnostic builds: waves per lgmax, LDS / global path
 
-template <int DIAG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
+// B: steps per store burst (4 = 64 bytes; 8 = whole 128-byte lines, which
+// needs the register budget of three waves per SIMD: tuning builds)
+template <int DIAG, int B = 4>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(B == 8 ? 3 : 4))) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
                                                       const uint8_t *__restrict__ comp,
                                                       const uint8_t *__restrict__ slots,
                                                       uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
@@ -1544,13 +1546,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zs
             const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(&tabs[first]);
             auto T = [&](uint32_t i) -> uint32_t { return *la<uint16_t>(tb + 2 * i); };
             if (lgmax <= 8)
-                huf_stream<4, 1, DIAG>(b, T, jlg, out, J.dst, J.cnt, J.lim);
+                huf_stream<4, 1, DIAG, B>(b, T, jlg, out, J.dst, J.cnt, J.lim);
             else
-                huf_stream<2, 2, DIAG>(b, T, jlg, out, J.dst, J.cnt, J.lim);
+                huf_stream<2, 2, DIAG, B>(b, T, jlg, out, J.dst, J.cnt, J.lim);
         } else {
             const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)jslot * kZSlot);
             auto T = [&](uint32_t i) -> uint32_t { return gt[i]; };
-            huf_stream<2, 2, DIAG>(b, T, jlg, out, J.dst, J.cnt, J.lim);
+            huf_stream<2, 2, DIAG, B>(b, T, jlg, out, J.dst, J.cnt, J.lim);
         }
         bad = bad || br_left(b) != 0;
     };
@@ -2291,7 +2293,9 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     const uint32_t K = zstd_chunks(nframes);
     static const bool serial = getenv("ZSEEK_ZSTD_SERIAL") != nullptr;   // diagnostics: one stream
     hipStream_t const hs = serial ? stream : s->side, qs = serial ? stream : s->sq;
+#ifdef ZSK_TUNING
     static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
+#endif
     if (blocks && hipMemsetAsync(s->hjobs, 0, (size_t)(4 * blocks) * sizeof(HufJob), stream) != hipSuccess)
         return -1;
     auto drain = [&] {   // an enqueue failed: nothing may still write the scratch
@@ -2317,21 +2321,33 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         if (nj) {
             if (hipStreamWaitEvent(hs, s->ev_f[c], 0) != hipSuccess)
                 return drain();
-            if (diag) {
-                unsigned int z[32] = {};
-                (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, hs);
-            }
             const uint8_t *jb = s->hjobs + 4 * b0 * sizeof(HufJob);
             uint8_t *hb = s->hbad + 4 * b0;
             const dim3 g((nj + 63) / 64), b(64);
+#ifdef ZSK_TUNING
+            // diagnostics and variants (tuning builds, ZSEEK_ZSTD_HUF_DIAG):
+            // 1 / 3 / 7 / 8 counters and elisions (printed), 100 = 128-byte
+            // store bursts at three waves per SIMD
+            const bool counters = diag != 0 && diag != 100;
+            if (counters) {
+                unsigned int z[32] = {};
+                (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, hs);
+            }
             switch (diag) {
+            case 100:
+                hipLaunchKernelGGL((zstd_huf_kernel<0, 8>), g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb);
+                break;
             case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             case 7: hipLaunchKernelGGL(zstd_huf_kernel<7>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             default: hipLaunchKernelGGL(zstd_huf_kernel<8>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             }
-            if (diag) {
+#else
+            hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb);
+#endif
+#ifdef ZSK_TUNING
+            if (counters) {
                 unsigned int z[32] = {};
                 (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_hdiag), sizeof(z), 0, hipMemcpyDeviceToHost, hs);
                 (void)hipStreamSynchronize(hs);
@@ -2341,6 +2357,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                         fprintf(stderr, " %d:%u", i, z[i]);
                 fprintf(stderr, "  global %u lds %u\n", z[16], z[17]);
             }
+#endif
             if (hipEventRecord(s->ev_h[c], hs) != hipSuccess)
                 return drain();
         }
