@@ -180,11 +180,13 @@ __device__ __forceinline__ uint32_t win32(const ZLds &L, uint32_t bit)
 }
 
 // ---- FSE tables -----------------------------------------------------------------
-// Normalized counts from the window at bit 0 of window offset wofs (lane 0),
+// Normalized counts from the window at bit 0 of window offset wofs,
 // RFC 8878 §4.1.1 / FSE_readNCount.  Returns bytes used, or 0 on error
 // (*err set).  norm[] receives nsym entries; the caller zeroes norm[0..max_sym]
 // first (zero counts are not written).  The bits are read through a 64-bit
 // register window W = window bits [wp, wp + 64), reloaded every 32 bits.
+// Wave-uniform (every lane runs it, its state in scalar registers: the scalar
+// unit has issue to spare in the VALU-bound frame kernel; lane 0 stores).
 __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t avail, uint32_t max_sym,
                                                 uint32_t max_log, uint32_t *tlog, uint32_t *nsym, uint32_t *err)
 {
@@ -194,8 +196,8 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
         if (pos - wp >= 32) {
             wp = pos & ~31u;
             const uint32_t d = wp >> 5;
-            const uint32_t lo = d < 64 ? *lp<uint32_t>(L.win + 4 * d) : 0u;
-            const uint32_t hi = d + 1 < 64 ? *lp<uint32_t>(L.win + 4 * d + 4) : 0u;
+            const uint32_t lo = d < 64 ? uni(*lp<uint32_t>(L.win + 4 * d)) : 0u;
+            const uint32_t hi = d + 1 < 64 ? uni(*lp<uint32_t>(L.win + 4 * d + 4)) : 0u;
             W = ((uint64_t)hi << 32) | lo;
         }
         return (uint32_t)(W >> (pos - wp)) & ((1u << n) - 1);
@@ -242,7 +244,7 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
         }
         count--;
         remaining -= count < 0 ? -count : count;
-        if (count)
+        if (count && lane_id() == 0)
             *lp<int16_t>(&L.norm[sym]) = (int16_t)count;
         sym++;
         prev0 = count == 0;
@@ -364,27 +366,36 @@ __device__ __forceinline__ void fse_build(ZLds &L, uint32_t *tab, uint32_t nsym,
     if (low)   // low-probability symbols at the top, in symbol order from size - 1 down
         *lp<uint32_t>(tab + size - 1 - (uint32_t)__builtin_popcountll(lm & below)) = lane;
     wave_lds_sync();
-    uint32_t cntr = low ? 1u : c;   // lane s: next state of symbol s
+    // next states: lane s holds symbol s's counter; per 64-cell group each lane
+    // finds the lanes holding its symbol with six bit-sliced ballots (symbols
+    // < 64), ranks itself among them, and the group's per-symbol totals come
+    // back through cnt[] (one ballot loop per distinct symbol cost ~5x the
+    // VALU issue of the whole kernel's other table work)
+    uint32_t cntr = low ? 1u : c;
     for (uint32_t u0 = 0; u0 < size; u0 += 64) {
         const uint32_t u = u0 + lane;
         const bool act = u < size;
-        const uint32_t s = act ? (*lp<uint32_t>(tab + u) & 0xFF) : 0xFFFFu;
-        uint64_t rem = __ballot(act);
-        while (rem) {
-            const uint32_t sj = uni(lane_val(s, __builtin_ctzll(rem)));
-            const uint64_t m = __ballot(act && s == sj);
-            const uint32_t base = lane_val(cntr, (int)sj);
-            if ((m >> lane) & 1) {
-                const uint32_t ns = base + (uint32_t)__builtin_popcountll(m & below);
-                const uint32_t nb = tl - (uint32_t)hibit(ns);
-                *lp<uint32_t>(tab + u) = sj | nb << 8 | ((ns << nb) - size) << 16;
-            }
-            if (lane == sj)
-                cntr += (uint32_t)__builtin_popcountll(m);
-            rem &= ~m;
+        const uint32_t s = act ? (*lp<uint32_t>(tab + u) & 0xFF) : 0u;
+        uint64_t m = __ballot(act);
+#pragma unroll
+        for (int bit = 0; bit < 6; bit++) {
+            const bool one = (s >> bit) & 1;
+            const uint64_t bb = __ballot(one);
+            m &= one ? bb : ~bb;
         }
+        const uint32_t base = (uint32_t)__shfl((int)cntr, (int)s, 64);
+        *lp<uint32_t>(&L.cnt[lane]) = 0;
+        wave_lds_sync();
+        if (act) {
+            const uint32_t ns = base + (uint32_t)__builtin_popcountll(m & below);
+            const uint32_t nb = tl - (uint32_t)hibit(ns);
+            *lp<uint32_t>(tab + u) = s | nb << 8 | ((ns << nb) - size) << 16;
+            *lp<uint32_t>(&L.cnt[s]) = (uint32_t)__builtin_popcountll(m);   // equal for every lane of s
+        }
+        wave_lds_sync();
+        cntr += *lp<uint32_t>(&L.cnt[lane]);
+        wave_lds_sync();
     }
-    wave_lds_sync();
 }
 
 // ---- Huffman tables --------------------------------------------------------------
@@ -404,18 +415,18 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
         uint32_t tl = 0, nsym = 0;
         uint32_t hs = 0;
         norm_clear(L, 256);
-        if (lane == 0)
-            hs = read_ncount(L, wofs, hb, 255, 6, &tl, &nsym, &err);
+        hs = read_ncount(L, wofs, hb, 255, 6, &tl, &nsym, &err);
         hs = uni(hs);
         if (uni(err))
             return 0;
         tl = uni(tl);
         nsym = uni(nsym);
         fse_build(L, L.wfse, nsym, tl);
-        if (lane == 0) {
+        {
             // backward stream inside the window: two interleaved states
+            // (wave-uniform, as read_ncount; lane 0 stores the weights)
             const uint32_t b0 = wofs + hs, bn = hb - hs;
-            const uint32_t lastb = bn ? *lp<uint8_t>(L.win + b0 + bn - 1) : 0;
+            const uint32_t lastb = bn ? uni(*lp<uint8_t>(L.win + b0 + bn - 1)) : 0;
             if (!lastb) {
                 err = 1;
             } else {
@@ -424,10 +435,15 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
                 auto rb = [&](uint32_t n) -> uint32_t {
                     pos -= (int32_t)n;
                     const int32_t x = (int32_t)(8 * b0) + pos;
-                    uint32_t v = (x >= 0 ? win32(L, (uint32_t)x) : win32(L, 0) << (uint32_t)(-x)) & ((1u << n) - 1);
+                    uint32_t v = uni(x >= 0 ? win32(L, (uint32_t)x) : win32(L, 0) << (uint32_t)(-x)) & ((1u << n) - 1);
                     if (pos < 0)
                         v = -pos >= (int32_t)n ? 0u : v & (~0u << (uint32_t)(-pos));
                     return v;
+                };
+                auto put = [&](uint32_t c) {
+                    if (lane == 0)
+                        L.wts[nw] = (uint8_t)c;
+                    nw++;
                 };
                 uint32_t s1 = rb(tl), s2 = rb(tl);
                 for (;;) {
@@ -435,27 +451,28 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
                         err = 1;
                         break;
                     }
-                    uint32_t c = *lp<uint32_t>(L.wfse + s1);
-                    L.wts[nw++] = (uint8_t)c;
+                    uint32_t c = uni(*lp<uint32_t>(L.wfse + s1));
+                    put(c);
                     s1 = (c >> 16) + rb((c >> 8) & 0xFF);
                     if (pos < 0) {
-                        L.wts[nw++] = (uint8_t)*lp<uint32_t>(L.wfse + s2);
+                        put(uni(*lp<uint32_t>(L.wfse + s2)));
                         break;
                     }
                     if (nw > 253) {
                         err = 1;
                         break;
                     }
-                    c = *lp<uint32_t>(L.wfse + s2);
-                    L.wts[nw++] = (uint8_t)c;
+                    c = uni(*lp<uint32_t>(L.wfse + s2));
+                    put(c);
                     s2 = (c >> 16) + rb((c >> 8) & 0xFF);
                     if (pos < 0) {
-                        L.wts[nw++] = (uint8_t)*lp<uint32_t>(L.wfse + s1);
+                        put(uni(*lp<uint32_t>(L.wfse + s1)));
                         break;
                     }
                 }
             }
         }
+        wave_lds_sync();   // lane 0's weights before every lane reads them
         used = 1 + hb;
     } else {
         nw = hb - 127;
@@ -786,8 +803,7 @@ __device__ __forceinline__ uint32_t seq_table(ZLds &L, Frame &F, uint32_t t, uin
         const uint32_t wx = stage_win(L, F.I, p);
         uint32_t tl = 0, nsym = 0, e = 0, used = 0;
         norm_clear(L, max_sym + 1);
-        if (lane == 0)
-            used = read_ncount(L, F.I.s0 + p - wx, avail, max_sym, max_log, &tl, &nsym, &e);
+        used = read_ncount(L, F.I.s0 + p - wx, avail, max_sym, max_log, &tl, &nsym, &e);
         if (uni(e) || uni(used) == 0) {
             *err = ZE_CORRUPT;
             return ~0u;
