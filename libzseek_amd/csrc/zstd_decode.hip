@@ -1476,7 +1476,12 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     // line arrives in two halves, where 16-byte stores a step apart left
     // partial lines in L2 to be evicted (and merged in HBM) under this
     // kernel's write load (5.2 -> 3.9 ms; no stores at all: 1.9 ms; 8 steps
-    // need more than the 128 VGPRs four waves per SIMD leave: spills)
+    // need more than the 128 VGPRs four waves per SIMD leave: spills).
+    // Round 3, config 5 (6-bit codes, kernels serialized): 2.90 ms; without
+    // the stores 1.85, also without the ring refills 1.33, also without the
+    // lookups 0.58.  Neither 128-byte bursts (three waves per SIMD) nor
+    // keeping the second step's chunk wait clear of the stores just issued
+    // (the loop head's wait-count merge made it wait for them) moved it.
     while (i + 16 * B <= lim) {
         u32x4 v[B];
 #pragma unroll
@@ -1504,10 +1509,9 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
 
 __device__ unsigned int g_hdiag[32];   // diagnostic builds: waves per lgmax, LDS / global path
 
-// B: steps per store burst (4 = 64 bytes; 8 = whole 128-byte lines, which
-// needs the register budget of three waves per SIMD: tuning builds)
+// B: steps per store burst (4 = 64 bytes)
 template <int DIAG, int B = 4>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(B == 8 ? 3 : 4))) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zstd_huf_kernel(const uint8_t *__restrict__ jobs, uint32_t nj,
                                                       const uint8_t *__restrict__ comp,
                                                       const uint8_t *__restrict__ slots,
                                                       uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
@@ -2341,18 +2345,14 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             uint8_t *hb = s->hbad + 4 * b0;
             const dim3 g((nj + 63) / 64), b(64);
 #ifdef ZSK_TUNING
-            // diagnostics and variants (tuning builds, ZSEEK_ZSTD_HUF_DIAG):
-            // 1 / 3 / 7 / 8 counters and elisions (printed), 100 = 128-byte
-            // store bursts at three waves per SIMD
-            const bool counters = diag != 0 && diag != 100;
+            // diagnostics (tuning builds, ZSEEK_ZSTD_HUF_DIAG): 1 / 3 / 7 / 8
+            // counters and elisions (printed)
+            const bool counters = diag != 0;
             if (counters) {
                 unsigned int z[32] = {};
                 (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, hs);
             }
             switch (diag) {
-            case 100:
-                hipLaunchKernelGGL((zstd_huf_kernel<0, 8>), g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb);
-                break;
             case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;

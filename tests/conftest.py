@@ -91,6 +91,21 @@ def gpu_available() -> bool:
         return False
 
 
+@pytest.fixture(autouse=True)
+def _hang_dump(request):
+    """A GPU test still running after 90 s prints every thread's Python stack
+    (once; the run goes on), so a hang names the call it is stuck in."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import faulthandler
+    faulthandler.dump_traceback_later(90, exit=False)
+    try:
+        yield
+    finally:
+        faulthandler.cancel_dump_traceback_later()
+
+
 @pytest.fixture(scope="session")
 def gpu():
     if not gpu_available():
