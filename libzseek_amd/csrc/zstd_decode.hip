@@ -1680,14 +1680,17 @@ __device__ __forceinline__ void sr_issue(SRd &b)
 __device__ __forceinline__ void sr_use(SRd &b)
 {
     const int32_t D = b.D, k0 = D - 4;
-    const u32x4 L = b.L;
-    const int32_t sft = k0 < 0 ? -k0 : 0;
-    u32x4 w;
-    w.x = sft == 0 ? L.x : 0u;
-    w.y = sft == 0 ? L.y : sft == 1 ? L.x : 0u;
-    w.z = sft == 0 ? L.z : sft == 1 ? L.y : sft == 2 ? L.x : 0u;
-    w.w = sft == 0 ? L.w : sft == 1 ? L.z : sft == 2 ? L.y : sft == 3 ? L.x : 0u;
-    if (k0 <= 0) {   // dword 0 holds the stream's first byte: clear the bits below it
+    u32x4 w = b.L;
+    // the window reaches the stream's first dword only at a block's last few
+    // sequences: a branch the wave skips, not selects on every sequence
+    if (k0 <= 0) {
+        const u32x4 L = b.L;
+        const int32_t sft = -k0;
+        w.x = sft == 0 ? L.x : 0u;
+        w.y = sft == 0 ? L.y : sft == 1 ? L.x : 0u;
+        w.z = sft == 0 ? L.z : sft == 1 ? L.y : sft == 2 ? L.x : 0u;
+        w.w = sft == 0 ? L.w : sft == 1 ? L.z : sft == 2 ? L.y : sft == 3 ? L.x : 0u;
+        // dword 0 holds the stream's first byte: clear the bits below it
         w.x &= above(b.xs, 32 * k0);
         w.y &= above(b.xs, 32 * k0 + 32);
         w.z &= above(b.xs, 32 * k0 + 64);
@@ -1715,10 +1718,11 @@ __device__ __forceinline__ void sr_fill(SRd &b)
     b.base = need ? b.base - 32 : b.base;
 }
 
-// n (<= 32) bits; nb >= n
+// n (<= 31) bits; nb >= n (a bitfield extract: width 0 reads 0)
 __device__ __forceinline__ uint32_t sr_take(SRd &b, uint32_t n)
 {
-    const uint32_t v = (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)n) & 63)) & (uint32_t)((1ull << n) - 1);
+    const uint32_t v =
+        __builtin_amdgcn_ubfe((uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)n) & 63)), 0u, n);
     b.nb -= (int32_t)n;
     return v;
 }
@@ -1870,42 +1874,38 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 // offset bits (<= 31; the window holds >= 33), a fill before
                                 // the ML + LL extra bits (<= 32) and one before the three
                                 // state updates (<= 26)
-                                const uint64_t ofv = (1ull << ofc) + sr_take(b, ofc);
+                                // offset value < 2^32 (ofc <= 31)
+                                const uint32_t ofv = (1u << ofc) + sr_take(b, ofc);
                                 const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
                                 sr_fill(b);
                                 const uint32_t ml = (mlcode & 0xFFFFFF) + sr_take(b, mlcode >> 24);
                                 const uint32_t ll = (llcode & 0xFFFFFF) + sr_take(b, llcode >> 24);
-                                uint64_t off;
-                                if (ofv > 3) {
-                                    off = ofv - 3;
-                                    rep2 = rep1;
-                                    rep1 = rep0;
-                                    rep0 = (uint32_t)off;
-                                } else {
-                                    const uint32_t idx = (uint32_t)ofv - 1 + (ll == 0);
-                                    if (idx == 0) {
-                                        off = rep0;
-                                    } else {
-                                        off = idx == 1 ? rep1 : idx == 2 ? rep2 : rep0 - 1;
-                                        if (off == 0)
-                                            off = 1;
-                                        if (idx != 1)
-                                            rep2 = rep1;
-                                        rep1 = rep0;
-                                        rep0 = (uint32_t)off;
-                                    }
-                                }
+                                // repeat offsets as selects (RFC 8878 §3.1.2.5): a new
+                                // offset (ofv > 3) or repeat idx 0..3; idx 0 keeps the
+                                // history, idx 1 swaps the first two, 2 and 3 rotate
+                                const bool fresh = ofv > 3;
+                                const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
+                                uint32_t off = fresh ? ofv - 3
+                                               : idx == 0 ? rep0
+                                               : idx == 1 ? rep1
+                                               : idx == 2 ? rep2
+                                                          : max(rep0 - 1, 1u);   // rep0 - 1, 0 read as 1
+                                const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
+                                rep2 = sh2 ? rep1 : rep2;
+                                rep1 = sh1 ? rep0 : rep1;
+                                rep0 = sh1 ? off : rep0;
                                 sr_fill(b);
                                 sll = fse_next(b, ell, tll);
                                 sml = fse_next(b, eml, tml);
                                 sof = fse_next(b, eof, tof);
                                 sr_done(b);
                                 sr_issue(b);
-                                if ((uint64_t)o + ll + ml > cap)
+                                // o <= cap: no 32-bit overflow in these tests
+                                if (ll + ml > cap - o)
                                     err = ZE_DST_SMALL;
                                 else if (le - lp_ < ll)
                                     err = ZE_CORRUPT;
-                                else if (off > (uint64_t)o + ll)
+                                else if (off > o + ll)
                                     err = ZE_CORRUPT;
                                 else if (!lemit(S, lp_, ll, (uint32_t)off, ml))
                                     err = ZE_GENERIC;

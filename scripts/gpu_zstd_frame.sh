@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/zfr
 mkdir -p $O
-timeout -k 10 400 python -u -X faulthandler -m pytest -x -v --timeout 60 --timeout-method thread tests/test_gpu_zstd.py > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
+timeout -k 10 400 python -u -X faulthandler -m pytest -x -v tests/test_gpu_zstd.py > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 ZSEEK_ZSTD_CHUNKS=1 ZSEEK_ZSTD_SERIAL=1 timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tr -- python bench.py --codec zstd --profile --steps 3 --warmup 1 > $O/tr.log 2>&1 || { tail -20 $O/tr.log; exit 1; }
 python3 -c "

@@ -93,17 +93,28 @@ def gpu_available() -> bool:
 
 @pytest.fixture(autouse=True)
 def _hang_dump(request):
-    """A GPU test still running after 90 s prints every thread's Python stack
-    (once; the run goes on), so a hang names the call it is stuck in."""
+    """A GPU test still running after 120 s is taken to be hung: every
+    thread's Python stack is printed, then the main thread gets SIGABRT, whose
+    handler (the `gpu` fixture's) prints the native stack it is stuck in."""
     if request.node.get_closest_marker("gpu") is None:
         yield
         return
     import faulthandler
-    faulthandler.dump_traceback_later(90, exit=False)
+    import signal
+    import threading
+    main = threading.main_thread().ident
+
+    def _fire():
+        faulthandler.dump_traceback(all_threads=True)
+        signal.pthread_kill(main, signal.SIGABRT)
+
+    t = threading.Timer(120.0, _fire)
+    t.daemon = True
+    t.start()
     try:
         yield
     finally:
-        faulthandler.cancel_dump_traceback_later()
+        t.cancel()
 
 
 @pytest.fixture(scope="session")
