@@ -293,6 +293,96 @@ void pool_wait(CopyTicket *t)
 }
 
 // ---------------------------------------------------------------------------
+// HIP stream / event recycling (process lifetime; see zsk_internal.h)
+// ---------------------------------------------------------------------------
+namespace {
+struct HandlePool {
+    std::mutex mu;
+    // free handles per (device, kind); kind 0 = stream, 1 = low-priority
+    // stream, 2 = event; owner[] remembers each handle's key
+    std::unordered_map<uint64_t, std::vector<void *>> free_;
+    std::unordered_map<void *, uint64_t> owner;
+};
+HandlePool &handle_pool()
+{
+    static HandlePool *p = new HandlePool();   // never destroyed, like the handles
+    return *p;
+}
+uint64_t handle_key(int kind)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return (uint64_t)(uint32_t)dev << 8 | (uint32_t)kind;
+}
+void *handle_take(uint64_t key)
+{
+    HandlePool &p = handle_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    auto it = p.free_.find(key);
+    if (it == p.free_.end() || it->second.empty())
+        return nullptr;
+    void *h = it->second.back();
+    it->second.pop_back();
+    return h;
+}
+void handle_note(void *h, uint64_t key)
+{
+    HandlePool &p = handle_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    p.owner[h] = key;
+}
+void handle_give(void *h)
+{
+    HandlePool &p = handle_pool();
+    std::lock_guard<std::mutex> g(p.mu);
+    auto it = p.owner.find(h);
+    if (it != p.owner.end())
+        p.free_[it->second].push_back(h);
+}
+}   // namespace
+
+hipError_t hip_stream_get(hipStream_t *s, bool low)
+{
+    const uint64_t key = handle_key(low ? 1 : 0);
+    if ((*s = (hipStream_t)handle_take(key)) != nullptr)
+        return hipSuccess;
+    hipError_t e;
+    if (low) {
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        e = hipStreamCreateWithPriority(s, hipStreamNonBlocking, lo);
+    } else {
+        e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
+    if (e == hipSuccess)
+        handle_note(*s, key);
+    return e;
+}
+
+void hip_stream_put(hipStream_t s)
+{
+    if (s)
+        handle_give(s);
+}
+
+hipError_t hip_event_get(hipEvent_t *ev)
+{
+    const uint64_t key = handle_key(2);
+    if ((*ev = (hipEvent_t)handle_take(key)) != nullptr)
+        return hipSuccess;
+    const hipError_t e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e == hipSuccess)
+        handle_note(*ev, key);
+    return e;
+}
+
+void hip_event_put(hipEvent_t e)
+{
+    if (e)
+        handle_give(e);
+}
+
+// ---------------------------------------------------------------------------
 // GPU context: a lane of kSlots batch slots on one device
 // ---------------------------------------------------------------------------
 namespace {
@@ -346,25 +436,22 @@ bool Slot::reserve(size_t comp, size_t out, size_t host_out, size_t nframes, boo
     return true;
 }
 
-// Teardown order: the slot's stream drained (its copies too), then the zstd
-// scratch (which drains and destroys its side stream before its events: the
-// side stream's wait on this stream's event goes while this stream is
-// alive), then memory, then this stream's event and the stream itself.
+// Teardown order: every stream drained (the slot's, its host copies, the
+// zstd scratch's side streams); then all memory, while every stream that used
+// it still exists; then the streams and the events recorded on them go back
+// to the process-wide pool (hip_stream_put / hip_event_put: never destroyed).
+// Round 2 saw the host heap corrupted when events went before streams; round
+// 3 saw hipFree fault (and, in later runs, the host heap left corrupted) when
+// device buffers were freed after the streams whose kernels last used them
+// had been destroyed (scripts/hang_probe.py reproduced it within ~25
+// open/read/close cycles).
 void Slot::destroy()
 {
     if (!stream)
         return;
-    // every stream drained, then every stream destroyed before any event
-    // recorded on it (the slot's event and the zstd chunk events are recorded
-    // on this stream; round 2 saw the host heap corrupted when events went
-    // first), then the memory
     (void)hipStreamSynchronize(stream);
     pool_wait(&copies);
-    zstd_scratch_drop_streams(&zs);
-    (void)hipStreamDestroy(stream);
-    if (done)
-        (void)hipEventDestroy(done);
-    zstd_scratch_free(&zs);
+    zstd_scratch_release_memory(&zs);
     split_scratch_free(&split);
     for (void *p : {(void *)d_comp, (void *)d_out, (void *)d_desc, (void *)d_status, (void *)d_fail,
                     (void *)d_ck})
@@ -374,6 +461,10 @@ void Slot::destroy()
                     (void *)h_out})
         if (p)
             (void)hipHostFree(p);
+    zstd_scratch_drop_streams(&zs);
+    hip_stream_put(stream);
+    hip_event_put(done);
+    zstd_scratch_free(&zs);   // its events (its memory and streams are gone)
     stream = nullptr;
     done = nullptr;
     h_comp = h_out = nullptr;
@@ -423,8 +514,7 @@ bool DeviceCtx::init(int dev, char *errbuf)
         return false;
     }
     for (Slot &s : slot) {
-        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+        if (hip_stream_get(&s.stream, false) != hipSuccess || hip_event_get(&s.done) != hipSuccess) {
             set_error(errbuf, "create HIP stream failed");
             for (Slot &t : slot)
                 t.destroy();

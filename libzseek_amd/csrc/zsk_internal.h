@@ -165,6 +165,17 @@ enum : int { ENGINE_AUTO = 0, ENGINE_SPLIT, ENGINE_WAVE };
 // while enabled.
 constexpr int kTimedStages = 4;
 void stage_mark(int boundary, hipStream_t stream);
+
+// HIP streams and events are recycled process-wide, never destroyed: a
+// reader's slots take them at open and give them back (drained) at close.
+// Destroying them per reader let the runtime's own threads touch freed
+// objects after hipStreamSynchronize had returned (host heap corruption under
+// reader open/close churn, scripts/hang_probe.py).  On the current device;
+// low = the lowest stream priority.
+hipError_t hip_stream_get(hipStream_t *s, bool low);
+void hip_stream_put(hipStream_t s);
+hipError_t hip_event_get(hipEvent_t *e);
+void hip_event_put(hipEvent_t e);
 int kernel_timing(int on);
 int kernel_times(double *ms, int cap);
 int lz4_engine();
@@ -220,8 +231,12 @@ struct ZstdScratch {
 int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, uint64_t items,
                          uint64_t blocks, hipStream_t stream);
 void zstd_scratch_free(ZstdScratch *s);
-// drain and destroy the scratch's own streams (its events stay until
-// zstd_scratch_free): lets an owner destroy every stream before any event
+// Teardown in three steps for an owner with streams of its own: the
+// scratch's memory (after draining its streams; streams and events kept),
+// then its streams, then (zstd_scratch_free) its events -- memory goes while
+// every stream that used it exists, streams before the events recorded on
+// them
+void zstd_scratch_release_memory(ZstdScratch *s);
 void zstd_scratch_drop_streams(ZstdScratch *s);
 int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      ZstdScratch *s, hipStream_t stream);

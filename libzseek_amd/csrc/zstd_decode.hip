@@ -1757,10 +1757,15 @@ __device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 // launch at 32 frames per wave, 11.42 at 64, against 10.34 as here; the
 // sequence loop made branch-free (repeat offsets, checks, window unpack)
 // 11 % more wave cycles (its window wait no longer clear of the stores).
+// OFG: only the LL and ML tables in LDS (544 cells: four workgroups per CU,
+// 128 frames in flight instead of 96); the OF cell of the next sequence is
+// loaded from the slot right after its state is known, just ahead of the
+// next window load, so the one wait for the window covers it.
 constexpr uint32_t kSeqLanes = 32;
-constexpr uint32_t kSeqCells = 800;   // u16 cells per frame (768 + copy slack)
+constexpr uint32_t kSeqCells = 544;   // u16 cells per frame (LL + ML 512 + copy slack)
+constexpr bool kSeqOfg = true;
 
-template <uint32_t LANES, uint32_t CELLS>
+template <uint32_t LANES, uint32_t CELLS, bool OFG = false>
 __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
@@ -1841,15 +1846,17 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
                         const uint32_t nll = 1u << tll, nof = 1u << tof, nml = 1u << tml;
                         const uint16_t *TL = gt + kFseOff[0], *TO = gt + kFseOff[1], *TM = gt + kFseOff[2];
-                        const bool fit = CELLS && nll + nof + nml + 32 <= CELLS;
+                        const uint32_t nofl = OFG ? 0u : nof;   // OF cells in LDS
+                        const bool fit = CELLS && nll + nofl + nml + 32 <= CELLS;
                         if (fit) {
                             auto cp = [&](const uint16_t *src, uint32_t at, uint32_t cells) {
                                 for (uint32_t c = 0; c < cells; c += 8)
                                     *reinterpret_cast<u32x4 *>(mytab + at + c) = *reinterpret_cast<const u32x4 *>(src + c);
                             };
                             cp(TL, 0, nll);
-                            cp(TO, nll, nof);
-                            cp(TM, nll + nof, nml);
+                            if (!OFG)
+                                cp(TO, nll, nof);
+                            cp(TM, nll + nofl, nml);
                         }
                         // the sequence loop, over tables in LDS (ds_read: the
                         // lookups' waits stay off vmcnt) or in the slot
@@ -1863,8 +1870,9 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             // VMEM pattern of its back edge (window, then three
                             // stores), so the window's wait stays vmcnt(3)
                             lput3(S, 0, 0, 0, 0);
+                            uint32_t eof_n = TOf(sof);   // the OF cell, one sequence ahead
                             for (uint32_t i = 0; i < nseq; i++) {
-                                const uint32_t ell = TLf(sll), eof = TOf(sof), eml = TMf(sml);
+                                const uint32_t ell = TLf(sll), eof = eof_n, eml = TMf(sml);
                                 sr_use(b);
                                 const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
                                 if (llc > 35 || ofc > 31 || mlc > 52) {
@@ -1898,6 +1906,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 sll = fse_next(b, ell, tll);
                                 sml = fse_next(b, eml, tml);
                                 sof = fse_next(b, eof, tof);
+                                eof_n = TOf(sof);
                                 sr_done(b);
                                 sr_issue(b);
                                 // o <= cap: no 32-bit overflow in these tests
@@ -1916,7 +1925,11 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             }
                         };
                         const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(mytab);
-                        if (fit)
+                        if (fit && OFG)
+                            seqs([&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * x); },
+                                 [&](uint32_t x) -> uint32_t { return TO[x]; },
+                                 [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + x)); });
+                        else if (fit)
                             seqs([&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * x); },
                                  [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + x)); },
                                  [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + nof + x)); });
@@ -2156,7 +2169,7 @@ void drop_streams(ZstdScratch *s)
     for (hipStream_t *q : {&s->side, &s->sq})
         if (*q) {
             (void)hipStreamSynchronize(*q);
-            (void)hipStreamDestroy(*q);
+            hip_stream_put(*q);
             *q = nullptr;
         }
 }
@@ -2168,7 +2181,7 @@ void side_destroy(ZstdScratch *s)
     for (int c = 0; c < ZstdScratch::kChunks; c++)
         for (hipEvent_t *e : {&s->ev_f[c], &s->ev_s[c], &s->ev_h[c]})
             if (*e) {
-                (void)hipEventDestroy(*e);
+                hip_event_put(*e);
                 *e = nullptr;
             }
 }
@@ -2178,14 +2191,11 @@ int side_create(ZstdScratch *s)
     // the Huffman stream at the lowest priority: the sequence kernel, the
     // longer of the two, gets the CUs' LDS first (10.9 -> 10.6 ms per launch
     // at config 5; launching the sequence kernel first made no difference)
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     (void)hipGetDevice(&s->side_dev);
-    bool ok = hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, lo) == hipSuccess &&
-              hipStreamCreateWithFlags(&s->sq, hipStreamNonBlocking) == hipSuccess;
+    bool ok = hip_stream_get(&s->side, true) == hipSuccess && hip_stream_get(&s->sq, false) == hipSuccess;
     for (int c = 0; ok && c < ZstdScratch::kChunks; c++)
         for (hipEvent_t *e : {&s->ev_f[c], &s->ev_s[c], &s->ev_h[c]})
-            ok = ok && (*e || hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess);
+            ok = ok && (*e || hip_event_get(e) == hipSuccess);
     if (!ok) {   // partly created, nothing recorded on it yet
         side_destroy(s);
         return -1;
@@ -2258,9 +2268,11 @@ void zstd_scratch_drop_streams(ZstdScratch *s)
     drop_streams(s);
 }
 
-void zstd_scratch_free(ZstdScratch *s)
+void zstd_scratch_release_memory(ZstdScratch *s)
 {
-    side_destroy(s);   // drains the side stream before anything goes
+    for (hipStream_t q : {s->side, s->sq})
+        if (q)
+            (void)hipStreamSynchronize(q);
     for (void *p : {(void *)s->bound, (void *)s->bblk, (void *)s->rec_base, (void *)s->blk_base,
                     (void *)s->nitems, (void *)s->ck, (void *)s->stop, (void *)s->lit, (void *)s->items,
                     (void *)s->ops, (void *)s->hjobs, (void *)s->slots, (void *)s->hbad, (void *)s->d_total})
@@ -2268,6 +2280,20 @@ void zstd_scratch_free(ZstdScratch *s)
             (void)hipFree(p);
     if (s->total)
         (void)hipHostFree(s->total);
+    s->bound = s->bblk = s->nitems = s->stop = nullptr;
+    s->rec_base = s->blk_base = s->ck = s->d_total = s->total = nullptr;
+    s->lit = s->slots = s->hbad = nullptr;
+    s->items = nullptr;
+    s->ops = s->hjobs = nullptr;
+    s->frames_cap = 0;
+    s->lit_cap = s->items_cap = s->blocks_cap = s->ops_cap = 0;
+}
+
+// memory (its streams drained), then streams, then events
+void zstd_scratch_free(ZstdScratch *s)
+{
+    zstd_scratch_release_memory(s);
+    side_destroy(s);
     *s = ZstdScratch();
 }
 
@@ -2379,7 +2405,8 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         }
 #ifdef ZSK_TUNING
         // A/B (tuning builds): ZSEEK_ZSTD_SEQ=1 tables from the slot (no LDS),
-        // 64 frames per wave; 2: the same, 32 frames per wave
+        // 64 frames per wave; 2: the same, 32 frames per wave; 3: all three
+        // tables in LDS (800 cells per frame)
         static const int seqv = getenv("ZSEEK_ZSTD_SEQ") ? atoi(getenv("ZSEEK_ZSTD_SEQ")) : 0;
         if (seqv == 1)
             hipLaunchKernelGGL((zstd_seq_kernel<64, 0>), dim3((m + 63) / 64), dim3(64), 0, qs, d_desc, f1, d_comp,
@@ -2389,9 +2416,13 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             hipLaunchKernelGGL((zstd_seq_kernel<32, 0>), dim3((m + 31) / 32), dim3(64), 0, qs, d_desc, f1, d_comp,
                                s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems, d_status,
                                s->ck, d_fail_at, f0);
+        else if (seqv == 3)   // round 3's layout: all three tables in LDS (800 cells)
+            hipLaunchKernelGGL((zstd_seq_kernel<32, 800>), dim3((m + 31) / 32), dim3(64), 0, qs, d_desc, f1, d_comp,
+                               s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems, d_status,
+                               s->ck, d_fail_at, f0);
         else
 #endif
-        hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
+        hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells, kSeqOfg>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
                            qs, d_desc, f1, d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items,
                            s->nitems, d_status, s->ck, d_fail_at, f0);
         if (hipEventRecord(s->ev_s[c], qs) != hipSuccess)
