@@ -1764,11 +1764,15 @@ __device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 // at config 5: kernel alone 2.42 ms against 2.79 with all three tables in
 // LDS (800 cells); the 4-chunk pipeline 9.25 / 9.27 against 9.43 / 9.40 ms
 // per launch.
+// GM generalizes it: bit t set = table t (LL, OF, ML) read from the slot, its
+// cell loaded one sequence ahead; the others are staged in LDS.  More tables
+// from the slot lose: OF + ML (288 cells, eight workgroups per CU) 4.71 ms
+// alone, all three 6.45 ms, against 2.43 (pipeline 9.70 / 10.15 vs 9.26).
 constexpr uint32_t kSeqLanes = 32;
 constexpr uint32_t kSeqCells = 544;   // u16 cells per frame (LL + ML 512 + copy slack)
-constexpr bool kSeqOfg = true;
+constexpr uint32_t kSeqGm = 2;        // OF from the slot
 
-template <uint32_t LANES, uint32_t CELLS, bool OFG = false>
+template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0>
 __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
@@ -1849,17 +1853,18 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
                         const uint32_t nll = 1u << tll, nof = 1u << tof, nml = 1u << tml;
                         const uint16_t *TL = gt + kFseOff[0], *TO = gt + kFseOff[1], *TM = gt + kFseOff[2];
-                        const uint32_t nofl = OFG ? 0u : nof;   // OF cells in LDS
-                        const bool fit = CELLS && nll + nofl + nml + 32 <= CELLS;
+                        // cells staged in LDS per table (0: read from the slot)
+                        const uint32_t nlll = (GM & 1) ? 0u : nll, nofl = (GM & 2) ? 0u : nof,
+                                       nmll = (GM & 4) ? 0u : nml;
+                        const bool fit = nlll + nofl + nmll == 0 || (CELLS && nlll + nofl + nmll + 32 <= CELLS);
                         if (fit) {
                             auto cp = [&](const uint16_t *src, uint32_t at, uint32_t cells) {
                                 for (uint32_t c = 0; c < cells; c += 8)
                                     *reinterpret_cast<u32x4 *>(mytab + at + c) = *reinterpret_cast<const u32x4 *>(src + c);
                             };
-                            cp(TL, 0, nll);
-                            if (!OFG)
-                                cp(TO, nll, nof);
-                            cp(TM, nll + nofl, nml);
+                            cp(TL, 0, nlll);
+                            cp(TO, nlll, nofl);
+                            cp(TM, nlll + nofl, nmll);
                         }
                         // the sequence loop, over tables in LDS (ds_read: the
                         // lookups' waits stay off vmcnt) or in the slot
@@ -1873,9 +1878,17 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             // VMEM pattern of its back edge (window, then three
                             // stores), so the window's wait stays vmcnt(3)
                             lput3(S, 0, 0, 0, 0);
-                            uint32_t eof_n = TOf(sof);   // the OF cell, one sequence ahead
+                            // the slot tables' cells, one sequence ahead
+                            uint32_t ell_n = 0, eof_n = 0, eml_n = 0;
+                            if (GM & 1)
+                                ell_n = TLf(sll);
+                            if (GM & 2)
+                                eof_n = TOf(sof);
+                            if (GM & 4)
+                                eml_n = TMf(sml);
                             for (uint32_t i = 0; i < nseq; i++) {
-                                const uint32_t ell = TLf(sll), eof = eof_n, eml = TMf(sml);
+                                const uint32_t ell = (GM & 1) ? ell_n : TLf(sll), eof = (GM & 2) ? eof_n : TOf(sof),
+                                               eml = (GM & 4) ? eml_n : TMf(sml);
                                 sr_use(b);
                                 const uint32_t llc = ell & 63, ofc = eof & 63, mlc = eml & 63;
                                 if (llc > 35 || ofc > 31 || mlc > 52) {
@@ -1909,7 +1922,12 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 sll = fse_next(b, ell, tll);
                                 sml = fse_next(b, eml, tml);
                                 sof = fse_next(b, eof, tof);
-                                eof_n = TOf(sof);
+                                if (GM & 1)
+                                    ell_n = TLf(sll);
+                                if (GM & 2)
+                                    eof_n = TOf(sof);
+                                if (GM & 4)
+                                    eml_n = TMf(sml);
                                 sr_done(b);
                                 sr_issue(b);
                                 // o <= cap: no 32-bit overflow in these tests
@@ -1928,14 +1946,17 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             }
                         };
                         const uint32_t tb = (uint32_t)(uintptr_t)lp<uint16_t>(mytab);
-                        if (fit && OFG)
-                            seqs([&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * x); },
-                                 [&](uint32_t x) -> uint32_t { return TO[x]; },
-                                 [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + x)); });
-                        else if (fit)
-                            seqs([&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * x); },
-                                 [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + x)); },
-                                 [&](uint32_t x) -> uint32_t { return *la<uint16_t>(tb + 2 * (nll + nof + x)); });
+                        if (fit)
+                            seqs([&](uint32_t x) -> uint32_t {
+                                     return (GM & 1) ? (uint32_t)TL[x] : (uint32_t)*la<uint16_t>(tb + 2 * x);
+                                 },
+                                 [&](uint32_t x) -> uint32_t {
+                                     return (GM & 2) ? (uint32_t)TO[x] : (uint32_t)*la<uint16_t>(tb + 2 * (nlll + x));
+                                 },
+                                 [&](uint32_t x) -> uint32_t {
+                                     return (GM & 4) ? (uint32_t)TM[x]
+                                                     : (uint32_t)*la<uint16_t>(tb + 2 * (nlll + nofl + x));
+                                 });
                         else
                             seqs([&](uint32_t x) -> uint32_t { return TL[x]; }, [&](uint32_t x) -> uint32_t { return TO[x]; },
                                  [&](uint32_t x) -> uint32_t { return TM[x]; });
@@ -2425,7 +2446,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                                s->ck, d_fail_at, f0);
         else
 #endif
-        hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells, kSeqOfg>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
+        hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells, kSeqGm>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
                            qs, d_desc, f1, d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items,
                            s->nitems, d_status, s->ck, d_fail_at, f0);
         if (hipEventRecord(s->ev_s[c], qs) != hipSuccess)
