@@ -174,17 +174,23 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
     const uint64_t dl = ((uint64_t)((saddr(S, op) - S.base) | (lit < 16 ? lit : 16) << 16 | K_LIT << 24) << 32) | src;
     const uint64_t dm = ((uint64_t)((saddr(S, mb) - S.base) | (mn < 16 ? mn : 16) << 16 | K_HBM << 24) << 32) | msrc;
     const uint32_t lm = lit < 16 ? 0 : lit - 16, mm = mn < 16 ? 0 : mn - 16;
-    uint32_t a = descs + 8 * x;
-    for (uint32_t i = 0; __ballot(i < np); i++) {
-        if (i < np) {
-            const bool isl = i < lpn;
-            const uint32_t o = min(16 * (isl ? i : i - lpn), isl ? lm : mm);
-            uint64_t D = (isl ? dl : dm) + (uint64_t)o * 0x100000001ull;
-            if (!isl && msrc + o + 16 > flushed)
-                D += (uint64_t)(K_STAGE - K_HBM) << 56;
-            *lp<uint64_t>(a) = D;
+    // piece i of the literal run and piece i of the match in one step: as
+    // many steps as the batch's longest run, no per-piece selects between
+    // the two (one step per piece of the longest literal + match cost ~22
+    // VALU per step)
+    const uint32_t al = descs + 8 * x;
+    for (uint32_t i = 0; __ballot(i < lpn || i + lpn < np); i++) {
+        if (i < lpn) {
+            const uint32_t o = min(16 * i, lm);
+            *lp<uint64_t>(al + 8 * i) = dl + (uint64_t)o * 0x100000001ull;
         }
-        a += 8;
+        if (i + lpn < np) {
+            const uint32_t o = min(16 * i, mm);
+            uint64_t D = dm + (uint64_t)o * 0x100000001ull;
+            if (msrc + o + 16 > flushed)
+                D += (uint64_t)(K_STAGE - K_HBM) << 56;
+            *lp<uint64_t>(al + 8 * (lpn + i)) = D;
+        }
     }
     wave_lds_sync();
     for (uint32_t t0 = 0; t0 < T; t0 += 256) {
