@@ -1481,7 +1481,9 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     // the stores 1.85, also without the ring refills 1.33, also without the
     // lookups 0.58.  Neither 128-byte bursts (three waves per SIMD) nor
     // keeping the second step's chunk wait clear of the stores just issued
-    // (the loop head's wait-count merge made it wait for them) moved it.
+    // (the loop head's wait-count merge made it wait for them) moved it;
+    // nontemporal stores doubled it (6.03 ms: L2 write-combining is doing
+    // real work here).
     while (i + 16 * B <= lim) {
         u32x4 v[B];
 #pragma unroll
