@@ -2232,11 +2232,13 @@ int side_create(ZstdScratch *s)
 // Chunks a decode of n frames runs in (frames [n c / k, n (c + 1) / k)): the
 // frame kernel of chunk c + 1 and the execute of chunk c - 1 run beside the
 // sequence and Huffman kernels of chunk c, which leave most of each CU's
-// issue slots idle.  Env ZSEEK_ZSTD_CHUNKS (A/B runs).
+// issue slots idle.  Env ZSEEK_ZSTD_CHUNKS (A/B runs).  Config
+// 5 (65,536 frames), same box, after the round-3 kernel changes: 2 chunks
+// 9.50 / 9.57 ms, 3 8.71 / 8.73, 4 9.04 / 9.03, 6 10.07 / 10.17.
 uint32_t zstd_chunks(uint32_t n)
 {
     static const int forced = getenv("ZSEEK_ZSTD_CHUNKS") ? atoi(getenv("ZSEEK_ZSTD_CHUNKS")) : 0;
-    uint32_t k = n >= 16384 ? 4 : n >= 4096 ? 2 : 1;
+    uint32_t k = n >= 16384 ? 3 : n >= 4096 ? 2 : 1;
     if (forced > 0)
         k = (uint32_t)forced;
     if (k > (uint32_t)ZstdScratch::kChunks)
