@@ -126,6 +126,22 @@ def test_device_zstd_synthetic(gpu, zs, frame):
     assert b"".join(out) == data.tobytes()
 
 
+@pytest.mark.parametrize("nframes", [16384, 20001])
+def test_device_zstd_three_chunk_pipeline(gpu, zs, nframes):
+    """batches of >= 16,384 frames decode in three pipelined chunks (ragged
+    at 20,001): every frame OK, bytes == the source"""
+    data = zs.synth_buffer(nframes * 4096)
+    img = zs.zstd_seekable(data, 4096)
+    c_off, d_off = zs.seek_table_of(img)
+    n = len(c_off) - 1
+    assert n == nframes
+    frames = [img[c_off[i]: c_off[i + 1]].tobytes() for i in range(n)]
+    sizes = [int(d_off[i + 1] - d_off[i]) for i in range(n)]
+    out, st = device_decode(zs, gpu, frames, sizes)
+    assert int((st != 0).sum()) == 0
+    assert b"".join(out) == data.tobytes()
+
+
 def test_device_zstd_corrupt_status(gpu, zs, oracle, zstd):
     """single-byte corruptions and truncations: every frame's status is the
     libzstd error code the oracle gives, intact frames decode bit-exact"""
