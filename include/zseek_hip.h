@@ -20,6 +20,10 @@
  *   zsk_verify_frame_checksums — the seek table's per-frame checksum,
  *                            parsed by seek_table.c:95-97 and never checked
  *                            there, checked on the GPU.
+ *   zsk_lz4_compress_frames — the writer's per-frame LZ4F_compressFrame call
+ *                            (compress.c:750 direct frames, :483 buffered
+ *                            ones; prefs compress.c:203-207), batched over
+ *                            frames of <= 64 KiB in one grid.
  */
 #ifndef ZSEEK_HIP_H
 #define ZSEEK_HIP_H
@@ -211,6 +215,42 @@ ZSEEK_EXPORT bool zsk_reader_set_devices(zseek_reader_t *reader,
     const int *devices, int n);
 ZSEEK_EXPORT int zsk_reader_devices(zseek_reader_t *reader, int *devices,
     int cap);
+
+/*
+ * LZ4 frame compression, byte-identical to the reference
+ * writer's frames: LZ4F_compressFrame(level, autoFlush = 1, 64 KiB blocks) of
+ * liblz4 1.9.3, as compress.c:737-786 / :463-518 call it.  One frame per
+ * descriptor, src_size <= 65536 (one block; larger frames are refused with
+ * c_size 0).  ZSK_COMPRESS_CONTENT_SIZE = the writer's contentSize != 0 case
+ * (a buffered frame flushed by end_frame_lz4, compress.c:472): the header
+ * then carries the frame's size.
+ */
+typedef struct {
+    uint64_t src_off;   /* frame input start in d_src                        */
+    uint64_t dst_off;   /* output slot start in d_dst: 16-byte aligned, at    */
+                        /* least ZSK_LZ4_COMPRESS_BOUND(src_size) bytes       */
+    uint32_t src_size;  /* <= 65536                                           */
+    uint32_t flags;     /* ZSK_COMPRESS_CONTENT_SIZE                          */
+} zsk_compress_desc_t;
+#define ZSK_COMPRESS_CONTENT_SIZE 1u
+#define ZSK_LZ4_COMPRESS_BOUND(n) ((((uint64_t)(n)) + 24 + 15) & ~(uint64_t)15)
+
+/* Device scratch bytes zsk_lz4_compress_frames needs for @nframes frames
+ * (a 16 KiB position table per frame). */
+ZSEEK_EXPORT size_t zsk_lz4_compress_scratch_size(uint32_t nframes);
+
+/*
+ * Compress @nframes frames on the GPU, asynchronously on @stream: frame f's
+ * bytes d_src[src_off, src_off + src_size) become one LZ4 frame written at
+ * d_dst + dst_off, its size in d_csize[f] (0 for a refused descriptor).
+ * @level is the writer's compressionLevel (< 3: liblz4's fast encoder,
+ * acceleration 1 - level for negative levels; HC levels return -1).
+ * @d_scratch holds zsk_lz4_compress_scratch_size(nframes) bytes.  All
+ * pointers are device pointers.  Returns 0 if queued, -1 otherwise.
+ */
+ZSEEK_EXPORT int zsk_lz4_compress_frames(const zsk_compress_desc_t *d_desc,
+    uint32_t nframes, const void *d_src, void *d_dst, uint32_t *d_csize,
+    int level, void *d_scratch, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,354 @@
+// lz4_compress.hip — the reference writer's LZ4 frame compression on the GPU
+// (gfx950), SURVEY §8f row 4.
+//
+// What it must reproduce, byte for byte: the writer compresses each seekable
+// frame with one LZ4F_compressFrame call (compress.c:737-786 direct frames,
+// :463-518 buffered ones) with prefs { level, autoFlush = 1, blockSizeID =
+// LZ4F_max64KB } (compress.c:203-207) and contentSize = the writer's frame_uc
+// counter (compress.c:741, :472).  For a frame of n <= 64 KiB liblz4 1.9.3
+// writes: header (magic, FLG = 0x60 | 0x08 with a content size, BD = 0x40,
+// [8-byte size], HC = XXH32 >> 8), one block made by LZ4F_makeBlock
+// (fast encoder, capacity n - 1, stored raw with bit 31 when it does not
+// fit), end mark.  The encoder is LZ4_compress_generic on a fresh state:
+// 16-bit positions in a 2^13-entry table, hash = read32 * 2654435761 >> 19,
+// search step growing by one every (64 * acceleration) misses, backward
+// extension, an immediate re-match test after every match, and the
+// limited-output checks that decide "stored".  oracle/lz4c_oracle.c is the
+// CPU restatement (pinned against liblz4); this kernel follows it decision
+// for decision.
+//
+// Mapping: one lane per frame (the parse is inherently serial: every table
+// entry depends on all earlier probes).  The lane's 16 KiB position table
+// lives in HBM scratch (zeroed per launch: liblz4's fresh state); input is
+// read in place; output goes through a little-endian dword packer so each
+// lane issues dword stores.  A sequence is emitted whole once its match
+// length is known, with both limited-output checks evaluated on the byte
+// counts they would see.  Frames that do not fit are flagged and their raw
+// block written by a second, wave-per-frame kernel (coalesced copy).
+//
+// Algorithmic bytes per frame: n read + the frame's compressed size written.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/zseek_hip.h"
+#include "zsk_internal.h"
+
+namespace zsk {
+
+namespace {
+
+typedef uint32_t u32_ua __attribute__((aligned(1)));
+
+constexpr uint32_t kHashLog = 13;
+constexpr uint32_t kTable = 1u << kHashLog;   // u16 entries per frame
+constexpr uint32_t kMaxFrame = 65536;
+constexpr uint32_t kStoredFlag = 0x80000000u;
+
+__device__ __forceinline__ uint32_t rd32(const uint8_t *p)
+{
+    return *reinterpret_cast<const u32_ua *>(p);
+}
+
+__device__ __forceinline__ uint32_t hash4(uint32_t v)
+{
+    return (v * 2654435761u) >> (32 - kHashLog);
+}
+
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r)
+{
+    return (x << r) | (x >> (32 - r));
+}
+
+// XXH32(seed 0) of a short header descriptor (2 or 10 bytes)
+__device__ uint32_t xxh32_short(const uint8_t *p, uint32_t len)
+{
+    uint32_t h = 0x165667B1u + len;
+    uint32_t i = 0;
+    for (; i + 4 <= len; i += 4) {
+        const uint32_t v = p[i] | p[i + 1] << 8 | p[i + 2] << 16 | (uint32_t)p[i + 3] << 24;
+        h = rotl32(h + v * 0xC2B2AE3Du, 17) * 0x27D4EB2Fu;
+    }
+    for (; i < len; i++)
+        h = rotl32(h + p[i] * 0x165667B1u, 11) * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA77u;
+    h ^= h >> 13;
+    h *= 0xC2B2AE3Du;
+    h ^= h >> 16;
+    return h;
+}
+
+// Little-endian byte packer over a 4-byte-aligned destination.
+struct Packer {
+    uint32_t *w;
+    uint32_t acc;
+    uint32_t k;   // bytes held in acc
+
+    __device__ __forceinline__ void put(uint32_t b)
+    {
+        acc |= (b & 0xFF) << (8 * k);
+        if (++k == 4) {
+            *w++ = acc;
+            acc = 0;
+            k = 0;
+        }
+    }
+    __device__ __forceinline__ void run(uint32_t len)   // 255 ... 255 rem
+    {
+        for (; len >= 255; len -= 255)
+            put(255);
+        put(len);
+    }
+    __device__ __forceinline__ void copy(const uint8_t *s, uint32_t len)
+    {
+        for (uint32_t i = 0; i < len; i++)
+            put(s[i]);
+    }
+    __device__ __forceinline__ void flush()
+    {
+        if (k)
+            *w = acc;
+    }
+};
+
+// Extra length bytes of a literal run / match code of value v (>= 15 -> 1 + (v-15)/255).
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t v)
+{
+    return v >= 15 ? (v - 15) / 255 + 1 : 0;
+}
+
+// Emit one sequence: token, literal-length bytes, literals, offset, match-length bytes.
+__device__ __forceinline__ void emit_seq(Packer &o, const uint8_t *lits, uint32_t lit, uint32_t off,
+                                         uint32_t mc)
+{
+    o.put((lit >= 15 ? 15u : lit) << 4 | (mc >= 15 ? 15u : mc));
+    if (lit >= 15)
+        o.run(lit - 15);
+    o.copy(lits, lit);
+    o.put(off);
+    o.put(off >> 8);
+    if (mc >= 15)
+        o.run(mc - 15);
+}
+
+// Equal bytes of s[a..] and s[b..] before a reaches lim (b < a).
+__device__ __forceinline__ uint32_t count_eq(const uint8_t *s, uint32_t a, uint32_t b, uint32_t lim)
+{
+    const uint32_t a0 = a;
+    while (a + 4 <= lim) {
+        const uint32_t x = rd32(s + a) ^ rd32(s + b);
+        if (x)
+            return a - a0 + (__builtin_ctz(x) >> 3);
+        a += 4;
+        b += 4;
+    }
+    while (a < lim && s[a] == s[b]) {
+        a++;
+        b++;
+    }
+    return a - a0;
+}
+
+// liblz4's LZ4_compress_generic (byU16, noDict, limitedOutput, capacity n-1)
+// on s[0..n); writes the block payload through o and returns its size, or
+// 0 when it does not fit (the frame's block is then stored raw).
+__device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, uint16_t *__restrict__ T,
+                                   Packer &o, uint32_t accel)
+{
+    const uint32_t cap = n - 1;
+    uint32_t op = 0, anchor = 0;
+    if (n >= 13) {
+        const uint32_t mflimit1 = n - 11, matchlimit = n - 5;
+        T[hash4(rd32(s))] = 0;
+        uint32_t ip = 1;
+        uint32_t fwd_h = hash4(rd32(s + 1));
+        for (;;) {
+            uint32_t m;
+            {
+                uint32_t fwd = ip, step = 1, nb = accel << 6;
+                for (;;) {
+                    const uint32_t h = fwd_h;
+                    const uint32_t cand = T[h];
+                    ip = fwd;
+                    fwd += step;
+                    step = nb++ >> 6;
+                    if (fwd > mflimit1)
+                        goto last_literals;
+                    m = cand;
+                    fwd_h = hash4(rd32(s + fwd));
+                    T[h] = (uint16_t)ip;
+                    if (rd32(s + m) == rd32(s + ip))
+                        break;
+                }
+            }
+            while (ip > anchor && m > 0 && s[ip - 1] == s[m - 1]) {
+                ip--;
+                m--;
+            }
+            uint32_t lit = ip - anchor;
+            // liblz4: after the token, op + lit + 8 + lit/255 must fit
+            if (op + 1 + lit + 8 + lit / 255 > cap)
+                return 0;
+            for (;;) {
+                const uint32_t mc = count_eq(s, ip + 4, m + 4, matchlimit);
+                const uint32_t op2 = op + 1 + ext_bytes(lit) + lit + 2;
+                if (op2 + 6 + (mc + 240) / 255 > cap)
+                    return 0;
+                emit_seq(o, s + anchor, lit, ip - m, mc);
+                op = op2 + ext_bytes(mc);
+                ip += mc + 4;
+                anchor = ip;
+                if (ip >= mflimit1)
+                    goto last_literals;
+                T[hash4(rd32(s + ip - 2))] = (uint16_t)(ip - 2);
+                const uint32_t h = hash4(rd32(s + ip));
+                const uint32_t cand = T[h];
+                T[h] = (uint16_t)ip;
+                if (rd32(s + cand) != rd32(s + ip))
+                    break;
+                m = cand;   // immediate match: no literals, no literal check
+                lit = 0;
+            }
+            ip++;
+            fwd_h = hash4(rd32(s + ip));
+        }
+    }
+last_literals:
+    {
+        const uint32_t run = n - anchor;
+        if (op + run + 1 + (run + 240) / 255 > cap)
+            return 0;
+        o.put((run >= 15 ? 15u : run) << 4);
+        if (run >= 15)
+            o.run(run - 15);
+        o.copy(s + anchor, run);
+        op += 1 + ext_bytes(run) + run;
+    }
+    return op;
+}
+
+__global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_desc_t *__restrict__ desc,
+                                                          uint32_t nframes, const uint8_t *__restrict__ src,
+                                                          uint8_t *__restrict__ dst,
+                                                          uint32_t *__restrict__ csize,
+                                                          uint16_t *__restrict__ tables,
+                                                          uint32_t *__restrict__ stored, uint32_t accel)
+{
+    const uint32_t f = blockIdx.x * 64 + threadIdx.x;
+    if (f >= nframes)
+        return;
+    const zsk_compress_desc_t d = desc[f];
+    stored[f] = 0;
+    if (d.src_size > kMaxFrame || (d.dst_off & 15)) {
+        csize[f] = 0;
+        return;
+    }
+    const uint32_t n = d.src_size;
+    const bool with_size = (d.flags & ZSK_COMPRESS_CONTENT_SIZE) && n > 0;
+    uint8_t hdr[15];
+    hdr[0] = 0x04;
+    hdr[1] = 0x22;
+    hdr[2] = 0x4D;
+    hdr[3] = 0x18;
+    hdr[4] = with_size ? 0x68 : 0x60;
+    hdr[5] = 0x40;
+    uint32_t hlen = 6;
+    if (with_size) {
+        for (int i = 0; i < 8; i++)
+            hdr[6 + i] = i < 4 ? (uint8_t)(n >> (8 * i)) : 0;
+        hlen = 14;
+    }
+    hdr[hlen] = (uint8_t)(xxh32_short(hdr + 4, hlen - 4) >> 8);
+    hlen++;
+
+    uint8_t *out = dst + d.dst_off;
+    Packer o{reinterpret_cast<uint32_t *>(out), 0, 0};
+    for (uint32_t i = 0; i < hlen; i++)
+        o.put(hdr[i]);
+    if (n == 0) {
+        for (int i = 0; i < 4; i++)
+            o.put(0);
+        o.flush();
+        csize[f] = hlen + 4;
+        return;
+    }
+    for (int i = 0; i < 4; i++)   // block word, patched below
+        o.put(0);
+    const uint32_t c = compress_block(src + d.src_off, n, tables + (size_t)f * kTable, o, accel);
+    if (c == 0) {
+        // the header stays; block word, raw block and end mark come from
+        // lz4_store_kernel
+        o.flush();
+        stored[f] = hlen;
+        csize[f] = hlen + 4 + n + 4;
+        return;
+    }
+    for (int i = 0; i < 4; i++)
+        o.put(0);
+    o.flush();
+    for (int i = 0; i < 4; i++)
+        out[hlen + i] = (uint8_t)(c >> (8 * i));
+    csize[f] = hlen + 4 + c + 4;
+}
+
+// Raw blocks of the frames lz4_compress_kernel flagged: one wave per frame.
+__global__ __launch_bounds__(256) void lz4_store_kernel(const zsk_compress_desc_t *__restrict__ desc,
+                                                        uint32_t nframes, const uint8_t *__restrict__ src,
+                                                        uint8_t *__restrict__ dst,
+                                                        const uint32_t *__restrict__ stored)
+{
+    const uint32_t f = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (f >= nframes)
+        return;
+    const uint32_t hlen = stored[f];
+    if (hlen == 0)
+        return;
+    const zsk_compress_desc_t d = desc[f];
+    const uint32_t n = d.src_size;
+    uint8_t *out = dst + d.dst_off + hlen;
+    const uint8_t *in = src + d.src_off;
+    const uint32_t word = n | kStoredFlag;
+    if (lane < 4) {
+        out[lane] = (uint8_t)(word >> (8 * lane));
+        out[4 + n + lane] = 0;
+    }
+    for (uint32_t i = lane; i < n; i += 64)
+        out[4 + i] = in[i];
+}
+
+}   // namespace
+
+int launch_lz4_compress(const zsk_compress_desc_t *d_desc, uint32_t nframes, const uint8_t *d_src,
+                        uint8_t *d_dst, uint32_t *d_csize, int level, void *d_scratch, hipStream_t stream)
+{
+    if (nframes == 0)
+        return 0;
+    if (!d_desc || !d_src || !d_dst || !d_csize || !d_scratch || level >= 3)
+        return -1;
+    const uint32_t accel = level < 0 ? (level < -65536 ? 65537u : (uint32_t)(1 - level)) : 1u;
+    uint16_t *tables = static_cast<uint16_t *>(d_scratch);
+    uint32_t *stored = reinterpret_cast<uint32_t *>(tables + (size_t)nframes * kTable);
+    if (hipMemsetAsync(tables, 0, (size_t)nframes * kTable * sizeof(uint16_t), stream) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(lz4_compress_kernel, dim3((nframes + 63) / 64), dim3(64), 0, stream, d_desc, nframes,
+                       d_src, d_dst, d_csize, tables, stored, accel);
+    hipLaunchKernelGGL(lz4_store_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes, d_src,
+                       d_dst, stored);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}   // namespace zsk
+
+extern "C" ZSEEK_EXPORT size_t zsk_lz4_compress_scratch_size(uint32_t nframes)
+{
+    return (size_t)nframes * (zsk::kTable * sizeof(uint16_t) + sizeof(uint32_t));
+}
+
+extern "C" ZSEEK_EXPORT int zsk_lz4_compress_frames(const zsk_compress_desc_t *d_desc, uint32_t nframes,
+                                                    const void *d_src, void *d_dst, uint32_t *d_csize,
+                                                    int level, void *d_scratch, void *stream)
+{
+    return zsk::launch_lz4_compress(d_desc, nframes, static_cast<const uint8_t *>(d_src),
+                                    static_cast<uint8_t *>(d_dst), d_csize, level, d_scratch,
+                                    static_cast<hipStream_t>(stream));
+}

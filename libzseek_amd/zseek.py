@@ -85,6 +85,11 @@ class GpuStatsC(C.Structure):
 FRAME_DESC_DTYPE = np.dtype([("c_off", "<u8"), ("d_off", "<u8"), ("c_size", "<u4"),
                              ("d_size", "<u4")])
 assert FRAME_DESC_DTYPE.itemsize == 24
+# zsk_compress_desc_t (include/zseek_hip.h)
+COMPRESS_DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("src_size", "<u4"),
+                                ("flags", "<u4")])
+assert COMPRESS_DESC_DTYPE.itemsize == 24
+COMPRESS_CONTENT_SIZE = 1
 
 # exported C symbols that include/zseek.h and include/zseek_hip.h declare
 EXPORTED = [
@@ -97,6 +102,7 @@ EXPORTED = [
     "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
     "zsk_verify_frame_checksums", "zsk_reader_set_verify_checksums",
     "zsk_reader_set_devices", "zsk_reader_devices", "zsk_reader_set_io_threads",
+    "zsk_lz4_compress_scratch_size", "zsk_lz4_compress_frames",
 ]
 
 _lib = None
@@ -173,6 +179,11 @@ def lib() -> C.CDLL:
     L.zsk_reader_set_io_threads.argtypes = [C.c_void_p, C.c_int]
     L.zsk_reader_devices.restype = C.c_int
     L.zsk_reader_devices.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    L.zsk_lz4_compress_scratch_size.restype = C.c_size_t
+    L.zsk_lz4_compress_scratch_size.argtypes = [C.c_uint32]
+    L.zsk_lz4_compress_frames.restype = C.c_int
+    L.zsk_lz4_compress_frames.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     _lib = L
     return L
 
@@ -576,6 +587,58 @@ def verify_frame_checksums(desc, out, checksums, status, stream: int | None = No
     if lib().zsk_verify_frame_checksums(desc.data_ptr(), n, out.data_ptr(), checksums.data_ptr(),
                                         status.data_ptr(), stream) != 0:
         raise ZseekError("zsk_verify_frame_checksums launch failed")
+
+
+def lz4_compress_bound(n: int) -> int:
+    """ZSK_LZ4_COMPRESS_BOUND: output slot bytes for a frame of n bytes."""
+    return (n + 24 + 15) & ~15
+
+
+def lz4_compress_layout(sizes, src_offsets=None, flags=None) -> tuple[np.ndarray, int]:
+    """Descriptors for zsk_lz4_compress_frames: frame f reads
+    src[src_offsets[f], +sizes[f]) (default: the frames back to back) and
+    writes its slot at a 16-byte aligned dst_off.  -> (COMPRESS_DESC_DTYPE
+    array, dst bytes needed)."""
+    sizes = np.asarray(sizes, np.uint64)
+    n = sizes.size
+    d = np.zeros(n, COMPRESS_DESC_DTYPE)
+    d["src_size"] = sizes
+    if src_offsets is None:
+        src_offsets = np.concatenate(([0], np.cumsum(sizes)[:-1])) if n else sizes
+    d["src_off"] = src_offsets
+    slots = (sizes + 24 + 15) & ~np.uint64(15)
+    d["dst_off"] = np.concatenate(([0], np.cumsum(slots)[:-1])) if n else slots
+    if flags is not None:
+        d["flags"] = flags
+    return d, int(slots.sum())
+
+
+def lz4_compress_scratch_size(nframes: int) -> int:
+    return int(lib().zsk_lz4_compress_scratch_size(nframes))
+
+
+def lz4_compress_frames(desc, src, dst, csize, level: int = 0, scratch=None,
+                        stream: int | None = None) -> None:
+    """zsk_lz4_compress_frames on torch device tensors (async on the current
+    stream): desc = COMPRESS_DESC_DTYPE bytes (uint8), src / dst uint8,
+    csize one int32 per frame (frame sizes out; 0 = refused descriptor)."""
+    import torch
+    n = csize.numel()
+    if desc.numel() != n * 24:
+        raise ValueError("desc must hold 24 bytes per frame")
+    if scratch is None:
+        scratch = torch.empty(max(lz4_compress_scratch_size(n), 1), dtype=torch.uint8,
+                              device=csize.device)
+    for t in (desc, src, dst, csize, scratch):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("lz4_compress_frames needs contiguous device tensors")
+    if scratch.numel() < lz4_compress_scratch_size(n):
+        raise ValueError("scratch too small")
+    if stream is None:
+        stream = torch.cuda.current_stream().cuda_stream
+    if lib().zsk_lz4_compress_frames(desc.data_ptr(), n, src.data_ptr(), dst.data_ptr(),
+                                     csize.data_ptr(), level, scratch.data_ptr(), stream) != 0:
+        raise ZseekError("zsk_lz4_compress_frames launch failed")
 
 
 def with_frame_checksums(image, checksums) -> np.ndarray:

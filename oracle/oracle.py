@@ -75,6 +75,21 @@ class Oracle:
         L.orc_zstd_decode_at.restype = C.c_longlong
         L.orc_zstd_decode_at.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                          C.POINTER(C.c_size_t)]
+        L.orc_lz4f_compress_frame.restype = C.c_longlong
+        L.orc_lz4f_compress_frame.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                              C.c_int, C.c_int]
+
+    # -- LZ4 frame compression (the reference writer's, lz4c_oracle.c) ------
+    def lz4f_compress_frame(self, data, level: int = 0, content_size: bool = False) -> bytes:
+        """LZ4F_compressFrame(level, autoFlush, 64 KiB blocks) of one frame of
+        <= 64 KiB, as compress.c:750 / :483 call it."""
+        s = np.frombuffer(bytes(data), np.uint8)
+        out = np.empty(s.size + 32, np.uint8)
+        r = self.lib.orc_lz4f_compress_frame(s.ctypes.data if s.size else None, s.size,
+                                             out.ctypes.data, out.size, level, int(content_size))
+        if r < 0:
+            raise ValueError("orc_lz4f_compress_frame: unsupported input")
+        return out[:r].tobytes()
 
     # -- hashes -----------------------------------------------------------
     def xxh32(self, data: bytes, seed: int = 0) -> int:
