@@ -50,6 +50,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "decompressed GB/s whole-node + achieved %HBM-read, LZ4 64KiB frames"
 METRIC_ZSTD = "decompressed GB/s whole-node, zstd 64KiB frames (config 5)"
+METRIC_LZ4C = "LZ4 frame compression GB/s (input bytes) whole-node, 64KiB frames (SURVEY 8f row 4)"
 GiB = 1 << 30
 CHUNK_BYTES = 4 * GiB    # decoded bytes per decode launch (config 4's 64 GiB steps: several)
 
@@ -92,8 +93,9 @@ def parse(argv=None):
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--reassemble", type=int, default=-1, help="1/0; default on when N > 1")
     p.add_argument("--profile", action="store_true", help="few steps, no extras (rocprof runs)")
-    p.add_argument("--codec", choices=["lz4", "zstd"], default="lz4",
-                   help="lz4 = configs 2-4 (the headline metric); zstd = config 5")
+    p.add_argument("--codec", choices=["lz4", "zstd", "lz4c"], default="lz4",
+                   help="lz4 = configs 2-4 (the headline metric); zstd = config 5; lz4c = "
+                        "GPU LZ4 frame compression (SURVEY §8f row 4, not a BASELINE config)")
     p.add_argument("--harness-check", action="store_true",
                    help="CPU rehearsal of the multi-rank harness (gloo, no GPU: a host "
                         "copy of the expected bytes stands in for the decode)")
@@ -291,6 +293,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
     if args.profile:
         args.no_cpu_baseline = args.no_e2e = args.no_verify = args.no_latency = True
+    if args.codec == "lz4c":
+        return main_compress(args, torch, dist, z, dev, world, rank)
     zstd = args.codec == "zstd"
 
     # ---- workload -------------------------------------------------------------
@@ -503,6 +507,140 @@ def main():
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_compress(args, torch, dist, z, dev, world, rank):
+    """--codec lz4c: every rank compresses its own --size bytes of the §8d
+    synthetic into --frame (<= 64 KiB) LZ4 frames on its GPU, input resident
+    in HBM (weak scaling).  One step = one zsk_lz4_compress_frames launch over
+    every frame (memset of the position tables, lz4_compress_kernel,
+    lz4_store_kernel).  Output: byte-identical to liblz4's frames (checked
+    against the writer-identical seekable image after the timed region)."""
+    if args.frame > 65536:
+        raise SystemExit("--codec lz4c: frames of at most 64 KiB")
+    t0 = time.time()
+    size = args.size - args.size % args.frame
+    data = z.synth_buffer(size, args.threads)
+    nfr = size // args.frame
+    desc, dst_bytes = z.lz4_compress_layout(np.full(nfr, args.frame, np.uint64))
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+    d_src = torch.from_numpy(data).to(dev)
+    d_dst = torch.empty(dst_bytes, dtype=torch.uint8, device=dev)
+    csize = torch.zeros(nfr, dtype=torch.int32, device=dev)
+    scratch = torch.empty(z.lz4_compress_scratch_size(nfr), dtype=torch.uint8, device=dev)
+    log(f"[rank {rank}] lz4c input: {size / GiB:.2f} GiB, {nfr} frames ({time.time() - t0:.1f}s)")
+    stream = torch.cuda.current_stream()
+
+    def step():
+        z.lz4_compress_frames(d_desc, d_src, d_dst, csize, 0, scratch, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(args.steps):
+        step()
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - w0
+    if world > 1:
+        dist.barrier()
+    step_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
+    t_local = sum(step_ms) / 1e3
+    t = torch.tensor([t_local, wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t[0])
+
+    cs = csize.cpu().numpy().astype(np.int64)
+    comp_bytes = int(cs.sum())
+    verified = None
+    if not args.no_verify:
+        img = np.asarray(z.lz4_seekable(data, args.frame, 0, args.threads))
+        c_off, _ = z.seek_table_of(img)
+        host = d_dst.cpu().numpy()
+        ok = bool((cs == np.diff(c_off)).all())
+        offs = desc["dst_off"]
+        for f in range(nfr if ok else 0):
+            if host[int(offs[f]):int(offs[f]) + int(cs[f])].tobytes() != \
+                    img[int(c_off[f]):int(c_off[f + 1])].tobytes():
+                ok = False
+                break
+        verified = ok
+        if not ok:
+            raise SystemExit("GPU frames differ from liblz4's")
+    cpu = None
+    host_info = host_cpus()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_compress(z, data, args.frame, host_info, args.threads)
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    avg_s = t_local / args.steps
+    alg = size + comp_bytes                  # input read once + frames written once
+    line = {
+        "metric": METRIC_LZ4C, "value": round(size * world * args.steps / t_max / 1e9, 2),
+        "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(t_max / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (SURVEY §8d generator), resident in HBM",
+        "config": {"workload": f"lz4c: {size / GiB:g} GiB synthetic per GPU into {args.frame >> 10}KiB "
+                               "LZ4 frames (level 0, as compress.c:203-207 / :750)",
+                   "frame_bytes": args.frame, "frames_per_gpu": nfr, "input_bytes_per_gpu": size,
+                   "compressed_bytes_per_gpu": comp_bytes,
+                   "parallelism": f"x{world} independent ranks" if world > 1 else "one GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(alg / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": None, "kernel": "lz4_compress_kernel",
+                     "launch": "zsk_lz4_compress_frames (memset + lz4_compress_kernel + lz4_store_kernel)",
+                     "avg_launch_ms": round(avg_s * 1e3, 4), "algorithmic_bytes_per_launch": alg},
+        "cpu_baseline": cpu,
+        "verified_bit_exact": verified,
+        "host": host_info,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_compress(z, data, frame, host, threads):
+    """liblz4 1.9.3's LZ4F_compressFrame, the compressor the reference writer
+    calls, on the host: the reference writer itself (oracle/_ref, one thread)
+    on the first 512 MiB, and frame-parallel liblz4 (libzseek_tools, T
+    threads over independent frames, the writer's prefs) on the whole input."""
+    res = {"unit": "GB/s", "kind": "reference"}
+    one = min(data.size, 512 << 20)
+    try:
+        from oracle.oracle import RefZseek, ZSEEK_LZ4
+        ref = RefZseek()
+        t0 = time.perf_counter()
+        ref.compress(data[:one].tobytes(), ZSEEK_LZ4, frame, frame)
+        res["one_thread_GBps"] = round(one / (time.perf_counter() - t0) / 1e9, 3)
+    except Exception as e:   # reference build absent
+        res["one_thread_GBps"] = None
+        res["one_thread_note"] = f"reference writer unavailable: {e}"
+    runs = {}
+    for t in sorted({host["usable"], host["visible"]}):
+        best = 0.0
+        for _ in range(2):
+            t0 = time.perf_counter()
+            z.lz4_seekable(data, frame, 0, t)
+            best = max(best, data.size / (time.perf_counter() - t0) / 1e9)
+        runs[t] = best
+    cores = max(runs, key=runs.get)
+    res.update({"value": round(runs[cores], 2), "cores": cores,
+                "by_threads": {str(t): round(v, 2) for t, v in runs.items()},
+                "sample": (f"reference writer (1 thread, {frame >> 10} KiB direct writes) on the first "
+                           f"{one >> 20} MiB; liblz4 LZ4F_compressFrame with the writer's prefs over "
+                           f"the whole {data.size >> 20} MiB, frames spread over T threads "
+                           f"(value: the faster T); host {host['model']}")})
+    return res
 
 
 def fill_expected(torch, out, sh, base_dev, frame):

@@ -38,11 +38,14 @@ namespace zsk {
 namespace {
 
 typedef uint32_t u32_ua __attribute__((aligned(1)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_ua __attribute__((aligned(1)));
 
 constexpr uint32_t kHashLog = 13;
 constexpr uint32_t kTable = 1u << kHashLog;   // u16 entries per frame
 constexpr uint32_t kMaxFrame = 65536;
 constexpr uint32_t kStoredFlag = 0x80000000u;
+constexpr uint32_t kProbe = 8;   // search probes per batch
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t *p)
 {
@@ -99,9 +102,27 @@ struct Packer {
             put(255);
         put(len);
     }
+    __device__ __forceinline__ void put4(uint32_t x)   // four bytes, little-endian
+    {
+        const uint64_t t = (uint64_t)x << (8 * k) | acc;
+        *w++ = (uint32_t)t;
+        acc = (uint32_t)(t >> 32);
+    }
+    // s[0..len), all inside the frame: 16-byte loads while they stay inside,
+    // so a literal run costs one load latency per 16 bytes, not per byte
     __device__ __forceinline__ void copy(const uint8_t *s, uint32_t len)
     {
-        for (uint32_t i = 0; i < len; i++)
+        uint32_t i = 0;
+        for (; i + 16 <= len; i += 16) {
+            const u32x4 v = *reinterpret_cast<const u32x4_ua *>(s + i);
+            put4(v.x);
+            put4(v.y);
+            put4(v.z);
+            put4(v.w);
+        }
+        for (; i + 4 <= len; i += 4)
+            put4(rd32(s + i));
+        for (; i < len; i++)
             put(s[i]);
     }
     __device__ __forceinline__ void flush()
@@ -135,6 +156,16 @@ __device__ __forceinline__ void emit_seq(Packer &o, const uint8_t *lits, uint32_
 __device__ __forceinline__ uint32_t count_eq(const uint8_t *s, uint32_t a, uint32_t b, uint32_t lim)
 {
     const uint32_t a0 = a;
+    while (a + 16 <= lim) {
+        const u32x4 x = *reinterpret_cast<const u32x4_ua *>(s + a) ^ *reinterpret_cast<const u32x4_ua *>(s + b);
+        if (x.x | x.y | x.z | x.w) {
+            const uint32_t q = x.x ? 0 : x.y ? 4 : x.z ? 8 : 12;
+            const uint32_t d = x.x ? x.x : x.y ? x.y : x.z ? x.z : x.w;
+            return a - a0 + q + (__builtin_ctz(d) >> 3);
+        }
+        a += 16;
+        b += 16;
+    }
     while (a + 4 <= lim) {
         const uint32_t x = rd32(s + a) ^ rd32(s + b);
         if (x)
@@ -161,30 +192,77 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, ui
         const uint32_t mflimit1 = n - 11, matchlimit = n - 5;
         T[hash4(rd32(s))] = 0;
         uint32_t ip = 1;
-        uint32_t fwd_h = hash4(rd32(s + 1));
         for (;;) {
             uint32_t m;
             {
+                // kProbe probes at a time: their positions follow the step
+                // schedule alone, so the input words, the table entries and
+                // the candidates' words are each loaded as one batch; a probe
+                // whose hash an earlier probe of the batch wrote takes that
+                // probe's position (what the serial loop would read back)
                 uint32_t fwd = ip, step = 1, nb = accel << 6;
                 for (;;) {
-                    const uint32_t h = fwd_h;
-                    const uint32_t cand = T[h];
-                    ip = fwd;
-                    fwd += step;
-                    step = nb++ >> 6;
-                    if (fwd > mflimit1)
-                        goto last_literals;
-                    m = cand;
-                    fwd_h = hash4(rd32(s + fwd));
-                    T[h] = (uint16_t)ip;
-                    if (rd32(s + m) == rd32(s + ip))
+                    uint32_t pk[kProbe], in[kProbe], hk[kProbe], ck[kProbe], cw[kProbe];
+                    uint32_t f = fwd, st = step, nbb = nb, nvalid = kProbe;
+#pragma unroll
+                    for (uint32_t k = 0; k < kProbe; k++) {
+                        pk[k] = f;
+                        f += st;
+                        st = nbb++ >> 6;
+                        if (f > mflimit1 && nvalid == kProbe)
+                            nvalid = k;   // probe k ends the search (liblz4: goto _last_literals)
+                    }
+#pragma unroll
+                    for (uint32_t k = 0; k < kProbe; k++)
+                        in[k] = rd32(s + min(pk[k], mflimit1));
+#pragma unroll
+                    for (uint32_t k = 0; k < kProbe; k++) {
+                        hk[k] = hash4(in[k]);
+                        ck[k] = T[hk[k]];
+                    }
+#pragma unroll
+                    for (uint32_t k = 1; k < kProbe; k++)
+#pragma unroll
+                        for (uint32_t j = 0; j < k; j++)
+                            ck[k] = hk[j] == hk[k] ? pk[j] : ck[k];
+#pragma unroll
+                    for (uint32_t k = 0; k < kProbe; k++)
+                        cw[k] = rd32(s + min(ck[k], mflimit1));   // clamped: probes past nvalid
+                    uint32_t hit = kProbe;
+#pragma unroll
+                    for (uint32_t k = kProbe; k-- > 0;)
+                        hit = (k < nvalid && cw[k] == in[k]) ? k : hit;
+#pragma unroll
+                    for (uint32_t k = 0; k < kProbe; k++)   // the probes that ran, in order
+                        if (k < nvalid && k <= hit)
+                            T[hk[k]] = (uint16_t)pk[k];
+                    if (hit < kProbe) {
+                        ip = pk[hit];
+                        m = ck[hit];
                         break;
+                    }
+                    if (nvalid < kProbe)
+                        goto last_literals;
+                    fwd = f;
+                    step = st;
+                    nb = nbb;
                 }
             }
-            while (ip > anchor && m > 0 && s[ip - 1] == s[m - 1]) {
-                ip--;
-                m--;
+            // backward extension, four bytes per compare (equal top bytes of
+            // the words ending at ip and m are the bytes just before them)
+            while (m >= 4 && ip > anchor) {
+                const uint32_t x = rd32(s + ip - 4) ^ rd32(s + m - 4);
+                const uint32_t k = min(x ? (uint32_t)__builtin_clz(x) >> 3 : 4u, ip - anchor);
+                ip -= k;
+                m -= k;
+                if (k < 4)
+                    break;
             }
+            if (m < 4)
+                while (ip > anchor && m > 0 && s[ip - 1] == s[m - 1]) {
+                    ip--;
+                    m--;
+                }
             uint32_t lit = ip - anchor;
             // liblz4: after the token, op + lit + 8 + lit/255 must fit
             if (op + 1 + lit + 8 + lit / 255 > cap)
@@ -210,7 +288,6 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, ui
                 lit = 0;
             }
             ip++;
-            fwd_h = hash4(rd32(s + ip));
         }
     }
 last_literals:
