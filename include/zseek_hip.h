@@ -20,7 +20,8 @@
  *   zsk_verify_frame_checksums — the seek table's per-frame checksum,
  *                            parsed by seek_table.c:95-97 and never checked
  *                            there, checked on the GPU.
- *   zsk_lz4_compress_frames — the writer's per-frame LZ4F_compressFrame call
+ *   zsk_lz4_compress_frames, zsk_writer_set_gpu_compress — the writer's
+ *                            per-frame LZ4F_compressFrame call
  *                            (compress.c:750 direct frames, :483 buffered
  *                            ones; prefs compress.c:203-207), batched over
  *                            frames of <= 64 KiB in one grid.
@@ -251,6 +252,21 @@ ZSEEK_EXPORT size_t zsk_lz4_compress_scratch_size(uint32_t nframes);
 ZSEEK_EXPORT int zsk_lz4_compress_frames(const zsk_compress_desc_t *d_desc,
     uint32_t nframes, const void *d_src, void *d_dst, uint32_t *d_csize,
     int level, void *d_scratch, void *stream);
+
+/*
+ * Writer GPU mode: an LZ4 writer's frames of <= 64 KiB are compressed on the
+ * GPU (zsk_lz4_compress_frames, on the calling thread's current device) in
+ * batches of @batch_bytes input bytes (0: 64 MiB; (size_t)-1: GPU mode off,
+ * after writing what is queued).  The file is byte-identical to host
+ * compression.  Frames are written and logged when their batch is compressed:
+ * when it fills, when a frame the GPU does not take (> 64 KiB) arrives, at
+ * zseek_writer_stats and at zseek_writer_close; each write callback gets the
+ * call_data of the zseek_write that produced the frame, and a callback
+ * failure is reported by the call that flushed.  Env ZSEEK_GPU_COMPRESS=1
+ * (or a batch size in bytes) at open turns it on.  false for NULL, a zstd
+ * writer, an HC level (>= 3) or no HIP device.
+ */
+ZSEEK_EXPORT bool zsk_writer_set_gpu_compress(zseek_writer_t *writer, size_t batch_bytes);
 
 #ifdef __cplusplus
 }

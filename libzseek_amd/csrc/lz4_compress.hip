@@ -29,6 +29,7 @@
 // Algorithmic bytes per frame: n read + the frame's compressed size written.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/zseek_hip.h"
 #include "zsk_internal.h"
@@ -45,7 +46,7 @@ constexpr uint32_t kHashLog = 13;
 constexpr uint32_t kTable = 1u << kHashLog;   // u16 entries per frame
 constexpr uint32_t kMaxFrame = 65536;
 constexpr uint32_t kStoredFlag = 0x80000000u;
-constexpr uint32_t kProbe = 8;   // search probes per batch
+constexpr int kDefaultProbe = 16;
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t *p)
 {
@@ -183,6 +184,7 @@ __device__ __forceinline__ uint32_t count_eq(const uint8_t *s, uint32_t a, uint3
 // liblz4's LZ4_compress_generic (byU16, noDict, limitedOutput, capacity n-1)
 // on s[0..n); writes the block payload through o and returns its size, or
 // 0 when it does not fit (the frame's block is then stored raw).
+template <uint32_t kProbe>   // search probes per batch
 __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, uint16_t *__restrict__ T,
                                    Packer &o, uint32_t accel)
 {
@@ -304,6 +306,7 @@ last_literals:
     return op;
 }
 
+template <uint32_t kProbe>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_desc_t *__restrict__ desc,
                                                           uint32_t nframes, const uint8_t *__restrict__ src,
                                                           uint8_t *__restrict__ dst,
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_des
     }
     for (int i = 0; i < 4; i++)   // block word, patched below
         o.put(0);
-    const uint32_t c = compress_block(src + d.src_off, n, tables + (size_t)f * kTable, o, accel);
+    const uint32_t c = compress_block<kProbe>(src + d.src_off, n, tables + (size_t)f * kTable, o, accel);
     if (c == 0) {
         // the header stays; block word, raw block and end mark come from
         // lz4_store_kernel
@@ -407,8 +410,15 @@ int launch_lz4_compress(const zsk_compress_desc_t *d_desc, uint32_t nframes, con
     uint32_t *stored = reinterpret_cast<uint32_t *>(tables + (size_t)nframes * kTable);
     if (hipMemsetAsync(tables, 0, (size_t)nframes * kTable * sizeof(uint16_t), stream) != hipSuccess)
         return -1;
-    hipLaunchKernelGGL(lz4_compress_kernel, dim3((nframes + 63) / 64), dim3(64), 0, stream, d_desc, nframes,
-                       d_src, d_dst, d_csize, tables, stored, accel);
+    // probes per search batch: env ZSEEK_LZ4C_PROBE (tuning only)
+    static const int probe = [] {
+        const char *e = getenv("ZSEEK_LZ4C_PROBE");
+        return e ? atoi(e) : kDefaultProbe;
+    }();
+    auto kern = probe == 8 ? lz4_compress_kernel<8> : probe == 32 ? lz4_compress_kernel<32>
+                                                                   : lz4_compress_kernel<16>;
+    hipLaunchKernelGGL(kern, dim3((nframes + 63) / 64), dim3(64), 0, stream, d_desc, nframes, d_src, d_dst,
+                       d_csize, tables, stored, accel);
     hipLaunchKernelGGL(lz4_store_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes, d_src,
                        d_dst, stored);
     return hipGetLastError() == hipSuccess ? 0 : -1;

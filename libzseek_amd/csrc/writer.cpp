@@ -9,6 +9,14 @@
 // followed by a write >= min_frame_size (compress.c:791-795 checks frame_cm,
 // which LZ4 never sets) logs a frame with a stale dSize and corrupts the file;
 // here buffered bytes always end their frame first.
+//
+// GPU mode (zsk_writer_set_gpu_compress, env ZSEEK_GPU_COMPRESS; LZ4 frames
+// of <= 64 KiB, levels < 3): lz4_frame queues the frame instead of
+// compressing it, and a batch of queued frames is compressed by
+// zsk_lz4_compress_frames (csrc/lz4_compress.hip, byte-identical to
+// LZ4F_compressFrame) and then written and logged in queue order, each with
+// the call_data of the zseek_write that produced it.  Frames the GPU path
+// does not take flush the queue first, so the file is the same byte for byte.
 #include <errno.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -18,10 +26,12 @@
 #include <new>
 #include <vector>
 
+#include <hip/hip_runtime.h>
 #include <lz4frame.h>
 #include <zstd.h>
 
 #include "../../include/zseek.h"
+#include "../../include/zseek_hip.h"
 #include "host.h"
 
 using namespace zsk;
@@ -31,6 +41,45 @@ constexpr uint32_t kMaxFrames = 0x8000000u;   // ZSTD_SEEKABLE_MAXFRAMES (ref se
 
 struct FrameLogEntry {
     uint32_t c_size, d_size;
+};
+
+constexpr size_t kGpuDefaultBatch = 64u << 20;
+constexpr size_t kGpuMaxFrame = 65536;      // one LZ4 block: the GPU compressor's limit
+constexpr size_t kGpuMaxBatchFrames = 65536;
+
+// Queued LZ4 frames of a writer in GPU mode and the buffers they go through.
+struct GpuLz4 {
+    size_t batch_bytes = 0;   // 0: off
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t *h_in = nullptr, *h_out = nullptr;   // pinned staging
+    size_t in_cap = 0, out_cap = 0, in_used = 0, out_used = 0;
+    uint8_t *d_in = nullptr, *d_out = nullptr, *d_scratch = nullptr;
+    zsk_compress_desc_t *d_desc = nullptr;
+    uint32_t *d_csize = nullptr;
+    size_t d_frames = 0, d_scratch_cap = 0;
+    std::vector<zsk_compress_desc_t> desc;
+    std::vector<uint32_t> csize;
+    std::vector<void *> call_data;
+
+    void release()
+    {
+        if (device < 0)
+            return;
+        DeviceGuard keep;
+        (void)hipSetDevice(device);
+        if (stream)
+            (void)hipStreamSynchronize(stream);
+        for (void *p : {(void *)d_in, (void *)d_out, (void *)d_scratch, (void *)d_desc, (void *)d_csize})
+            if (p)
+                (void)hipFree(p);
+        for (void *p : {(void *)h_in, (void *)h_out})
+            if (p)
+                (void)hipHostFree(p);
+        if (stream)
+            hip_stream_put(stream);
+        *this = GpuLz4();
+    }
 };
 }   // namespace
 
@@ -46,6 +95,7 @@ struct zseek_writer {
     size_t total_cm = 0;
     std::vector<FrameLogEntry> log;
     std::vector<uint8_t> ubuf, cbuf;
+    GpuLz4 gpu;
 };
 
 static bool default_write(const void *data, size_t size, void *user_data, void *call_data)
@@ -76,12 +126,112 @@ static bool emit(zseek_writer *w, const void *p, size_t n, void *call_data, char
     return true;
 }
 
+// Compress the queued frames on the GPU, then write and log them in order.
+static bool gpu_flush(zseek_writer *w, char *errbuf)
+{
+    GpuLz4 &g = w->gpu;
+    const size_t n = g.desc.size();
+    if (n == 0)
+        return true;
+    DeviceGuard keep;
+    bool ok = hipSetDevice(g.device) == hipSuccess;
+    if (ok && g.d_frames < n) {
+        if (g.d_desc)
+            (void)hipFree(g.d_desc);
+        if (g.d_csize)
+            (void)hipFree(g.d_csize);
+        g.d_desc = nullptr;
+        g.d_csize = nullptr;
+        g.d_frames = 0;
+        ok = hipMalloc(&g.d_desc, n * sizeof(zsk_compress_desc_t)) == hipSuccess &&
+             hipMalloc(&g.d_csize, n * sizeof(uint32_t)) == hipSuccess;
+        if (ok)
+            g.d_frames = n;
+    }
+    const size_t scratch = zsk_lz4_compress_scratch_size((uint32_t)n);
+    if (ok && g.d_scratch_cap < scratch) {
+        if (g.d_scratch)
+            (void)hipFree(g.d_scratch);
+        g.d_scratch = nullptr;
+        g.d_scratch_cap = 0;
+        ok = hipMalloc(&g.d_scratch, scratch) == hipSuccess;
+        if (ok)
+            g.d_scratch_cap = scratch;
+    }
+    g.csize.resize(n);
+    ok = ok && hipMemcpyAsync(g.d_in, g.h_in, g.in_used, hipMemcpyHostToDevice, g.stream) == hipSuccess &&
+         hipMemcpyAsync(g.d_desc, g.desc.data(), n * sizeof(zsk_compress_desc_t), hipMemcpyHostToDevice,
+                        g.stream) == hipSuccess &&
+         zsk_lz4_compress_frames(g.d_desc, (uint32_t)n, g.d_in, g.d_out, g.d_csize, w->prefs.compressionLevel,
+                                 g.d_scratch, g.stream) == 0 &&
+         hipMemcpyAsync(g.csize.data(), g.d_csize, n * sizeof(uint32_t), hipMemcpyDeviceToHost, g.stream) ==
+             hipSuccess &&
+         hipMemcpyAsync(g.h_out, g.d_out, g.out_used, hipMemcpyDeviceToHost, g.stream) == hipSuccess &&
+         hipStreamSynchronize(g.stream) == hipSuccess;
+    std::vector<zsk_compress_desc_t> desc;
+    std::vector<void *> cds;
+    desc.swap(g.desc);
+    cds.swap(g.call_data);
+    g.in_used = g.out_used = 0;
+    if (!ok) {
+        set_error(errbuf, "%s: %s", "compress frame", "GPU compression failed");
+        return false;
+    }
+    // the frame being buffered (ubuf) keeps its counters across the flush
+    const size_t uc = w->frame_uc, cm = w->frame_cm;
+    for (size_t f = 0; f < n && ok; f++) {
+        if (g.csize[f] == 0) {
+            set_error(errbuf, "%s: %s", "compress frame", "GPU compression failed");
+            ok = false;
+            break;
+        }
+        w->frame_uc = desc[f].src_size;
+        w->frame_cm = g.csize[f];
+        ok = emit(w, g.h_out + desc[f].dst_off, g.csize[f], cds[f], errbuf) && log_frame(w, errbuf);
+    }
+    w->frame_uc = uc;
+    w->frame_cm = cm;
+    return ok;
+}
+
+// Queue one frame for the GPU (the frame's bytes are copied: the caller may
+// reuse its buffer when zseek_write returns).
+static bool gpu_queue(zseek_writer *w, const void *src, size_t n, bool with_size, void *call_data,
+                      char *errbuf)
+{
+    GpuLz4 &g = w->gpu;
+    const size_t slot = ZSK_LZ4_COMPRESS_BOUND(n);
+    if ((g.in_used + n > g.in_cap || g.out_used + slot > g.out_cap || g.desc.size() == kGpuMaxBatchFrames) &&
+        !gpu_flush(w, errbuf))
+        return false;
+    if (n)
+        memcpy(g.h_in + g.in_used, src, n);
+    zsk_compress_desc_t d;
+    d.src_off = g.in_used;
+    d.dst_off = g.out_used;
+    d.src_size = (uint32_t)n;
+    d.flags = with_size ? ZSK_COMPRESS_CONTENT_SIZE : 0;
+    g.desc.push_back(d);
+    g.call_data.push_back(call_data);
+    g.in_used += n;
+    g.out_used += slot;
+    w->frame_uc = 0;   // accounted when the batch is written (gpu_flush)
+    w->frame_cm = 0;
+    return g.in_used < g.batch_bytes || gpu_flush(w, errbuf);
+}
+
 // One LZ4 frame of src (ref compress.c:463-518 buffered, :737-786 direct).
 // content_size = 0 omits the content-size field, as the reference's direct
 // path does.
 static bool lz4_frame(zseek_writer *w, const void *src, size_t n, size_t content_size,
                       void *call_data, char *errbuf)
 {
+    if (w->gpu.batch_bytes) {
+        if (n <= kGpuMaxFrame)
+            return gpu_queue(w, src, n, content_size != 0, call_data, errbuf);
+        if (!gpu_flush(w, errbuf))   // frames stay in order
+            return false;
+    }
     w->prefs.frameInfo.contentSize = content_size;
     size_t bound = LZ4F_compressFrameBound(n, &w->prefs);
     w->cbuf.resize(bound);
@@ -146,6 +296,41 @@ static bool end_frame(zseek_writer *w, void *call_data, char *errbuf)
     return log_frame(w, errbuf);
 }
 
+extern "C" ZSEEK_EXPORT bool zsk_writer_set_gpu_compress(zseek_writer_t *w, size_t batch_bytes)
+{
+    if (!w || w->type != ZSEEK_LZ4 || w->prefs.compressionLevel >= 3)
+        return false;
+    char err[ZSEEK_ERRBUF_SIZE];
+    if (!gpu_flush(w, err))
+        return false;
+    w->gpu.release();
+    if (batch_bytes == (size_t)-1)   // off
+        return true;
+    if (batch_bytes == 0)
+        batch_bytes = kGpuDefaultBatch;
+    batch_bytes = batch_bytes < kGpuMaxFrame ? kGpuMaxFrame : batch_bytes;
+    GpuLz4 &g = w->gpu;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || hipGetDevice(&g.device) != hipSuccess) {
+        g = GpuLz4();
+        return false;
+    }
+    g.in_cap = batch_bytes + kGpuMaxFrame;
+    // a slot per frame: ZSK_LZ4_COMPRESS_BOUND(n) <= n + 39 bytes
+    g.out_cap = g.in_cap + 40 * kGpuMaxBatchFrames;
+    bool ok = hip_stream_get(&g.stream, false) == hipSuccess &&
+              hipHostMalloc((void **)&g.h_in, g.in_cap, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc((void **)&g.h_out, g.out_cap, hipHostMallocDefault) == hipSuccess &&
+              hipMalloc((void **)&g.d_in, g.in_cap) == hipSuccess &&
+              hipMalloc((void **)&g.d_out, g.out_cap) == hipSuccess;
+    if (!ok) {
+        g.release();
+        return false;
+    }
+    g.batch_bytes = batch_bytes;
+    return true;
+}
+
 extern "C" ZSEEK_EXPORT zseek_writer_t *zseek_writer_open_full(zseek_write_file_t user_file,
                                                                zseek_compression_param_t *zsp,
                                                                size_t min_frame_size,
@@ -172,6 +357,11 @@ extern "C" ZSEEK_EXPORT zseek_writer_t *zseek_writer_open_full(zseek_write_file_
         w->prefs.autoFlush = 1;
         w->prefs.frameInfo.blockSizeID = LZ4F_max64KB;
         w->ubuf.reserve(min_frame_size);
+        if (const char *e = getenv("ZSEEK_GPU_COMPRESS")) {
+            const unsigned long long v = strtoull(e, nullptr, 10);
+            if (v)
+                (void)zsk_writer_set_gpu_compress(w, v == 1 ? 0 : (size_t)v);
+        }
         return w;
     }
     int level = zsp ? zsp->params.zstd_params.compression_level : ZSTD_CLEVEL_DEFAULT;
@@ -302,6 +492,11 @@ extern "C" ZSEEK_EXPORT bool zseek_writer_close(zseek_writer_t *w, void *call_da
         set_error(errbuf, w->type == ZSEEK_LZ4 ? "end_frame_lz4 failed" : "end_frame_zstd failed");
         ok = false;
     }
+    if (ok && !gpu_flush(w, errbuf)) {
+        set_error(errbuf, "end_frame_lz4 failed");
+        ok = false;
+    }
+    w->gpu.release();
     // seekable-format seek table (ref seek_table.c:365-419): skippable
     // header, n x {cSize, dSize}, n, descriptor 0 (no checksums), magic
     std::vector<uint8_t> t(seek_table_size(w->log.size()));
@@ -342,6 +537,9 @@ extern "C" ZSEEK_EXPORT bool zseek_writer_stats(zseek_writer_t *w, zseek_writer_
         set_error(errbuf, "invalid stats pointer");
         return false;
     }
+    // queued GPU frames are written first, so the counts below include them
+    if (!gpu_flush(w, errbuf))
+        return false;
     // ref compress.c:835-881
     size_t frames = w->log.size() + (w->frame_uc > 0 ? 1 : 0);
     stats->seek_table_size = seek_table_size(w->log.size()) + (w->frame_uc > 0 ? 8 : 0);

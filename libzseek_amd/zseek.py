@@ -102,7 +102,7 @@ EXPORTED = [
     "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
     "zsk_verify_frame_checksums", "zsk_reader_set_verify_checksums",
     "zsk_reader_set_devices", "zsk_reader_devices", "zsk_reader_set_io_threads",
-    "zsk_lz4_compress_scratch_size", "zsk_lz4_compress_frames",
+    "zsk_lz4_compress_scratch_size", "zsk_lz4_compress_frames", "zsk_writer_set_gpu_compress",
 ]
 
 _lib = None
@@ -179,6 +179,8 @@ def lib() -> C.CDLL:
     L.zsk_reader_set_io_threads.argtypes = [C.c_void_p, C.c_int]
     L.zsk_reader_devices.restype = C.c_int
     L.zsk_reader_devices.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.c_int]
+    L.zsk_writer_set_gpu_compress.restype = C.c_bool
+    L.zsk_writer_set_gpu_compress.argtypes = [C.c_void_p, C.c_size_t]
     L.zsk_lz4_compress_scratch_size.restype = C.c_size_t
     L.zsk_lz4_compress_scratch_size.argtypes = [C.c_uint32]
     L.zsk_lz4_compress_frames.restype = C.c_int
@@ -302,10 +304,17 @@ class Writer:
     """zseek_writer over an in-memory sink (``getvalue()`` returns the file)."""
 
     def __init__(self, ctype: int = ZSEEK_LZ4, min_frame_size: int = 1 << 20,
-                 level: int | None = None, strategy: int = 1, nb_workers: int = 1):
+                 level: int | None = None, strategy: int = 1, nb_workers: int = 1,
+                 fail_on_callback: int | None = None):
         self._out = bytearray()
+        self.callbacks = 0          # write callbacks so far
+        self.call_data_seen = []    # call_data of each callback (None or int)
 
         def _w(ptr, size, ud, cd):
+            self.callbacks += 1
+            self.call_data_seen.append(cd)
+            if fail_on_callback is not None and self.callbacks == fail_on_callback:
+                return False
             self._out.extend(C.string_at(ptr, size))
             return True
 
@@ -324,11 +333,16 @@ class Writer:
         if not self._h:
             raise ZseekError(self._err.value.decode())
 
-    def write(self, data) -> None:
+    def write(self, data, call_data: int | None = None) -> None:
         b = bytes(data)
         buf = C.create_string_buffer(b, max(len(b), 1))
-        if not lib().zseek_write(self._h, buf, len(b), None, self._err):
+        if not lib().zseek_write(self._h, buf, len(b), call_data, self._err):
             raise ZseekError(self._err.value.decode())
+
+    def set_gpu_compress(self, batch_bytes: int = 0) -> bool:
+        """zsk_writer_set_gpu_compress: LZ4 frames of <= 64 KiB compressed on
+        the GPU in batches (0 = 64 MiB, -1 = off)."""
+        return bool(lib().zsk_writer_set_gpu_compress(self._h, batch_bytes & ((1 << 64) - 1)))
 
     def stats(self) -> dict:
         s = WriterStatsC()

@@ -96,3 +96,24 @@ def test_restatement_matches_reference_writer(oracle, ref, min_frame, write, lev
         has_size = bool(frame[4] & 0x08)
         assert has_size == (write < min_frame or f == n - 1 and len(chunk) < min_frame), f
         assert oracle.lz4f_compress_frame(chunk, level, has_size) == frame, f
+
+
+def test_writer_gpu_mode_refused_without_device(zs):
+    """zsk_writer_set_gpu_compress reports false (and the writer stays on the
+    host) where no HIP device is visible, for zstd writers and for HC levels."""
+    from conftest import gpu_available
+    data = bytes(zs.synth_buffer(300000))
+    w = zs.Writer(zs.ZSEEK_LZ4, 65536)
+    if not gpu_available():
+        assert not w.set_gpu_compress(0)
+    w.write(data)
+    img = w.close()
+    h = zs.Writer(zs.ZSEEK_LZ4, 65536)
+    h.write(data)
+    assert img == h.close()
+    z = zs.Writer(zs.ZSEEK_ZSTD, 65536)
+    assert not z.set_gpu_compress(0)
+    z.close()
+    hc = zs.Writer(zs.ZSEEK_LZ4, 65536, level=3)
+    assert not hc.set_gpu_compress(0)
+    hc.close()
