@@ -574,8 +574,28 @@ def main_compress(args, torch, dist, z, dev, world, rank):
         verified = ok
         if not ok:
             raise SystemExit("GPU frames differ from liblz4's")
-    cpu = None
+    cpu = by_frames = writer = None
     host_info = host_cpus()
+    if rank == 0 and world == 1 and not args.profile:
+        # launch time against frames per launch (a lane compresses one frame
+        # serially, so throughput grows with frames in flight)
+        by_frames = {}
+        for k in (1024, 4096, 16384):
+            if k < nfr:
+                ts = []
+                for _ in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    z.lz4_compress_frames(d_desc[: 24 * k], d_src, d_dst, csize[:k], 0, scratch,
+                                          stream.cuda_stream)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                by_frames[str(k)] = {"ms": round(min(ts), 3),
+                                     "GBps": round(k * args.frame / min(ts) / 1e6, 2)}
+        by_frames[str(nfr)] = {"ms": round(t_local / args.steps * 1e3, 3),
+                               "GBps": round(size / (t_local / args.steps) / 1e9, 2)}
+        writer = writer_end_to_end(z, data, args.frame)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_compress(z, data, args.frame, host_info, args.threads)
     if rank != 0:
@@ -584,29 +604,56 @@ def main_compress(args, torch, dist, z, dev, world, rank):
         return
     avg_s = t_local / args.steps
     alg = size + comp_bytes                  # input read once + frames written once
+    workload_c = (f"lz4c: {size / GiB:g} GiB synthetic per GPU into {args.frame >> 10}KiB "
+                  "LZ4 frames (level 0, as compress.c:203-207 / :750)")
     line = {
         "metric": METRIC_LZ4C, "value": round(size * world * args.steps / t_max / 1e9, 2),
         "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(t_max / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (SURVEY §8d generator), resident in HBM",
-        "config": {"workload": f"lz4c: {size / GiB:g} GiB synthetic per GPU into {args.frame >> 10}KiB "
-                               "LZ4 frames (level 0, as compress.c:203-207 / :750)",
+        "config": {"workload": workload_c,
                    "frame_bytes": args.frame, "frames_per_gpu": nfr, "input_bytes_per_gpu": size,
                    "compressed_bytes_per_gpu": comp_bytes,
                    "parallelism": f"x{world} independent ranks" if world > 1 else "one GPU"},
         "roofline": {"bound": "hbm", "achieved": round(alg / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / avg_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel": "lz4_compress_kernel",
+                     "traffic": traffic_from_profile("lz4_compress_kernel", workload_c),
+                     "kernel": "lz4_compress_kernel",
                      "launch": "zsk_lz4_compress_frames (memset + lz4_compress_kernel + lz4_store_kernel)",
                      "avg_launch_ms": round(avg_s * 1e3, 4), "algorithmic_bytes_per_launch": alg},
         "cpu_baseline": cpu,
         "verified_bit_exact": verified,
+        "launch_by_frames": by_frames,
+        "writer_end_to_end": writer,
         "host": host_info,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def writer_end_to_end(z, data, frame, size=1 << 30):
+    """The drop-in writer (zseek_write of frame-sized writes into an in-memory
+    sink, then zseek_writer_close) over the first `size` bytes: host liblz4
+    (the reference's path) against GPU mode with 1 GiB and 4 GiB batches
+    (host staging, PCIe both ways and the write callbacks included).  Files
+    compared byte for byte."""
+    size = min(size, data.size)
+    chunks = [data[o: o + frame] for o in range(0, size, frame)]
+    res, files = {"input_bytes": size}, {}
+    for name, batch in (("host", None), ("gpu_batch_1GiB", 1 << 30), ("gpu_batch_4GiB", 4 << 30)):
+        w = z.Writer(z.ZSEEK_LZ4, frame)
+        if batch is not None and not w.set_gpu_compress(batch):
+            res[name] = None
+            continue
+        t0 = time.perf_counter()
+        for c in chunks:
+            w.write(c)
+        files[name] = w.close()
+        res[name + "_GBps"] = round(size / (time.perf_counter() - t0) / 1e9, 3)
+    res["identical"] = len(set(files.values())) == 1
+    return res
 
 
 def cpu_baseline_compress(z, data, frame, host, threads):
@@ -792,7 +839,7 @@ def traffic_from_profile(kernel, workload):
     workload."""
     if not kernel:
         return None
-    for name in ("pmc_traffic.json", "pmc_traffic_zstd.json"):
+    for name in ("pmc_traffic.json", "pmc_traffic_zstd.json", "pmc_traffic_lz4c.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 rec = json.load(f)

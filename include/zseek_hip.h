@@ -256,7 +256,7 @@ ZSEEK_EXPORT int zsk_lz4_compress_frames(const zsk_compress_desc_t *d_desc,
 /*
  * Writer GPU mode: an LZ4 writer's frames of <= 64 KiB are compressed on the
  * GPU (zsk_lz4_compress_frames, on the calling thread's current device) in
- * batches of @batch_bytes input bytes (0: 64 MiB; (size_t)-1: GPU mode off,
+ * batches of @batch_bytes input bytes (0: 1 GiB; (size_t)-1: GPU mode off,
  * after writing what is queued).  The file is byte-identical to host
  * compression.  Frames are written and logged when their batch is compressed:
  * when it fills, when a frame the GPU does not take (> 64 KiB) arrives, at

@@ -43,7 +43,7 @@ struct FrameLogEntry {
     uint32_t c_size, d_size;
 };
 
-constexpr size_t kGpuDefaultBatch = 64u << 20;
+constexpr size_t kGpuDefaultBatch = 1u << 30;   // 16,384 frames of 64 KiB: ~20 GB/s per launch (bench launch_by_frames)
 constexpr size_t kGpuMaxFrame = 65536;      // one LZ4 block: the GPU compressor's limit
 constexpr size_t kGpuMaxBatchFrames = 65536;
 

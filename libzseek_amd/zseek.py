@@ -341,7 +341,7 @@ class Writer:
 
     def set_gpu_compress(self, batch_bytes: int = 0) -> bool:
         """zsk_writer_set_gpu_compress: LZ4 frames of <= 64 KiB compressed on
-        the GPU in batches (0 = 64 MiB, -1 = off)."""
+        the GPU in batches (0 = 1 GiB, -1 = off)."""
         return bool(lib().zsk_writer_set_gpu_compress(self._h, batch_bytes & ((1 << 64) - 1)))
 
     def stats(self) -> dict:
