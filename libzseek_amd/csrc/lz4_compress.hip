@@ -46,6 +46,7 @@ constexpr uint32_t kHashLog = 13;
 constexpr uint32_t kTable = 1u << kHashLog;   // u16 entries per frame
 constexpr uint32_t kMaxFrame = 65536;
 constexpr uint32_t kStoredFlag = 0x80000000u;
+constexpr bool kDefaultVal = true;   // position + word entries: 103.7 ms against 125.8 (u16, 4 GiB)
 constexpr int kDefaultProbe = 8;   // 8 / 16 / 32 measured 125.7 / 134.0 / 169.8 ms (4 GiB)
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t *p)
@@ -184,15 +185,25 @@ __device__ __forceinline__ uint32_t count_eq(const uint8_t *s, uint32_t a, uint3
 // liblz4's LZ4_compress_generic (byU16, noDict, limitedOutput, capacity n-1)
 // on s[0..n); writes the block payload through o and returns its size, or
 // 0 when it does not fit (the frame's block is then stored raw).
-template <uint32_t kProbe>   // search probes per batch
-__device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, uint16_t *__restrict__ T,
+// Table layouts: kVal = false is liblz4's (u16 positions; a candidate's word
+// is loaded from the input); kVal = true keeps each entry's input word beside
+// its position (u64: word << 32 | position + 1; 0 = liblz4's zeroed entry,
+// position 0), so a probe compares without loading the candidate's word.
+template <uint32_t kProbe, bool kVal>   // search probes per batch, table layout
+__device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, void *__restrict__ table,
                                    Packer &o, uint32_t accel)
 {
+    uint16_t *__restrict__ T = static_cast<uint16_t *>(table);
+    uint64_t *__restrict__ V = static_cast<uint64_t *>(table);
     const uint32_t cap = n - 1;
     uint32_t op = 0, anchor = 0;
     if (n >= 13) {
         const uint32_t mflimit1 = n - 11, matchlimit = n - 5;
-        T[hash4(rd32(s))] = 0;
+        const uint32_t first4 = rd32(s);
+        if constexpr (kVal)
+            V[hash4(first4)] = (uint64_t)first4 << 32 | 1u;
+        else
+            T[hash4(first4)] = 0;
         uint32_t ip = 1;
         for (;;) {
             uint32_t m;
@@ -217,27 +228,46 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, ui
 #pragma unroll
                     for (uint32_t k = 0; k < kProbe; k++)
                         in[k] = rd32(s + min(pk[k], mflimit1));
+                    if constexpr (kVal) {
 #pragma unroll
-                    for (uint32_t k = 0; k < kProbe; k++) {
-                        hk[k] = hash4(in[k]);
-                        ck[k] = T[hk[k]];
+                        for (uint32_t k = 0; k < kProbe; k++) {
+                            hk[k] = hash4(in[k]);
+                            const uint64_t e = V[hk[k]];
+                            ck[k] = e ? (uint32_t)e - 1 : 0;
+                            cw[k] = e ? (uint32_t)(e >> 32) : first4;
+                        }
+                    } else {
+#pragma unroll
+                        for (uint32_t k = 0; k < kProbe; k++) {
+                            hk[k] = hash4(in[k]);
+                            ck[k] = T[hk[k]];
+                        }
                     }
 #pragma unroll
                     for (uint32_t k = 1; k < kProbe; k++)
 #pragma unroll
-                        for (uint32_t j = 0; j < k; j++)
+                        for (uint32_t j = 0; j < k; j++) {
                             ck[k] = hk[j] == hk[k] ? pk[j] : ck[k];
+                            if constexpr (kVal)
+                                cw[k] = hk[j] == hk[k] ? in[j] : cw[k];
+                        }
+                    if constexpr (!kVal) {
 #pragma unroll
-                    for (uint32_t k = 0; k < kProbe; k++)
-                        cw[k] = rd32(s + min(ck[k], mflimit1));   // clamped: probes past nvalid
+                        for (uint32_t k = 0; k < kProbe; k++)
+                            cw[k] = rd32(s + min(ck[k], mflimit1));   // clamped: probes past nvalid
+                    }
                     uint32_t hit = kProbe;
 #pragma unroll
                     for (uint32_t k = kProbe; k-- > 0;)
                         hit = (k < nvalid && cw[k] == in[k]) ? k : hit;
 #pragma unroll
                     for (uint32_t k = 0; k < kProbe; k++)   // the probes that ran, in order
-                        if (k < nvalid && k <= hit)
-                            T[hk[k]] = (uint16_t)pk[k];
+                        if (k < nvalid && k <= hit) {
+                            if constexpr (kVal)
+                                V[hk[k]] = (uint64_t)in[k] << 32 | (pk[k] + 1);
+                            else
+                                T[hk[k]] = (uint16_t)pk[k];
+                        }
                     if (hit < kProbe) {
                         ip = pk[hit];
                         m = ck[hit];
@@ -280,11 +310,22 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, ui
                 anchor = ip;
                 if (ip >= mflimit1)
                     goto last_literals;
-                T[hash4(rd32(s + ip - 2))] = (uint16_t)(ip - 2);
-                const uint32_t h = hash4(rd32(s + ip));
-                const uint32_t cand = T[h];
-                T[h] = (uint16_t)ip;
-                if (rd32(s + cand) != rd32(s + ip))
+                const uint32_t w2 = rd32(s + ip - 2), w0 = rd32(s + ip);
+                const uint32_t h = hash4(w0);
+                uint32_t cand, cval;
+                if constexpr (kVal) {
+                    V[hash4(w2)] = (uint64_t)w2 << 32 | (ip - 1);
+                    const uint64_t e = V[h];
+                    cand = e ? (uint32_t)e - 1 : 0;
+                    cval = e ? (uint32_t)(e >> 32) : first4;
+                    V[h] = (uint64_t)w0 << 32 | (ip + 1);
+                } else {
+                    T[hash4(w2)] = (uint16_t)(ip - 2);
+                    cand = T[h];
+                    T[h] = (uint16_t)ip;
+                    cval = rd32(s + cand);
+                }
+                if (cval != w0)
                     break;
                 m = cand;   // immediate match: no literals, no literal check
                 lit = 0;
@@ -306,12 +347,12 @@ last_literals:
     return op;
 }
 
-template <uint32_t kProbe>
+template <uint32_t kProbe, bool kVal>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_desc_t *__restrict__ desc,
                                                           uint32_t nframes, const uint8_t *__restrict__ src,
                                                           uint8_t *__restrict__ dst,
                                                           uint32_t *__restrict__ csize,
-                                                          uint16_t *__restrict__ tables,
+                                                          uint8_t *__restrict__ tables,
                                                           uint32_t *__restrict__ stored, uint32_t accel)
 {
     const uint32_t f = blockIdx.x * 64 + threadIdx.x;
@@ -354,7 +395,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_des
     }
     for (int i = 0; i < 4; i++)   // block word, patched below
         o.put(0);
-    const uint32_t c = compress_block<kProbe>(src + d.src_off, n, tables + (size_t)f * kTable, o, accel);
+    const uint32_t c = compress_block<kProbe, kVal>(src + d.src_off, n,
+                                                    tables + (size_t)f * kTable * (kVal ? 8 : 2), o, accel);
     if (c == 0) {
         // the header stays; block word, raw block and end mark come from
         // lz4_store_kernel
@@ -406,17 +448,27 @@ int launch_lz4_compress(const zsk_compress_desc_t *d_desc, uint32_t nframes, con
     if (!d_desc || !d_src || !d_dst || !d_csize || !d_scratch || level >= 3)
         return -1;
     const uint32_t accel = level < 0 ? (level < -65536 ? 65537u : (uint32_t)(1 - level)) : 1u;
-    uint16_t *tables = static_cast<uint16_t *>(d_scratch);
-    uint32_t *stored = reinterpret_cast<uint32_t *>(tables + (size_t)nframes * kTable);
-    if (hipMemsetAsync(tables, 0, (size_t)nframes * kTable * sizeof(uint16_t), stream) != hipSuccess)
-        return -1;
-    // probes per search batch: env ZSEEK_LZ4C_PROBE (tuning only)
+    // probes per search batch and table layout: env ZSEEK_LZ4C_PROBE,
+    // ZSEEK_LZ4C_VAL (tuning only)
     static const int probe = [] {
         const char *e = getenv("ZSEEK_LZ4C_PROBE");
         return e ? atoi(e) : kDefaultProbe;
     }();
-    auto kern = probe == 16 ? lz4_compress_kernel<16> : probe == 32 ? lz4_compress_kernel<32>
-                                                                     : lz4_compress_kernel<8>;
+    static const bool val = [] {
+        const char *e = getenv("ZSEEK_LZ4C_VAL");
+        return e ? atoi(e) != 0 : kDefaultVal;
+    }();
+    uint8_t *tables = static_cast<uint8_t *>(d_scratch);
+    uint32_t *stored = reinterpret_cast<uint32_t *>(tables + (size_t)nframes * kTable * 8);
+    if (hipMemsetAsync(tables, 0, (size_t)nframes * kTable * (val ? 8 : 2), stream) != hipSuccess)
+        return -1;
+    auto kern = val ? (probe == 16   ? lz4_compress_kernel<16, true>
+                       : probe == 4  ? lz4_compress_kernel<4, true>
+                       : probe == 12 ? lz4_compress_kernel<12, true>
+                                     : lz4_compress_kernel<8, true>)
+                    : probe == 16 ? lz4_compress_kernel<16, false>
+                    : probe == 32 ? lz4_compress_kernel<32, false>
+                                  : lz4_compress_kernel<8, false>;
     hipLaunchKernelGGL(kern, dim3((nframes + 63) / 64), dim3(64), 0, stream, d_desc, nframes, d_src, d_dst,
                        d_csize, tables, stored, accel);
     hipLaunchKernelGGL(lz4_store_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes, d_src,
@@ -428,7 +480,7 @@ int launch_lz4_compress(const zsk_compress_desc_t *d_desc, uint32_t nframes, con
 
 extern "C" ZSEEK_EXPORT size_t zsk_lz4_compress_scratch_size(uint32_t nframes)
 {
-    return (size_t)nframes * (zsk::kTable * sizeof(uint16_t) + sizeof(uint32_t));
+    return (size_t)nframes * (zsk::kTable * sizeof(uint64_t) + sizeof(uint32_t));
 }
 
 extern "C" ZSEEK_EXPORT int zsk_lz4_compress_frames(const zsk_compress_desc_t *d_desc, uint32_t nframes,
