@@ -115,12 +115,25 @@ struct Packer {
     __device__ __forceinline__ void copy(const uint8_t *s, uint32_t len)
     {
         uint32_t i = 0;
-        for (; i + 16 <= len; i += 16) {
+        for (; i + 32 <= len; i += 32) {   // two loads in flight
+            const u32x4 v = *reinterpret_cast<const u32x4_ua *>(s + i);
+            const u32x4 u = *reinterpret_cast<const u32x4_ua *>(s + i + 16);
+            put4(v.x);
+            put4(v.y);
+            put4(v.z);
+            put4(v.w);
+            put4(u.x);
+            put4(u.y);
+            put4(u.z);
+            put4(u.w);
+        }
+        if (i + 16 <= len) {
             const u32x4 v = *reinterpret_cast<const u32x4_ua *>(s + i);
             put4(v.x);
             put4(v.y);
             put4(v.z);
             put4(v.w);
+            i += 16;
         }
         for (; i + 4 <= len; i += 4)
             put4(rd32(s + i));
@@ -158,6 +171,23 @@ __device__ __forceinline__ void emit_seq(Packer &o, const uint8_t *lits, uint32_
 __device__ __forceinline__ uint32_t count_eq(const uint8_t *s, uint32_t a, uint32_t b, uint32_t lim)
 {
     const uint32_t a0 = a;
+    while (a + 32 <= lim) {   // 32 bytes per round trip
+        const u32x4 x = *reinterpret_cast<const u32x4_ua *>(s + a) ^ *reinterpret_cast<const u32x4_ua *>(s + b);
+        const u32x4 y =
+            *reinterpret_cast<const u32x4_ua *>(s + a + 16) ^ *reinterpret_cast<const u32x4_ua *>(s + b + 16);
+        if (x.x | x.y | x.z | x.w) {
+            const uint32_t q = x.x ? 0 : x.y ? 4 : x.z ? 8 : 12;
+            const uint32_t d = x.x ? x.x : x.y ? x.y : x.z ? x.z : x.w;
+            return a - a0 + q + (__builtin_ctz(d) >> 3);
+        }
+        if (y.x | y.y | y.z | y.w) {
+            const uint32_t q = y.x ? 16 : y.y ? 20 : y.z ? 24 : 28;
+            const uint32_t d = y.x ? y.x : y.y ? y.y : y.z ? y.z : y.w;
+            return a - a0 + q + (__builtin_ctz(d) >> 3);
+        }
+        a += 32;
+        b += 32;
+    }
     while (a + 16 <= lim) {
         const u32x4 x = *reinterpret_cast<const u32x4_ua *>(s + a) ^ *reinterpret_cast<const u32x4_ua *>(s + b);
         if (x.x | x.y | x.z | x.w) {

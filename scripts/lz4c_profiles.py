@@ -26,7 +26,8 @@ KERNEL = "lz4_compress_kernel"
 
 def median_counter(d, ctr):
     vals = []
-    for f in glob.glob(os.path.join(src, d, "**", "*counter_collection.csv"), recursive=True):
+    files = glob.glob(os.path.join(src, d, "**", "*counter_collection.csv"), recursive=True)
+    for f in [max(files, key=os.path.getmtime)] if files else []:
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == ctr and KERNEL in r["Kernel_Name"]:
                 vals.append(float(r["Counter_Value"]))
@@ -34,8 +35,8 @@ def median_counter(d, ctr):
 
 
 stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
-if stats:
-    shutil.copy(stats[0], os.path.join(prof, f"{tag}_lz4c_kernel_stats.csv"))
+if stats:   # the newest run (gpurun_out/ accumulates earlier calls' files)
+    shutil.copy(max(stats, key=os.path.getmtime), os.path.join(prof, f"{tag}_lz4c_kernel_stats.csv"))
 bench = json.load(open(os.path.join(src, "bench.json")))
 json.dump(bench, open(os.path.join(prof, f"{tag}_lz4c_bench.json"), "w"), indent=1)
 fetch, write = median_counter("pmc_fetch", "FETCH_SIZE"), median_counter("pmc_write", "WRITE_SIZE")
