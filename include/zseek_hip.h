@@ -101,6 +101,10 @@ ZSEEK_EXPORT const char *zsk_status_string(int32_t status);
 #define ZSK_DECODER_SCAN 3
 #define ZSK_DECODER_CHUNK 4
 #define ZSK_DECODER_BLOCK 5
+/* the one-frame route (every frame through the chunk parse reading it staged
+ * in LDS), the library's own choice for batches of <= 64 frames, forced at
+ * any size */
+#define ZSK_DECODER_ONE 6
 ZSEEK_EXPORT int zsk_lz4_decode_frames_ex(const zsk_frame_desc_t *d_desc,
     uint32_t nframes, const void *d_comp, void *d_out, int32_t *d_status,
     void *stream, int decoder);

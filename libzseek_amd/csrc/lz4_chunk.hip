@@ -69,6 +69,8 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 struct Src {
     __amdgpu_buffer_rsrc_t r;
     uint32_t s0;
+    bool staged;     // one-frame route: the frame is staged whole in LDS at `lds`
+    uint32_t lds;
 };
 
 struct Win {
@@ -84,6 +86,10 @@ __device__ __forceinline__ __attribute__((address_space(3))) T *lp(uint32_t a)
 
 __device__ __forceinline__ uint32_t rd4(const Src &S, Win &W, uint32_t x)
 {
+    if (S.staged) {   // (wave-uniform) the frame staged whole: one LDS round trip
+        const uint32_t a = S.lds + (x & ~3u);
+        return __builtin_amdgcn_alignbyte(*lp<uint32_t>(a + 4), *lp<uint32_t>(a), x & 3);
+    }
     const uint32_t rx = x + S.s0;
     if (rx - W.base > 59u) {
         W.base = rx & ~15u;
@@ -375,7 +381,16 @@ __device__ __forceinline__ uint32_t hdr_xxh32(const Src &S, Win &W, uint32_t n)
     return acc;
 }
 
-__global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
+// ONE (the one-frame route, small batches: DESIGN.md §3): one frame per
+// workgroup; its kOneWaves waves stage the compressed frame in LDS (the same
+// bytes the window reads, zeros past the resource), then wave 0 parses it
+// with every read an LDS round trip instead of an HBM / L2 one.  A frame too
+// big for the stage is parsed through the window as usual.
+constexpr uint32_t kOneWaves = 4;
+constexpr uint32_t kOneStage = 65536 + 1024;   // bytes: frames of <= kOneStage - 64 compressed
+
+template <bool ONE>
+__global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
@@ -385,12 +400,38 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
 {
     __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
     __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
+    __shared__ __attribute__((aligned(16))) u32x4 stage[ONE ? kOneStage / 16 : 1];
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t w = threadIdx.x >> 6;
-    const uint32_t f = uni(blockIdx.x * kCW + w);
+    const uint32_t w = ONE ? 0 : threadIdx.x >> 6;
+    const uint32_t f = ONE ? blockIdx.x : uni(blockIdx.x * kCW + w);
     if (f >= n)
         return;
     const FrameDesc d = desc[f];
+    bool staged = false;
+    if constexpr (ONE) {
+        staged = d.c_size + 64 <= kOneStage && d.c_size >= min_csize;
+        if (staged) {
+            const Span sp = make_span(comp + d.c_off, d.c_size);
+            const uint32_t np = (d.c_size + 64) / 16;
+            for (uint32_t i0 = 0; i0 < np; i0 += 4 * 64 * kOneWaves) {
+                u32x4 v[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t i = i0 + 64 * kOneWaves * j + threadIdx.x;
+                    v[j] = load16u(sp.r, i < np ? sp.s0 + 16 * i : 0x80000000u);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t i = i0 + 64 * kOneWaves * j + threadIdx.x;
+                    if (i < np)
+                        stage[i] = v[j];
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x >= 64)
+            return;
+    }
     if (uni(d.c_size) < min_csize)
         return;   // lz4_scan_kernel's frame
     if (bfirst) {
@@ -437,6 +478,8 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
         const Span sp = make_span(comp + d.c_off, clen);
         S.r = sp.r;
         S.s0 = sp.s0;
+        S.staged = staged;
+        S.lds = (uint32_t)(uintptr_t)stage;
     }
     Win W;
     W.base = 0x80000000u;   // no resource byte is within 59 of it: the first read refills
@@ -580,15 +623,20 @@ __global__ __launch_bounds__(64 * kCW) void lz4_chunk_kernel(
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
-                     SplitScratch *blk, uint32_t min_jobs)
+                     SplitScratch *blk, uint32_t min_jobs, bool one)
 {
     if (nframes == 0)
         return 0;
-    hipLaunchKernelGGL(lz4_chunk_kernel, dim3((nframes + kCW - 1) / kCW), dim3(64 * kCW), 0, stream,
-                       d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
-                       min_csize, blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr,
-                       blk ? blk->jobs : nullptr, blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr,
-                       min_jobs);
+    if (one)
+        hipLaunchKernelGGL(lz4_chunk_kernel<true>, dim3(nframes), dim3(64 * kOneWaves), 0, stream, d_desc, nframes,
+                           d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, 0u);
+    else
+        hipLaunchKernelGGL(lz4_chunk_kernel<false>, dim3((nframes + kCW - 1) / kCW), dim3(64 * kCW), 0, stream,
+                           d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
+                           min_csize, blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr,
+                           blk ? blk->jobs : nullptr, blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr,
+                           min_jobs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -300,6 +300,21 @@ BlockRoute block_route(uint32_t nframes, int route, const ParseRoute &r)
     return {true, r.chunk_min, 16384};
 }
 constexpr uint32_t kJobsCapMax = 1u << 21;
+
+// The one-frame route: batches of a few frames -- a cached
+// reader's single-frame miss, a request's first batch -- where one frame's
+// serial chain is the whole launch: each frame's chunk parse reads it staged
+// in LDS, one frame per workgroup.  Env
+// ZSEEK_ONE_ROUTE=0 turns the automatic choice off (A/B runs); ZSEEK_PARSE
+// forcing a parse keeps it off too.
+bool one_route(uint32_t nframes, int route)
+{
+    static const bool off = [] {
+        const char *v = getenv("ZSEEK_ONE_ROUTE");
+        return (v && !strcmp(v, "0")) || getenv("ZSEEK_PARSE") != nullptr;
+    }();
+    return route == ROUTE_ONE || (route == ROUTE_AUTO && !off && nframes <= kOneMaxFrames);
+}
 }   // namespace
 
 int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipStream_t stream)
@@ -431,7 +446,8 @@ ParseRoute parse_route(uint32_t nframes, int route)
     case ROUTE_LEAN: return {0xFFFFFFFFu, 0};
     case ROUTE_SCAN: return {0xFFFFFFFFu, 0xFFFFFFFFu};
     case ROUTE_CHUNK:
-    case ROUTE_BLOCK: return {0, 0};
+    case ROUTE_BLOCK:
+    case ROUTE_ONE: return {0, 0};
     default: break;
     }
     const uint32_t cmin = chunk_parse_min(nframes);
@@ -442,6 +458,8 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route)
 {
     if (lz4_pick_engine(nframes) == ENGINE_WAVE && route == ROUTE_AUTO)
         return "lz4_wave_kernel";
+    if (one_route(nframes, route))
+        return "lz4_chunk_kernel (one-frame route)";
     const ParseRoute r = parse_route(nframes, route);
     // (block route: frames of > 64 KiB decoded; named for the compressed
     // sizes those frames have)
@@ -464,8 +482,9 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
     uint64_t *total_dev = nullptr;
     (void)hipHostGetDevicePointer((void **)&total_dev, s->total, 0);
-    const ParseRoute r = parse_route(nframes, route);
-    BlockRoute br = block_route(nframes, route, r);
+    const bool one = one_route(nframes, route);
+    const ParseRoute r = one ? ParseRoute{0, 0} : parse_route(nframes, route);
+    BlockRoute br = one ? BlockRoute{false, 0, 0} : block_route(nframes, route, r);
     const uint64_t jw = (uint64_t)nframes * kMaxBlockJobs;
     const uint32_t jlanes = (uint32_t)(jw < kJobsCapMax ? jw : kJobsCapMax);
     if (br.on && block_scratch_reserve(s, nframes, jlanes, stream) != 0)
@@ -473,11 +492,14 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     SplitScratch *blk = br.on ? s : nullptr;
     stage_mark(0, stream);
     if (stages & 1) {
-        (void)hipMemsetAsync(s->redo, 0, sizeof(uint32_t), stream);
+        // (one frame is always in order: no redo flag, no scan)
+        if (nframes > 1)
+            (void)hipMemsetAsync(s->redo, 0, sizeof(uint32_t), stream);
         hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, s->rec_base, total_dev, s->redo);
-        hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
-                           s->rec_base, total_dev, s->redo);
+        if (nframes > 1)
+            hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
+                               s->rec_base, total_dev, s->redo);
         if (blk) {
             (void)hipMemsetAsync(s->njobs, 0, sizeof(uint32_t), stream);
             hipLaunchKernelGGL(lz4_block_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
@@ -501,7 +523,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                             s->nitems, d_status, d_fail_at, stream, r.lean_min < r.chunk_min ? r.lean_min : r.chunk_min);
         if (r.chunk_min != 0xFFFFFFFFu)
             launch_lz4_chunk(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                             s->nitems, d_status, d_fail_at, stream, r.chunk_min, blk, br.min_jobs);
+                             s->nitems, d_status, d_fail_at, stream, r.chunk_min, blk, br.min_jobs, one);
     }
     stage_mark(2, stream);
     if (stages & 4)

@@ -848,7 +848,7 @@ extern "C" ZSEEK_EXPORT int zsk_lz4_decode_frames_ex(const zsk_frame_desc_t *d_d
                                                      const void *d_comp, void *d_out, int32_t *d_status,
                                                      void *stream, int decoder)
 {
-    if (decoder < ZSK_DECODER_AUTO || decoder > ZSK_DECODER_BLOCK)
+    if (decoder < ZSK_DECODER_AUTO || decoder > ZSK_DECODER_ONE)
         return -1;
     return launch_lz4_frames(reinterpret_cast<const FrameDesc *>(d_desc), nframes,
                              static_cast<const uint8_t *>(d_comp), static_cast<uint8_t *>(d_out),

@@ -66,7 +66,12 @@ const char *lz4_kernel_name(uint32_t nframes);
 // parse for every frame.
 // BLOCK: every multi-block-capable frame through the block route below (any
 // batch size, no job minimum).
-enum : int { ROUTE_AUTO = 0, ROUTE_WAVE = 1, ROUTE_LEAN = 2, ROUTE_SCAN = 3, ROUTE_CHUNK = 4, ROUTE_BLOCK = 5 };
+// ONE: the one-frame route (batches of <= kOneMaxFrames frames under AUTO):
+// every frame takes the chunk parse, reading the frame staged whole in LDS
+// (one frame per workgroup); no plan scan, no lean / scan launches.
+enum : int { ROUTE_AUTO = 0, ROUTE_WAVE = 1, ROUTE_LEAN = 2, ROUTE_SCAN = 3, ROUTE_CHUNK = 4, ROUTE_BLOCK = 5,
+             ROUTE_ONE = 6 };
+constexpr uint32_t kOneMaxFrames = 64;
 
 // Launch the LZ4 frame decoder over nframes frames (asynchronous on stream).
 // d_fail_at (optional) receives, per frame, the output offset of the block
@@ -284,7 +289,7 @@ int launch_lz4_lean_blocks(const FrameDesc *d_desc, const uint8_t *d_comp, const
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
-                     SplitScratch *blk = nullptr, uint32_t min_jobs = 0);
+                     SplitScratch *blk = nullptr, uint32_t min_jobs = 0, bool one = false);
 // Frames of at least chunk_parse_min(nframes) compressed bytes go to the
 // chunk parse: with >= 32768 frames the lane-per-frame scan has a lane for
 // every frame it needs and wins on 64 KiB frames (2.07 vs 4.18 ms parse at

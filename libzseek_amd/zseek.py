@@ -534,7 +534,7 @@ def seek_table_of(image: np.ndarray):
 
 # The library's production decoders, forced for every frame through
 # zsk_lz4_decode_frames_ex (ZSK_DECODER_*): each one complete incl. hand-offs.
-DECODERS = {"auto": 0, "wave": 1, "lean": 2, "scan": 3, "chunk": 4, "block": 5}
+DECODERS = {"auto": 0, "wave": 1, "lean": 2, "scan": 3, "chunk": 4, "block": 5, "one": 6}
 
 
 def decode_frames(desc, comp, out, status, stream: int | None = None,
