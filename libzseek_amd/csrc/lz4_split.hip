@@ -473,7 +473,7 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route)
 
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
-                     hipStream_t stream, SplitScratch *s, int route, int stages, int tune)
+                     hipStream_t stream, SplitScratch *s, int route, int stages, int tune, uint32_t stop_last)
 {
     if (nframes == 0)
         return 0;
@@ -528,7 +528,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     stage_mark(2, stream);
     if (stages & 4)
         launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                        stream, (tune >> 8) & 0xFFF, blk);
+                        stream, (tune >> 8) & 0xFFF, blk, stop_last);
     stage_mark(3, stream);
     if (hipGetLastError() != hipSuccess) {
         stage_mark(4, stream);

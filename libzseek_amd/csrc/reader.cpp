@@ -397,6 +397,12 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     if (h_hi <= h_lo)
         h_lo = h_hi = d0;
     const bool ck = r->verify && st.checksum_flag;
+    // no cache and no checksum pass: the batch's last frame is executed only
+    // as far as the request reaches into it (the reference's no-cache read
+    // also stops there, decompress.c:646-663)
+    uint32_t stop_last = 0xFFFFFFFFu;
+    if (!J.cache_cap && !ck && J.end < st.d_off[f1])
+        stop_last = (uint32_t)(J.end - st.d_off[f1 - 1]);
     (void)hipSetDevice(g.device);
     // the host copies of this slot's previous batch read its pinned bounce
     // h_out: wait for them only when reserve() will reallocate it (waiting
@@ -445,7 +451,7 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
                                          s.stream) != 0) {
             e = hipErrorOutOfMemory;
         } else if (launch_lz4_split(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, s.d_fail,
-                                    s.stream, &s.split) != 0) {
+                                    s.stream, &s.split, ROUTE_AUTO, 15, 0, stop_last) != 0) {
             e = hipErrorLaunchFailure;
         }
     }

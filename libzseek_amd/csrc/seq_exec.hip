@@ -478,7 +478,7 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     const int32_t *__restrict__ status, const uint8_t *__restrict__ lit,
     const uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
-    const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres)
+    const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, uint32_t stop_last)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * x_wave(OUTB) + (SEG ? kXW * 8 * 65 : 0)];
     const uint32_t lane = threadIdx.x & 63;
@@ -536,7 +536,11 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
         tsec[i] += tn - tmark;                                        \
         tmark = tn;                                                   \
     }
-    while (b < nit) {
+    // the batch's last frame stops once it has produced stop_last bytes (a
+    // no-cache request ending inside it needs no more; its later bytes are
+    // never read back)
+    const uint32_t stop = f + 1 == n ? stop_last : 0xFFFFFFFFu;
+    while (b < nit && produced < stop) {
         const uint64_t nxt =
             __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(irs, J.addr(b + 64, lane, nit), 0, 0));
         const uint32_t w0 = (uint32_t)cur, w1 = (uint32_t)(cur >> 32);
@@ -678,7 +682,7 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
             cur = nb == 64 ? nxt : (lane + nb < 64 ? a : c2);
         }
         // flush complete chunks (the frame's last chunk exactly)
-        const bool last = b + nb >= nit;
+        const bool last = b + nb >= nit || produced >= stop;
         const uint32_t end_c = last ? (produced + S.a0 + 15) >> 4 : (produced + S.a0) >> 4;
         if (!(DIAG & 34))
             flush_chunks4<DIAG>(S, O, fc, end_c, lane);
@@ -719,7 +723,7 @@ int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
         return 0;
     hipLaunchKernelGGL((seq_exec_kernel<0, 4096, true>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0, stream,
                        d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status, nullptr, blk->bfirst,
-                       blk->bcount, blk->jobs, blk->jres);
+                       blk->bcount, blk->jobs, blk->jres, 0xFFFFFFFFu);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #else
@@ -728,7 +732,7 @@ int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                    int version, const SplitScratch *blk)
+                    int version, const SplitScratch *blk, uint32_t stop_last)
 {
     if (nframes == 0)
         return 0;
@@ -737,7 +741,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
 #define ZSK_X(D)                                                                                          \
     hipLaunchKernelGGL((seq_exec_kernel<D, 4096, false>), grid, block, 0, stream, d_desc, nframes, d_comp, \
-                       d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr)
+                       d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr, stop_last)
 #ifdef ZSK_TUNING
     switch (version) {
     case 0x101: ZSK_X(1); break;
@@ -777,7 +781,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
         return 0;
     hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit, nullptr,
-                       nullptr, nullptr, nullptr);
+                       nullptr, nullptr, nullptr, 0xFFFFFFFFu);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -143,6 +143,9 @@ ParseRoute parse_route(uint32_t nframes, int route);
 // nframes (what a kernel trace shows), for tooling.
 const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route = ROUTE_AUTO);
 
+// stop_last: the batch's last frame is executed only until it has produced
+// that many bytes (its status still covers the whole frame; the reader's
+// no-cache requests ending inside it).
 // Two-phase decoder with caller-owned scratch (must cover nframes and the
 // frames' item slots; frames that do not fit are decoded by the wave kernel).
 // stages: bitmask 1 plan, 2 parse, 4 execute, 8 hand-offs (tuning builds
@@ -150,7 +153,7 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route = ROU
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                      hipStream_t stream, SplitScratch *s, int route = ROUTE_AUTO, int stages = 15,
-                     int tune = 0);
+                     int tune = 0, uint32_t stop_last = 0xFFFFFFFFu);
 
 // Item slots of a frame in the split decoder's scratch.  An item is 8 bytes;
 // a sequence takes one (two when extended), a stored block two.  LZ4 data
@@ -194,7 +197,7 @@ int lz4_pick_engine(uint32_t nframes);   // never ENGINE_AUTO
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                    int version = 0, const SplitScratch *blk = nullptr);
+                    int version = 0, const SplitScratch *blk = nullptr, uint32_t stop_last = 0xFFFFFFFFu);
 int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         const int32_t *d_status, hipStream_t stream, const SplitScratch *blk);
