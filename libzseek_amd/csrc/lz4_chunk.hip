@@ -42,6 +42,9 @@
 // together itself), nitems[f], status[f], fail_at[f].
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "lz4_dev.h"
 #include "zsk_internal.h"
@@ -263,10 +266,43 @@ __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B
     return -1;
 }
 
+// One-frame route: pass 1 records, for each of a lane's first kRec visited
+// tokens, (position in the chunk, output bytes and items counted before it);
+// a true range always starts at a position its lane visited (the chunk start,
+// or where the lane before stopped on this lane's mark), so its count is the
+// lane's total through pass 2 minus the record at its entry -- no count pass
+// (a lane whose entry is past its records counts as before).
+constexpr uint32_t kRec = 64;
+
+#ifdef ZSK_TUNING
+// tuning builds: the one-frame route's phase cycles ([0] staging, [1]
+// header, [2] pass 1, [3] pass 2 + owners, [4] count, [5] emit, [6] rest) and
+// per-block wave-max iteration counts ([8] pass 1, [9] pass 2, [10] emit),
+// [12] blocks; printed by launch_lz4_chunk under ZSEEK_CHUNK_TIMERS
+__device__ unsigned long long g_ctime[16];
+#define ZSK_CT(i)                                                             \
+    if (ONE) {                                                                \
+        const uint64_t tn_ = __builtin_readcyclecounter();                    \
+        if (lane == 0)                                                        \
+            atomicAdd(&g_ctime[i], (unsigned long long)(tn_ - tmark_));       \
+        tmark_ = tn_;                                                         \
+    }
+#define ZSK_CN(i, v)                                                          \
+    if (ONE) {                                                                \
+        const uint32_t m_ = wave_incl_max(v);                                 \
+        if (lane == 63)                                                       \
+            atomicAdd(&g_ctime[i], (unsigned long long)m_);                   \
+    }
+#else
+#define ZSK_CT(i)
+#define ZSK_CN(i, v)
+#endif
+
 // One compressed block over the wave.  Returns -1 (block done: *op and *k
 // advanced) or a frame status.
+template <bool ONE>
 __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane, uint32_t mapbase,
-                               uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op)
+                               uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op, uint32_t recbase)
 {
     const uint32_t bsize = B.iend - B.ib;
     // chunking: C bytes per lane (>= kMinChunk), nl lanes
@@ -280,6 +316,12 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
     const uint32_t mymap = mapbase + lane * (kMapW * 4);
 
     uint32_t entry = kNone, y = B.iend;
+    uint32_t tout = 0, tnit = 0, nrec = 0;   // ONE: counts from s through pass 2, records
+    const uint32_t myrec = recbase + lane * (kRec * 8);
+#ifdef ZSK_TUNING
+    uint64_t tmark_ = __builtin_readcyclecounter();
+    uint32_t n1_ = 0, n2_ = 0;
+#endif
     if (nl == 1) {
         entry = lane == 0 ? B.ib : kNone;
     } else {
@@ -288,17 +330,25 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
         for (uint32_t i = 0; i < kMapW; i += 4)
             *lp<u32x4>(mymap + 4 * i) = (u32x4){0, 0, 0, 0};
         wave_lds_sync();
-        uint32_t p = s, dummy0 = 0, dummy1 = 0;
+        uint32_t p = s;
         if (act) {
             while (p < t) {
                 const uint32_t r = p - s;
                 if (r < mlen)
                     __hip_atomic_fetch_or(lp<uint32_t>(mymap + 4 * (r >> 5)), 1u << (r & 31),
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                skel(S, W, p, B.iend, dummy0, dummy1);
+                if (ONE && r < mlen && nrec < kRec) {
+                    *lp<uint64_t>(myrec + 8 * nrec) = ((uint64_t)tout << 32) | (tnit << 16) | r;
+                    nrec++;
+                }
+                skel(S, W, p, B.iend, tout, tnit);
+#ifdef ZSK_TUNING
+                n1_++;
+#endif
             }
         }
         wave_lds_sync();
+        ZSK_CT(2)
         // pass 2: continue to the first position another lane visited
         if (act) {
             while (p < B.iend) {
@@ -306,7 +356,10 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
                 const uint32_t r = p - (B.ib + c * C);
                 if (r < mlen && ((*lp<uint32_t>(mapbase + c * (kMapW * 4) + 4 * (r >> 5)) >> (r & 31)) & 1))
                     break;
-                skel(S, W, p, B.iend, dummy0, dummy1);
+                skel(S, W, p, B.iend, tout, tnit);
+#ifdef ZSK_TUNING
+                n2_++;
+#endif
             }
         }
         y = p;
@@ -334,14 +387,37 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
             }
         }
     }
+    ZSK_CT(3)
     const bool tru = entry != kNone;
     // count: output bytes and items of the true range
     uint32_t out = 0, nit = 0;
-    if (tru) {
+    bool counted = false;
+    if (ONE && tru && nl > 1) {
+        // the record at entry: positions ascend, binary search
+        const uint32_t re = entry - s;
+        uint32_t lo = 0, hi = nrec;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint32_t)(*lp<uint64_t>(myrec + 8 * mid) & 0xFFFF) < re)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        if (lo < nrec) {
+            const uint64_t e = *lp<uint64_t>(myrec + 8 * lo);
+            if ((uint32_t)(e & 0xFFFF) == re) {
+                out = tout - (uint32_t)(e >> 32);
+                nit = tnit - (uint32_t)((e >> 16) & 0xFFFF);
+                counted = true;
+            }
+        }
+    }
+    if (tru && !counted) {
         uint32_t p = entry;
         while (p < y)
             skel(S, W, p, B.iend, out, nit);
     }
+    ZSK_CT(4)
     const uint32_t oinc = wave_incl_add(out), kinc = wave_incl_add(nit);
     const uint32_t ktot = lane_val(kinc, 63);
     if (k + ktot > cap)
@@ -350,6 +426,13 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
     int32_t st = -1;
     if (tru)
         st = emit_range(S, W, B, entry, y, op + oinc - out, it, k + kinc - nit);
+#ifdef ZSK_TUNING
+    ZSK_CT(5)
+    ZSK_CN(8, n1_)
+    ZSK_CN(9, n2_)
+    if (ONE && lane == 0)
+        atomicAdd(&g_ctime[12], 1ull);
+#endif
     const uint64_t fails = __ballot(st >= 0);
     if (fails) {
         const int32_t fs = (int32_t)lane_val((uint32_t)st, __builtin_ctzll(fails));
@@ -401,12 +484,17 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
     __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
     __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
     __shared__ __attribute__((aligned(16))) u32x4 stage[ONE ? kOneStage / 16 : 1];
+    __shared__ __attribute__((aligned(16))) uint64_t recs[ONE ? 64 * kRec : 1];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = ONE ? 0 : threadIdx.x >> 6;
     const uint32_t f = ONE ? blockIdx.x : uni(blockIdx.x * kCW + w);
     if (f >= n)
         return;
     const FrameDesc d = desc[f];
+#ifdef ZSK_TUNING
+    uint64_t tmark_ = __builtin_readcyclecounter();
+    const uint64_t tstart_ = tmark_;
+#endif
     bool staged = false;
     if constexpr (ONE) {
         staged = d.c_size + 64 <= kOneStage && d.c_size >= min_csize;
@@ -431,6 +519,7 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
         __syncthreads();
         if (threadIdx.x >= 64)
             return;
+        ZSK_CT(0)
     }
     if (uni(d.c_size) < min_csize)
         return;   // lz4_scan_kernel's frame
@@ -546,6 +635,7 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
         const uint64_t csize = csz ? ((uint64_t)rd4(S, W, 6) | ((uint64_t)rd4(S, W, 10) << 32)) : 0;
         const uint32_t max_block = 1u << (8 + 2 * bsid);
         uint32_t ip = hdr;
+        ZSK_CT(1)
         st = -1;
         while (st < 0) {
             fail_op = op;
@@ -602,7 +692,8 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
                 st = block_fail(B, bsid, max_block);
                 break;
             }
-            const int32_t bs = chunk_block(S, W, B, lane, mapbase, it, k, cap, op);
+            const int32_t bs =
+                chunk_block<ONE>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs);
             if (bs == ST_BLOCK_ERR)
                 st = block_fail(B, bsid, max_block);
             else if (bs >= 0)
@@ -610,6 +701,10 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
             ip = B.iend;
         }
     } while (false);
+#ifdef ZSK_TUNING
+    if (ONE && lane == 0)
+        atomicAdd(&g_ctime[7], (unsigned long long)(__builtin_readcyclecounter() - tstart_));
+#endif
     if (lane == 0) {
         status[f] = st;
         nitems[f] = k;
@@ -627,16 +722,38 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 {
     if (nframes == 0)
         return 0;
-    if (one)
+    if (one) {
         hipLaunchKernelGGL(lz4_chunk_kernel<true>, dim3(nframes), dim3(64 * kOneWaves), 0, stream, d_desc, nframes,
                            d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
                            nullptr, nullptr, nullptr, nullptr, 0u);
-    else
+#ifdef ZSK_TUNING
+        if (getenv("ZSEEK_CHUNK_TIMERS")) {
+            unsigned long long z[16];
+            (void)hipStreamSynchronize(stream);
+            (void)hipMemcpyFromSymbol(z, HIP_SYMBOL(g_ctime), sizeof(z), 0, hipMemcpyDeviceToHost);
+            static unsigned long long acc[16];
+            static int calls = 0;
+            for (int i = 0; i < 16; i++)
+                acc[i] += z[i];
+            memset(z, 0, sizeof(z));
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ctime), z, sizeof(z), 0, hipMemcpyHostToDevice);
+            if (++calls % 100 == 0) {
+                const double nf = (double)calls, nb = (double)(acc[12] ? acc[12] : 1);
+                fprintf(stderr,
+                        "chunk one-route cycles per frame: stage %.0f hdr %.0f pass1 %.0f pass2+own %.0f count %.0f "
+                        "emit %.0f total %.0f | per block wave-max iters: pass1 %.1f pass2 %.1f (%d frames)\n",
+                        acc[0] / nf, acc[1] / nf, acc[2] / nf, acc[3] / nf, acc[4] / nf, acc[5] / nf, acc[7] / nf,
+                        acc[8] / nb, acc[9] / nb, calls);
+            }
+        }
+#endif
+    } else {
         hipLaunchKernelGGL(lz4_chunk_kernel<false>, dim3((nframes + kCW - 1) / kCW), dim3(64 * kCW), 0, stream,
                            d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
                            min_csize, blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr,
                            blk ? blk->jobs : nullptr, blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr,
                            min_jobs);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
