@@ -1,5 +1,5 @@
 """Single-frame read latency probe: 4 KiB zseek_pread requests at random
-offsets of a 64 KiB-frame LZ4 image (cache off), timed per request in C
+offsets of a 64 KiB-frame LZ4 (or, with a second argument `zstd`, zstd) image (cache off), timed per request in C
 (tools zsk_tool_latency).  Run under `rocprofv3 --kernel-trace --stats` to
 see where a request's time goes."""
 import ctypes as C
@@ -12,8 +12,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import libzseek_amd as z  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+codec = sys.argv[2] if len(sys.argv) > 2 else "lz4"
 data = z.synth_buffer(256 << 20)
-img = z.lz4_seekable(data, 65536)
+img = z.zstd_seekable(data, 65536) if codec == "zstd" else z.lz4_seekable(data, 65536)
 T, L = z.tools(), z.lib()
 fn = [C.cast(f, C.c_void_p) for f in (L.zseek_reader_open_full, L.zseek_pread, L.zseek_reader_close)]
 err = C.create_string_buffer(80)
@@ -26,6 +27,6 @@ failed = C.c_size_t(0)
 assert T.zsk_tool_latency(fn[1], r, offs.ctypes.data, n, 4096, buf.ctypes.data, ns.ctypes.data,
                           C.byref(failed)) == 0
 us = ns[20:].astype(np.float64) / 1e3
-print(f"4 KiB reads: p50 {np.percentile(us, 50):.1f} us  p99 {np.percentile(us, 99):.1f} us  "
+print(f"{codec} 4 KiB reads: p50 {np.percentile(us, 50):.1f} us  p99 {np.percentile(us, 99):.1f} us  "
       f"mean {us.mean():.1f} us over {len(us)}")
 T.zsk_tool_close_mem(fn[2], r)
