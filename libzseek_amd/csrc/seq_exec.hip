@@ -381,7 +381,9 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // waves per SIMD (80 VGPRs, spills); round 0's slot loads retired inside each
 // deal step; O(1) readiness pre-tests before the binary search; a persistent
 // grid with next-frame prefetch; nontemporal item / literal loads; 1, 2, 5 or
-// 8 waves per workgroup instead of kXW = 4.
+// 8 waves per workgroup instead of kXW = 4; the rounds' readiness by a
+// uniform loop over the pending lanes with readlane (no compaction, no binary
+// search: execute 2.886 vs 2.808 ms, more VALU per round).
 // Item addressing of the execute: contiguous items (JobMap<false>), or the
 // block route's job segments (JobMap<true>, below).
 template <bool SEG>
