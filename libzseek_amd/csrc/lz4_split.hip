@@ -49,11 +49,18 @@ using namespace lz4d;
 __global__ __launch_bounds__(256) void lz4_plan_direct_kernel(const FrameDesc *__restrict__ desc,
                                                                uint32_t n, uint64_t *__restrict__ rec_base,
                                                                uint64_t *__restrict__ total,
-                                                               uint32_t *__restrict__ redo)
+                                                               uint32_t *__restrict__ redo,
+                                                               int32_t *__restrict__ status,
+                                                               uint32_t *__restrict__ fail_at)
 {
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
     if (f >= n)
         return;
+    // every frame starts as not run (a parse kernel then owns it), with no
+    // failing block: the reader needs no fills of its own
+    status[f] = ST_NOT_RUN;
+    if (fail_at)
+        fail_at[f] = 0;
     const FrameDesc d = desc[f];
     const uint64_t c0 = desc[0].c_off;
     const uint64_t r = (((d.c_off - c0) >> 3) + 40ull * f + 3) & ~3ull;
@@ -496,7 +503,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         if (nframes > 1)
             (void)hipMemsetAsync(s->redo, 0, sizeof(uint32_t), stream);
         hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
-                           d_desc, nframes, s->rec_base, total_dev, s->redo);
+                           d_desc, nframes, s->rec_base, total_dev, s->redo, d_status, d_fail_at);
         if (nframes > 1)
             hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
                                s->rec_base, total_dev, s->redo);

@@ -435,9 +435,11 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         e = hipMemcpyAsync(s.d_comp, s.h_comp, csz, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(s.d_desc, s.h_desc, n * sizeof(FrameDesc), hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess)
+    // (the LZ4 two-phase decoder's plan kernel initializes both itself)
+    const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
+    if (e == hipSuccess && !lz4_split)
         e = hipMemsetD32Async((hipDeviceptr_t)s.d_status, ST_NOT_RUN, n, s.stream);
-    if (e == hipSuccess)
+    if (e == hipSuccess && !lz4_split)
         e = hipMemsetD32Async((hipDeviceptr_t)s.d_fail, 0, n, s.stream);
     if (e == hipSuccess && r->type == ZSEEK_ZSTD &&
         zstd_decode_frames(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream,
