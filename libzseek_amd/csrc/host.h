@@ -106,14 +106,12 @@ void pool_wait(CopyTicket *t);
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;   // recorded after the batch's last command
-    uint8_t *h_comp = nullptr;   // pinned: the batch's compressed span (user pread target)
+    uint8_t *h_comp = nullptr;   // pinned: the batch's compressed span (user pread target), then its descriptors
     size_t h_comp_cap = 0;
-    FrameDesc *h_desc = nullptr;   // pinned
-    size_t h_desc_cap = 0;
-    int32_t *h_status = nullptr;   // pinned, per frame
+    // pinned, per batch of n frames: n statuses, then n fail_at words (the
+    // output offset of a failure), downloaded together
+    int32_t *h_status = nullptr;
     size_t h_status_cap = 0;
-    uint32_t *h_fail = nullptr;    // pinned, per frame: output offset of a failure
-    size_t h_fail_cap = 0;
     uint32_t *h_ck = nullptr;      // pinned: the batch's seek-table checksums
     size_t h_ck_cap = 0;
     uint8_t *h_out = nullptr;      // pinned bounce of decoded bytes (host destinations)
@@ -122,12 +120,8 @@ struct Slot {
     size_t d_comp_cap = 0;
     uint8_t *d_out = nullptr;
     size_t d_out_cap = 0;
-    FrameDesc *d_desc = nullptr;
-    size_t d_desc_cap = 0;
-    int32_t *d_status = nullptr;
+    int32_t *d_status = nullptr;   // n statuses, then n fail_at words
     size_t d_status_cap = 0;
-    uint32_t *d_fail = nullptr;
-    size_t d_fail_cap = 0;
     uint32_t *d_ck = nullptr;
     size_t d_ck_cap = 0;
     SplitScratch split;   // two-phase LZ4 decoder scratch (lz4_split.hip)

@@ -421,13 +421,13 @@ bool grow_host(T **p, size_t *cap, size_t want_elems)
 bool Slot::reserve(size_t comp, size_t out, size_t host_out, size_t nframes, bool ck, char *errbuf)
 {
     if (!grow_dev(&d_comp, &d_comp_cap, comp) || !grow_dev(&d_out, &d_out_cap, out) ||
-        !grow_dev(&d_desc, &d_desc_cap, nframes) || !grow_dev(&d_status, &d_status_cap, nframes) ||
-        !grow_dev(&d_fail, &d_fail_cap, nframes) || (ck && !grow_dev(&d_ck, &d_ck_cap, nframes))) {
+        !grow_dev(&d_status, &d_status_cap, 2 * nframes) ||
+        (ck && !grow_dev(&d_ck, &d_ck_cap, nframes))) {
         set_error(errbuf, "allocate GPU decode buffers failed");
         return false;
     }
-    if (!grow_host(&h_comp, &h_comp_cap, comp) || !grow_host(&h_desc, &h_desc_cap, nframes) ||
-        !grow_host(&h_status, &h_status_cap, nframes) || !grow_host(&h_fail, &h_fail_cap, nframes) ||
+    if (!grow_host(&h_comp, &h_comp_cap, comp) ||
+        !grow_host(&h_status, &h_status_cap, 2 * nframes) ||
         (ck && !grow_host(&h_ck, &h_ck_cap, nframes)) ||
         (host_out && !grow_host(&h_out, &h_out_cap, host_out))) {
         set_error(errbuf, "allocate pinned staging failed");
@@ -453,12 +453,10 @@ void Slot::destroy()
     pool_wait(&copies);
     zstd_scratch_release_memory(&zs);
     split_scratch_free(&split);
-    for (void *p : {(void *)d_comp, (void *)d_out, (void *)d_desc, (void *)d_status, (void *)d_fail,
-                    (void *)d_ck})
+    for (void *p : {(void *)d_comp, (void *)d_out, (void *)d_status, (void *)d_ck})
         if (p)
             (void)hipFree(p);
-    for (void *p : {(void *)h_comp, (void *)h_desc, (void *)h_status, (void *)h_fail, (void *)h_ck,
-                    (void *)h_out})
+    for (void *p : {(void *)h_comp, (void *)h_status, (void *)h_ck, (void *)h_out})
         if (p)
             (void)hipHostFree(p);
     zstd_scratch_drop_streams(&zs);
@@ -468,26 +466,24 @@ void Slot::destroy()
     stream = nullptr;
     done = nullptr;
     h_comp = h_out = nullptr;
-    h_desc = nullptr;
     h_status = nullptr;
-    h_fail = h_ck = nullptr;
+    h_ck = nullptr;
     d_comp = d_out = nullptr;
-    d_desc = nullptr;
     d_status = nullptr;
-    d_fail = d_ck = nullptr;
-    h_comp_cap = h_desc_cap = h_status_cap = h_fail_cap = h_ck_cap = h_out_cap = 0;
-    d_comp_cap = d_out_cap = d_desc_cap = d_status_cap = d_fail_cap = d_ck_cap = 0;
+    d_ck = nullptr;
+    h_comp_cap = h_status_cap = h_ck_cap = h_out_cap = 0;
+    d_comp_cap = d_out_cap = d_status_cap = d_ck_cap = 0;
 }
 
 size_t Slot::device_bytes() const
 {
-    return d_comp_cap + d_out_cap + d_desc_cap * sizeof(FrameDesc) + (d_status_cap + d_fail_cap + d_ck_cap) * 4 +
+    return d_comp_cap + d_out_cap + (d_status_cap + d_ck_cap) * 4 +
            split.frames_cap * 12 + split.items_cap * 8 + zs.frames_cap * 24 + zs.lit_cap + zs.items_cap * 8;
 }
 
 size_t Slot::host_bytes() const
 {
-    return h_comp_cap + h_out_cap + h_desc_cap * sizeof(FrameDesc) + (h_status_cap + h_fail_cap + h_ck_cap) * 4;
+    return h_comp_cap + h_out_cap + (h_status_cap + h_ck_cap) * 4;
 }
 
 DeviceCtx::~DeviceCtx()

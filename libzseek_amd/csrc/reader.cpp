@@ -411,7 +411,10 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // waits for them anyway
     if (h_hi - h_lo > s.h_out_cap)
         pool_wait(&s.copies);
-    if (!s.reserve(csz, dsz, h_hi - h_lo, n, ck, J.err)) {
+    // the descriptors ride behind the compressed span (past its 256-byte
+    // read slack) in the same pinned buffer and the same upload
+    const uint64_t doff = (csz + 256 + 255) & ~255ull;
+    if (!s.reserve(doff + n * sizeof(FrameDesc), dsz, h_hi - h_lo, n, ck, J.err)) {
         J.io_failed = true;
         return false;
     }
@@ -419,8 +422,10 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         J.io_failed = true;
         return false;
     }
+    FrameDesc *const h_desc = reinterpret_cast<FrameDesc *>(s.h_comp + doff);
+    const FrameDesc *const d_desc = reinterpret_cast<const FrameDesc *>(s.d_comp + doff);
     for (size_t i = 0; i < n; i++) {
-        FrameDesc &d = s.h_desc[i];
+        FrameDesc &d = h_desc[i];
         d.c_off = st.c_off[f0 + i] - c0;
         d.d_off = st.d_off[f0 + i] - d0;
         d.c_size = (uint32_t)st.csize(f0 + i);
@@ -428,31 +433,30 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     }
     s.f0 = f0;
     s.f1 = f1;
+    // per-frame status then fail_at, back to back (one download for both)
+    uint32_t *d_fail = reinterpret_cast<uint32_t *>(s.d_status + n);
     s.h_from = h_lo - d0;
     s.h_len = h_hi - h_lo;
     hipError_t e = hipSuccess;
-    if (csz)
-        e = hipMemcpyAsync(s.d_comp, s.h_comp, csz, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(s.d_desc, s.h_desc, n * sizeof(FrameDesc), hipMemcpyHostToDevice, s.stream);
+    e = hipMemcpyAsync(s.d_comp, s.h_comp, doff + n * sizeof(FrameDesc), hipMemcpyHostToDevice, s.stream);
     // (the LZ4 two-phase decoder's plan kernel initializes both itself)
     const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
     if (e == hipSuccess && !lz4_split)
         e = hipMemsetD32Async((hipDeviceptr_t)s.d_status, ST_NOT_RUN, n, s.stream);
     if (e == hipSuccess && !lz4_split)
-        e = hipMemsetD32Async((hipDeviceptr_t)s.d_fail, 0, n, s.stream);
+        e = hipMemsetD32Async((hipDeviceptr_t)d_fail, 0, n, s.stream);
     if (e == hipSuccess && r->type == ZSEEK_ZSTD &&
-        zstd_decode_frames(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream,
-                           s.d_fail) != 0)
+        zstd_decode_frames(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream,
+                           d_fail) != 0)
         e = hipErrorLaunchFailure;
     if (e == hipSuccess && r->type == ZSEEK_LZ4) {
         if (lz4_pick_engine((uint32_t)n) == ENGINE_WAVE) {
-            if (launch_lz4_wave(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, s.d_fail, s.stream) != 0)
+            if (launch_lz4_wave(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, d_fail, s.stream) != 0)
                 e = hipErrorLaunchFailure;
-        } else if (split_scratch_reserve(&s.split, (uint32_t)n, split_items_needed(s.h_desc, (uint32_t)n),
+        } else if (split_scratch_reserve(&s.split, (uint32_t)n, split_items_needed(h_desc, (uint32_t)n),
                                          s.stream) != 0) {
             e = hipErrorOutOfMemory;
-        } else if (launch_lz4_split(s.d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, s.d_fail,
+        } else if (launch_lz4_split(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, d_fail,
                                     s.stream, &s.split, ROUTE_AUTO, 15, 0, stop_last) != 0) {
             e = hipErrorLaunchFailure;
         }
@@ -463,13 +467,11 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         memcpy(s.h_ck, st.checksum.data() + f0, n * sizeof(uint32_t));
         e = hipMemcpyAsync(s.d_ck, s.h_ck, n * sizeof(uint32_t), hipMemcpyHostToDevice, s.stream);
         if (e == hipSuccess &&
-            launch_frame_checksums(s.d_desc, (uint32_t)n, s.d_out, s.d_ck, s.d_status, s.stream) != 0)
+            launch_frame_checksums(d_desc, (uint32_t)n, s.d_out, s.d_ck, s.d_status, s.stream) != 0)
             e = hipErrorLaunchFailure;
     }
     if (e == hipSuccess)
-        e = hipMemcpyAsync(s.h_status, s.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(s.h_fail, s.d_fail, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream);
+        e = hipMemcpyAsync(s.h_status, s.d_status, 2 * n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
     // decoded bytes out: straight into a device destination (a peer copy from
     // another lane's device), or into the slot's pinned bounce once the host
     // copies of its previous batch are done
@@ -525,7 +527,7 @@ bool finish(LaneJob &J, Slot &s)
     if (bad < f1) {
         J.first_bad = bad;
         J.status = s.h_status[bad - f0];
-        J.fail_at = s.h_fail[bad - f0];
+        J.fail_at = reinterpret_cast<const uint32_t *>(s.h_status + n)[bad - f0];
         // Without a cache the reference decodes a frame only as far as the
         // request reaches (lz4_partial_ok, zstd_partial_ok).
         const uint64_t end_in = J.end - st.d_off[bad];
