@@ -36,6 +36,10 @@
 // reports.  Correctness never depends on the speculation succeeding: a chain
 // that does not join just makes its left neighbour parse further.
 //
+// One-frame route (ONE, batches of <= 64 frames): one frame per workgroup,
+// staged whole in LDS, and pass 1 records each lane's first tokens with the
+// counts before them so the count pass is skipped (below).
+//
 // Output: the items of lz4_scan.hip (8 bytes per sequence, two when a run is
 // longer than the small form holds) at rec_base[f], without the padding item
 // the older execute kernels needed (seq_exec.hip keeps an extended pair

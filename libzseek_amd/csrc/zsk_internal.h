@@ -289,6 +289,8 @@ int launch_lz4_lean_blocks(const FrameDesc *d_desc, const uint8_t *d_comp, const
 // With `blk`: a frame with a job list is accepted from its jobs' results
 // (when at least min_jobs were planned and every job parsed cleanly at its
 // speculative offset) or parsed here, its job list dropped.
+// `one` (the one-frame route; no `blk`): one frame per workgroup, the frame
+// staged whole in LDS when it fits (lz4_chunk.hip, ONE).
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
