@@ -84,7 +84,8 @@ def parse(argv=None):
                    help="fixed decoded total split over the ranks (strong scaling); "
                         "default 64 GiB (config 4) when N > 1")
     p.add_argument("--weak", action="store_true", help="N > 1: --size per rank (weak scaling)")
-    p.add_argument("--partition", choices=["contiguous", "round_robin"], default="contiguous")
+    p.add_argument("--partition", choices=["contiguous", "round_robin"], default="round_robin",
+                   help="N > 1: frame i -> rank i mod N (config 4), or contiguous slabs")
     p.add_argument("--frame", type=size_arg, default=64 << 10)
     p.add_argument("--threads", type=int, default=16, help="host threads for input generation")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -160,8 +161,22 @@ def host_cpus() -> dict:
     except OSError:
         pass
     usable = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    physical = None   # physical cores of the node (sockets x cores), for the reader's scale
+    try:
+        pairs, phys, core = set(), None, None
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("physical id"):
+                phys = ln.split(":", 1)[1].strip()
+            elif ln.startswith("core id"):
+                core = ln.split(":", 1)[1].strip()
+            elif not ln.strip() and phys is not None:
+                pairs.add((phys, core))
+                phys = core = None
+        physical = len(pairs) or None
+    except OSError:
+        pass
     return {"visible": visible, "affinity": aff, "cgroup_quota": quota, "usable": usable,
-            "model": model}
+            "physical_cores": physical, "model": model}
 
 
 # ---------------------------------------------------------------------------
@@ -435,7 +450,7 @@ def main():
         launches = 1 if zstd else (nfr + chunk_frames(args.frame) - 1) // chunk_frames(args.frame)
         # kernel_times averages per launch; a step is `launches` launches
         stages = {k: {"kernel": names[k], "avg_ms": round(v * launches, 4)} for k, v in stage_ms.items()}
-        kname = "zstd_seq_kernel" if zstd else names[max(("parse", "execute"), key=lambda k: stage_ms[k])]
+        kname = names[max(("parse", "execute"), key=lambda k: stage_ms[k])]
     dom = None
     if stages and kname:
         dk = [k for k, v in stages.items() if v["kernel"] == kname]
@@ -475,8 +490,8 @@ def main():
         "dtype": "u8",
         "data": ("harness rehearsal: gloo on CPU, a host copy of the expected bytes stands in "
                  "for the GPU decode (no measurement)" if harness else
-                 "synthetic (SURVEY §8d generator, compressed with libzstd 1.4.9 level 3 / "
-                 "strategy 1 as the reference writer does)" if zstd else
+                 (f"synthetic (SURVEY §8d generator, compressed with libzstd "
+                  f"{z.zstd_tool_version()} level 3 / strategy 1 as the reference writer does)") if zstd else
                  "synthetic (SURVEY §8d generator, compressed with liblz4 1.9.3 as the reference "
                  "writer does)"),
         "config": {"workload": workload,
@@ -672,21 +687,18 @@ def cpu_baseline_compress(z, data, frame, host, threads):
     except Exception as e:   # reference build absent
         res["one_thread_GBps"] = None
         res["one_thread_note"] = f"reference writer unavailable: {e}"
-    runs = {}
-    for t in sorted({host["usable"], host["visible"]}):
-        best = 0.0
-        for _ in range(2):
-            t0 = time.perf_counter()
-            z.lz4_seekable(data, frame, 0, t)
-            best = max(best, data.size / (time.perf_counter() - t0) / 1e9)
-        runs[t] = best
-    cores = max(runs, key=runs.get)
-    res.update({"value": round(runs[cores], 2), "cores": cores,
-                "by_threads": {str(t): round(v, 2) for t, v in runs.items()},
+    best = 0.0
+    cores = host["usable"]   # the CPUs this process may run on (affinity, cgroup quota)
+    for _ in range(2):
+        t0 = time.perf_counter()
+        z.lz4_seekable(data, frame, 0, cores)
+        best = max(best, data.size / (time.perf_counter() - t0) / 1e9)
+    res.update({"value": round(best, 2), "cores": cores, "per_core_GBps": round(best / cores, 3),
+                "node_physical_cores": host.get("physical_cores"),
                 "sample": (f"reference writer (1 thread, {frame >> 10} KiB direct writes) on the first "
                            f"{one >> 20} MiB; liblz4 LZ4F_compressFrame with the writer's prefs over "
-                           f"the whole {data.size >> 20} MiB, frames spread over T threads "
-                           f"(value: the faster T); host {host['model']}")})
+                           f"the whole {data.size >> 20} MiB, frames spread over {cores} threads "
+                           f"(the usable CPUs); host {host['model']}")})
     return res
 
 
@@ -855,8 +867,9 @@ def cpu_baseline(img, size, frame, host, zstd, with_latency):
     against liblz4 1.9.3 / libzstd 1.4.9) timed on this host: T independent
     readers over disjoint frame-aligned slices of the same image, in-memory
     pread, cache off, frame-sized zseek_pread calls.  T = 1 and T = every
-    usable core (affinity and cgroup CPU quota; when the quota is below the
-    visible CPUs, also T = all visible CPUs, quota-throttled)."""
+    usable CPU (affinity and cgroup CPU quota) — `value` and `cores`; when the
+    quota is below the visible CPUs, T = all visible CPUs is recorded beside
+    it as `oversubscribed` (quota-throttled, never the value)."""
     try:
         from oracle.oracle import REF_SO, RefBench
         rb = RefBench()
@@ -874,24 +887,30 @@ def cpu_baseline(img, size, frame, host, zstd, with_latency):
             best = max(best, nbytes / secs / 1e9)
         return best
 
-    runs = {usable: best_of(usable)}
-    if host["visible"] > usable:   # every visible CPU too (the cgroup quota may throttle it)
-        runs[host["visible"]] = best_of(host["visible"])
-    cores = max(runs, key=runs.get)
-    res = {"value": round(runs[cores], 2), "unit": "GB/s", "cores": cores, "kind": "reference",
+    # value = the CPUs this process may actually run on (affinity and the
+    # cgroup quota); T = every visible CPU is recorded beside it only: under a
+    # quota those threads share `usable` CPUs' time and measure the quota
+    value = best_of(usable)
+    res = {"value": round(value, 2), "unit": "GB/s", "cores": usable, "kind": "reference",
+           "per_core_GBps": round(value / usable, 3),
            "one_thread_GBps": round(b1 / s1 / 1e9, 2),
-           "by_threads": {str(t): round(v, 2) for t, v in sorted(runs.items())},
-           "sample": (f"{'zstd' if zstd else 'LZ4'}: the whole {size >> 20} MiB image decoded by T "
-                      f"reference readers (cache_size=0, {frame >> 10} KiB zseek_pread calls), best of "
-                      f"3, T = {' and '.join(str(t) for t in sorted(runs))} (value: the faster); 1 "
-                      f"reader on the first {one >> 20} MiB; host {host['model']}, {host['visible']} "
-                      f"CPUs visible, affinity {host['affinity']}, cgroup CPU quota "
-                      f"{host['cgroup_quota']}")}
+           "node_physical_cores": host.get("physical_cores"),
+           "sample": (f"{'zstd' if zstd else 'LZ4'}: the whole {size >> 20} MiB image decoded by "
+                      f"{usable} reference readers (cache_size=0, {frame >> 10} KiB zseek_pread calls; "
+                      f"liblz4 {rb.versions['lz4']} / libzstd {rb.versions['zstd']} in the reference's own "
+                      f"link namespace), best of 3; 1 reader on the first {one >> 20} MiB; host "
+                      f"{host['model']}: {usable} usable CPUs (affinity {host['affinity']}, cgroup quota "
+                      f"{host['cgroup_quota']}) of {host['visible']} visible, "
+                      f"{host.get('physical_cores')} physical cores in the node")}
+    if host["visible"] > usable:   # informational: every visible CPU, quota-throttled
+        res["oversubscribed"] = {"threads": host["visible"], "GBps": round(best_of(host["visible"], 2), 2),
+                                 "note": "threads beyond the cgroup quota share the usable CPUs' time"}
     if with_latency:
         import ctypes as C
         import libzseek_amd as z
         T = z.tools()
-        RL = C.CDLL(REF_SO)
+        from oracle.oracle import ref_cdll
+        RL = ref_cdll(REF_SO)
         fn = [C.cast(f, C.c_void_p) for f in (RL.zseek_reader_open_full, RL.zseek_pread,
                                               RL.zseek_reader_close)]
         res["latency_4k_us"] = {f"cache{c}": latency_of(T, *fn, img, size, 4096, c, 1000, 7)

@@ -241,7 +241,8 @@ typedef struct {
 #define ZSK_LZ4_COMPRESS_BOUND(n) ((((uint64_t)(n)) + 24 + 15) & ~(uint64_t)15)
 
 /* Device scratch bytes zsk_lz4_compress_frames needs for @nframes frames
- * (a 16 KiB position table per frame). */
+ * (a 64 KiB table of position + input-word entries per frame); size scratch
+ * with this call, not from the comment. */
 ZSEEK_EXPORT size_t zsk_lz4_compress_scratch_size(uint32_t nframes);
 
 /*
@@ -265,8 +266,15 @@ ZSEEK_EXPORT int zsk_lz4_compress_frames(const zsk_compress_desc_t *d_desc,
  * compression.  Frames are written and logged when their batch is compressed:
  * when it fills, when a frame the GPU does not take (> 64 KiB) arrives, at
  * zseek_writer_stats and at zseek_writer_close; each write callback gets the
- * call_data of the zseek_write that produced the frame, and a callback
- * failure is reported by the call that flushed.  Env ZSEEK_GPU_COMPRESS=1
+ * call_data of the zseek_write that produced the frame.  Deferred writes:
+ * zseek_write returns true once its frame is QUEUED, so a compression or
+ * write-callback failure of a queued frame is reported by the later call
+ * that flushes (zseek_write, zseek_writer_stats or zseek_writer_close), not
+ * by the zseek_write that queued it, and the writer then stays failed: every
+ * later call, close included, returns false.  Staging is allocated at the
+ * first queued frame and grows with the queue; frames per batch are capped
+ * so the compressor's scratch (64 KiB per frame) stays within @batch_bytes.
+ * Env ZSEEK_GPU_COMPRESS=1
  * (or a batch size in bytes) at open turns it on.  false for NULL, a zstd
  * writer, an HC level (>= 3) or no HIP device.
  */

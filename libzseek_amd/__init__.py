@@ -10,5 +10,5 @@ from .zseek import (  # noqa: F401
     seek_table_of, status_string, lz4_compress_bound, lz4_compress_frames, lz4_compress_layout,
     lz4_compress_scratch_size,
     synth_buffer, tools, verify_frame_checksums, with_frame_checksums, zstd_decode_frames,
-    zstd_seekable,
+    zstd_seekable, zstd_tool_version,
 )

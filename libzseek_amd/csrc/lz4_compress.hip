@@ -18,8 +18,8 @@
 // for decision.
 //
 // Mapping: one lane per frame (the parse is inherently serial: every table
-// entry depends on all earlier probes).  The lane's 16 KiB position table
-// lives in HBM scratch (zeroed per launch: liblz4's fresh state); input is
+// entry depends on all earlier probes).  The lane's 64 KiB table (8-byte
+// position + input-word entries, zsk_lz4_compress_scratch_size) lives in HBM scratch (zeroed per launch: liblz4's fresh state); input is
 // read in place; output goes through a little-endian dword packer so each
 // lane issues dword stores.  A sequence is emitted whole once its match
 // length is known, with both limited-output checks evaluated on the byte

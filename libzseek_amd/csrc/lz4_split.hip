@@ -549,9 +549,15 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 }
 
 // Public device API (zsk_lz4_decode_frames): the host does not see the
-// descriptors, so scratch is kept per (device, stream) and sized from the
-// frame count and the item total the previous plan on that stream reported;
-// frames that do not fit go to the wave kernel and the next call grows.
+// descriptors, so scratch comes from a per-device pool and is sized before
+// the plan runs: from the compressed bytes d_comp's allocation can hold past
+// d_comp (hipMemGetAddressRange) -- the plan lays frames out at
+// (c_off - c_off[0]) / 8 + 40 f, so span / 8 + 44 n + 64 slots always fit
+// frames stored in file order in that span, whatever their size -- else for
+// 64 KiB frames; and never below the item total the previous plan on that
+// set reported.  Frames that still do not fit go to the wave kernel and the
+// next call grows.  (Round 3 sized a first call for 64 KiB frames only, so
+// a first call over 1 MiB frames handed every frame to the wave kernel.)
 // `route` (ROUTE_*) forces one production decoder for every frame (tests).
 int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                       uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream,
@@ -565,11 +571,19 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
     SplitScratch *s = pool.acquire(stream);
     if (!s)
         return -1;
-    // first call: room for 64 KiB frames (capped at 4 GiB of items); later
-    // calls: what the previous plan on this stream needed
     uint64_t want = (uint64_t)nframes * slots_of(65536 + 64);
     if (want > (512ull << 20))
         want = 512ull << 20;
+    hipDeviceptr_t base = 0;
+    size_t bytes = 0;
+    if (hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t)d_comp) == hipSuccess && bytes &&
+        (uintptr_t)d_comp >= (uintptr_t)base && (uintptr_t)d_comp < (uintptr_t)base + bytes) {
+        const uint64_t span = (uintptr_t)base + bytes - (uintptr_t)d_comp;
+        const uint64_t by_span = span / 8 + 44ull * nframes + 64;
+        if (by_span <= (1ull << 30))   // up to 8 GiB of items
+            want = by_span;
+    }
+    (void)hipGetLastError();   // (a failed range query is not this launch's error)
     if (s->total && *s->total > want)
         want = *s->total;
     int rc;

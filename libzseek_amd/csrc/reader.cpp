@@ -37,11 +37,13 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <atomic>
 #include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -65,7 +67,17 @@ constexpr size_t kLaneMin = 1u << 20;          // decoded bytes per lane, at lea
 struct zseek_reader {
     zseek_read_file_t user_file;
     zseek_compression_type_t type;
-    std::mutex lock;      // serialises decode + cache (ref uses a rwlock, :38)
+    // the reference's rwlock (decompress.c:38): shared for cache hits
+    // (:699-706), exclusive for misses, no-cache reads and GPU batches
+    // (:714-720); lru_lock orders the MRU promotion of concurrent hits (the
+    // reference promotes under its read lock, cache.c:125)
+    std::shared_mutex lock;
+    std::mutex lru_lock;
+    // zseek_reader_stats' changing fields, published under the exclusive
+    // lock after every change, read without the reader lock: a stats call
+    // never waits behind a multi-GiB GPU read (the reference takes its read
+    // lock, :850-875, and waits at most one frame decode)
+    std::atomic<size_t> snap_cache_memory{0}, snap_cached_frames{0}, snap_buffered{0};
     std::mutex io_lock;   // one user pread callback at a time (lanes run in threads)
     SeekTable st;
     FrameCache *cache = nullptr;   // NULL when cache_size == 0 (ref :219-227)
@@ -627,6 +639,35 @@ bool ensure_lanes(zseek_reader *r, char *errbuf)
     return true;
 }
 
+// The reader's stats fields that change (cache, staging) -> the lock-free
+// snapshot zseek_reader_stats reads; called under the exclusive lock.
+void publish_stats(zseek_reader *r)
+{
+    r->snap_cache_memory.store(r->cache ? r->cache->memory_usage() : 0, std::memory_order_relaxed);
+    r->snap_cached_frames.store(r->cache ? r->cache->entries() : 0, std::memory_order_relaxed);
+    size_t buffered = 0;
+    for (auto &l : r->lanes)
+        buffered += l->host_bytes();
+    r->snap_buffered.store(buffered, std::memory_order_relaxed);
+}
+
+// bytes [rel, rel + count) of a cached frame (len bytes) -> the caller's
+// buffer (ref decompress.c:786-790)
+ssize_t copy_slice(void *buf, const uint8_t *data, size_t len, size_t rel, size_t count, bool device_dst,
+                   char *errbuf)
+{
+    size_t n = count < len - rel ? count : len - rel;
+    if (device_dst) {
+        if (n && hipMemcpy(buf, data + rel, n, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error(errbuf, "copy decoded data failed");
+            return -1;
+        }
+    } else {
+        memcpy(buf, data + rel, n);
+    }
+    return (ssize_t)n;
+}
+
 // Range read: [offset, offset+count) into buf (host or device memory), both
 // codecs (ref decompress.c:685-804 LZ4, :377-574 zstd).
 ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, void *call_data,
@@ -636,17 +677,35 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
     int64_t fi = st.frame_of(offset);
     if (fi < 0)
         return 0;   // EOF (ref decompress.c:695-697)
-    std::lock_guard<std::mutex> guard(r->lock);
     DeviceGuard keep_device;   // the caller's current device is restored on return
     const size_t f_first = (size_t)fi;
     const uint64_t end = offset + count < st.decompressed_size() ? offset + count
                                                                  : st.decompressed_size();
+    const bool one_cached = r->cache && (count == 0 || (size_t)st.frame_of(end - 1) == f_first);
+    // a cache hit under the shared lock (decompress.c:699-706): concurrent
+    // hits copy at once; a frame is only evicted under the exclusive lock
+    if (one_cached) {
+        std::shared_lock<std::shared_mutex> shared(r->lock);
+        size_t len = 0;
+        const uint8_t *data;
+        {
+            std::lock_guard<std::mutex> g(r->lru_lock);
+            data = r->cache->find(f_first, &len);
+        }
+        if (data)
+            return copy_slice(buf, data, len, offset - st.d_off[f_first], count, device_dst, errbuf);
+    }
+    std::unique_lock<std::shared_mutex> guard(r->lock);
+    struct Publish {   // the stats snapshot once this request is done
+        zseek_reader *r;
+        ~Publish() { publish_stats(r); }
+    } publish{r};
     // single-frame request with a cache: the reference's cached path
     // (decompress.c:699-796), GPU-decoded on a miss (one batch of one frame,
     // one synchronisation)
-    if (r->cache && (count == 0 || (size_t)st.frame_of(end - 1) == f_first)) {
+    if (one_cached) {
         size_t len = 0;
-        const uint8_t *data = r->cache->find(f_first, &len);
+        const uint8_t *data = r->cache->find(f_first, &len);   // (another thread's miss may have filled it)
         if (!data) {
             if (!ensure_lanes(r, errbuf))
                 return -1;
@@ -679,17 +738,7 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
             }
             data = r->cache->find(f_first, &len);
         }
-        size_t rel = offset - st.d_off[f_first];
-        size_t n = count < len - rel ? count : len - rel;
-        if (device_dst) {
-            if (n && hipMemcpy(buf, data + rel, n, hipMemcpyHostToDevice) != hipSuccess) {
-                set_error(errbuf, "copy decoded data failed");
-                return -1;
-            }
-        } else {
-            memcpy(buf, data + rel, n);
-        }
-        return (ssize_t)n;
+        return copy_slice(buf, data, len, offset - st.d_off[f_first], count, device_dst, errbuf);
     }
     if (count == 0)
         return 0;
@@ -828,16 +877,14 @@ extern "C" ZSEEK_EXPORT bool zseek_reader_stats(zseek_reader_t *reader,
         set_error(errbuf, "invalid stats pointer");
         return false;
     }
-    std::lock_guard<std::mutex> guard(reader->lock);
+    // the seek table is immutable after open; the rest is the snapshot the
+    // last request published (no reader lock: see publish_stats)
     stats->seek_table_memory = reader->st.memory_usage();
     stats->frames = reader->st.frames();
     stats->decompressed_size = reader->st.decompressed_size();
-    stats->cache_memory = reader->cache ? reader->cache->memory_usage() : 0;
-    stats->cached_frames = reader->cache ? reader->cache->entries() : 0;
-    size_t buffered = 0;
-    for (auto &l : reader->lanes)
-        buffered += l->host_bytes();
-    stats->buffer_size = buffered;
+    stats->cache_memory = reader->snap_cache_memory.load(std::memory_order_relaxed);
+    stats->cached_frames = reader->snap_cached_frames.load(std::memory_order_relaxed);
+    stats->buffer_size = reader->snap_buffered.load(std::memory_order_relaxed);
     return true;
 }
 
@@ -955,7 +1002,7 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader, zsk_gp
 {
     if (!reader || !s)
         return false;
-    std::lock_guard<std::mutex> guard(reader->lock);
+    std::unique_lock<std::shared_mutex> guard(reader->lock);
     memset(s, 0, sizeof(*s));
     s->device = reader->lanes.empty() ? -1 : reader->lanes[0]->device;
     for (auto &l : reader->lanes) {
@@ -972,7 +1019,7 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_set_batch_bytes(zseek_reader_t *reader, 
 {
     if (!reader || bytes < 4096)
         return false;
-    std::lock_guard<std::mutex> guard(reader->lock);
+    std::unique_lock<std::shared_mutex> guard(reader->lock);
     reader->batch_bytes = bytes;
     return true;
 }
@@ -983,7 +1030,7 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_set_io_threads(zseek_reader_t *reader, i
 {
     if (!reader || n < 1 || n > 64)
         return false;
-    std::lock_guard<std::mutex> guard(reader->lock);
+    std::unique_lock<std::shared_mutex> guard(reader->lock);
     reader->io_threads = n;
     return true;
 }
@@ -993,7 +1040,7 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_set_verify_checksums(zseek_reader_t *rea
 {
     if (!reader)
         return false;
-    std::lock_guard<std::mutex> guard(reader->lock);
+    std::unique_lock<std::shared_mutex> guard(reader->lock);
     reader->verify = on;
     return true;
 }
@@ -1011,9 +1058,10 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_set_devices(zseek_reader_t *reader, cons
     for (int i = 0; i < n; i++)
         if (devices[i] < 0 || devices[i] >= count)
             return false;
-    std::lock_guard<std::mutex> guard(reader->lock);
+    std::unique_lock<std::shared_mutex> guard(reader->lock);
     reader->lanes.clear();   // drains and frees the old lanes
     reader->devices.assign(devices, devices + n);
+    publish_stats(reader);
     return true;
 }
 
@@ -1023,7 +1071,7 @@ extern "C" ZSEEK_EXPORT int zsk_reader_devices(zseek_reader_t *reader, int *devi
 {
     if (!reader)
         return -1;
-    std::lock_guard<std::mutex> guard(reader->lock);
+    std::unique_lock<std::shared_mutex> guard(reader->lock);
     const int n = (int)reader->devices.size();
     for (int i = 0; devices && i < n && i < cap; i++)
         devices[i] = reader->devices[i];

@@ -12,7 +12,11 @@
 //                           a final short frame goes through the buffered path
 //                           and carries its content size, :463-518).
 //   zsk_tool_zstd_seekable  same for zstd (ZSTD_compress2, level/strategy as
-//                           compress.c:58-91, single worker).
+//                           compress.c:58-91, single worker), with the
+//                           libzstd the reference writer is built against
+//                           (1.4.9 under /opt/conda, opened by path into a
+//                           local scope) when present, else the linked one;
+//                           zsk_tool_zstd_version names the one used.
 //   zsk_tool_open_mem       a reader over an in-memory image with a C pread
 //   zsk_tool_close_mem      callback (memcpy), opened through the
 //                           zseek_reader_open_full / close of EITHER library
@@ -24,6 +28,7 @@
 //                           test/example.c:63-80 does).
 //   zsk_tool_read_all       wall time of reading [0, size) with one call
 //                           (looping on short reads).
+#include <dlfcn.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -37,6 +42,7 @@
 #include <map>
 #include <mutex>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include <lz4frame.h>
@@ -227,28 +233,78 @@ ZSK_TOOL int zsk_tool_lz4_seekable_ex(const uint8_t *in, size_t n, size_t frame_
                     });
 }
 
+namespace {
+// The compressor's libzstd: the reference's pinned 1.4.9 (SURVEY.md §8c,
+// /root/reference/meson.build:10-11) by full path -- a path dlopen maps its
+// own copy beside the system libzstd.so.1 this library links -- else the
+// linked one.
+struct ZstdApi {
+    unsigned (*version)(void) = ZSTD_versionNumber;
+    size_t (*bound)(size_t) = ZSTD_compressBound;
+    ZSTD_CCtx *(*create)(void) = ZSTD_createCCtx;
+    size_t (*reset)(ZSTD_CCtx *, ZSTD_ResetDirective) = ZSTD_CCtx_reset;
+    size_t (*set)(ZSTD_CCtx *, ZSTD_cParameter, int) = ZSTD_CCtx_setParameter;
+    size_t (*compress2)(ZSTD_CCtx *, void *, size_t, const void *, size_t) = ZSTD_compress2;
+    unsigned (*is_error)(size_t) = ZSTD_isError;
+};
+
+const ZstdApi &zstd_api()
+{
+    static const ZstdApi api = [] {
+        ZstdApi a;
+        const char *path = getenv("ZSEEK_TOOLS_LIBZSTD");
+        void *h = dlopen(path ? path : "/opt/conda/lib/libzstd.so.1.4.9", RTLD_NOW | RTLD_LOCAL);
+        if (!h)
+            return a;
+        ZstdApi b;
+        bool ok = true;
+        auto get = [&](auto &fn, const char *name) {
+            void *p = dlsym(h, name);
+            ok = ok && p;
+            if (p)
+                fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(p);
+        };
+        get(b.version, "ZSTD_versionNumber");
+        get(b.bound, "ZSTD_compressBound");
+        get(b.create, "ZSTD_createCCtx");
+        get(b.reset, "ZSTD_CCtx_reset");
+        get(b.set, "ZSTD_CCtx_setParameter");
+        get(b.compress2, "ZSTD_compress2");
+        get(b.is_error, "ZSTD_isError");
+        return ok ? b : a;
+    }();
+    return api;
+}
+}   // namespace
+
+ZSK_TOOL unsigned zsk_tool_zstd_version(void)
+{
+    return zstd_api().version();
+}
+
 ZSK_TOOL size_t zsk_tool_zstd_seekable_bound(size_t n, size_t frame_size)
 {
     size_t nf = frame_size ? (n + frame_size - 1) / frame_size : 0;
-    return nf * ZSTD_compressBound(frame_size) + 8 + 8 * nf + 9;
+    return nf * zstd_api().bound(frame_size) + 8 + 8 * nf + 9;
 }
 
 ZSK_TOOL int zsk_tool_zstd_seekable(const uint8_t *in, size_t n, size_t frame_size, int level,
                                     int strategy, int threads, uint8_t *out, size_t out_cap,
                                     size_t *out_len)
 {
-    size_t slot = ZSTD_compressBound(frame_size);
+    const ZstdApi &Z = zstd_api();
+    size_t slot = Z.bound(frame_size);
     return seekable(in, n, frame_size, threads, slot, out, out_cap, out_len,
-                    [level, strategy](uint8_t *dst, size_t cap, const uint8_t *src, size_t len,
-                                      bool) -> size_t {
+                    [level, strategy, &Z](uint8_t *dst, size_t cap, const uint8_t *src, size_t len,
+                                          bool) -> size_t {
                         thread_local ZSTD_CCtx *cctx = nullptr;
                         if (!cctx)
-                            cctx = ZSTD_createCCtx();
-                        ZSTD_CCtx_reset(cctx, ZSTD_reset_session_and_parameters);
-                        ZSTD_CCtx_setParameter(cctx, ZSTD_c_compressionLevel, level);
-                        ZSTD_CCtx_setParameter(cctx, ZSTD_c_strategy, strategy);
-                        size_t c = ZSTD_compress2(cctx, dst, cap, src, len);
-                        return ZSTD_isError(c) ? 0 : c;
+                            cctx = Z.create();
+                        Z.reset(cctx, ZSTD_reset_session_and_parameters);
+                        Z.set(cctx, ZSTD_c_compressionLevel, level);
+                        Z.set(cctx, ZSTD_c_strategy, strategy);
+                        size_t c = Z.compress2(cctx, dst, cap, src, len);
+                        return Z.is_error(c) ? 0 : c;
                     });
 }
 

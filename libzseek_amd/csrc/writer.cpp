@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -46,10 +47,14 @@ struct FrameLogEntry {
 constexpr size_t kGpuDefaultBatch = 1u << 30;   // 16,384 frames of 64 KiB: ~20 GB/s per launch (bench launch_by_frames)
 constexpr size_t kGpuMaxFrame = 65536;      // one LZ4 block: the GPU compressor's limit
 constexpr size_t kGpuMaxBatchFrames = 65536;
+constexpr size_t kGpuTableBytes = 65536;      // compressor scratch per queued frame
+constexpr size_t kGpuFirstStaging = 64u << 20;   // staging starts here, grows x2 to the batch
 
 // Queued LZ4 frames of a writer in GPU mode and the buffers they go through.
 struct GpuLz4 {
     size_t batch_bytes = 0;   // 0: off
+    size_t max_frames = 0;    // frames per flush: table scratch <= batch_bytes
+    bool failed = false;      // a flush failed: later writes and close fail too
     int device = -1;
     hipStream_t stream = nullptr;
     uint8_t *h_in = nullptr, *h_out = nullptr;   // pinned staging
@@ -79,6 +84,37 @@ struct GpuLz4 {
         if (stream)
             hip_stream_put(stream);
         *this = GpuLz4();
+    }
+
+    // pinned + device staging for in_need input bytes (a flush happened
+    // first: nothing is queued)
+    bool reserve(size_t in_need)
+    {
+        if (in_need <= in_cap)
+            return true;
+        size_t cap = in_cap ? in_cap : kGpuFirstStaging;
+        while (cap < in_need)
+            cap *= 2;
+        cap = std::min(cap, batch_bytes + kGpuMaxFrame);
+        if (cap < in_need)
+            return false;
+        for (void *p : {(void *)d_in, (void *)d_out})
+            if (p)
+                (void)hipFree(p);
+        for (void *p : {(void *)h_in, (void *)h_out})
+            if (p)
+                (void)hipHostFree(p);
+        d_in = d_out = h_in = h_out = nullptr;
+        in_cap = out_cap = 0;
+        // a slot per frame: ZSK_LZ4_COMPRESS_BOUND(n) <= n + 39 bytes
+        const size_t ocap = cap + 40 * std::min(max_frames, cap / 16 + 1);
+        if (hipHostMalloc((void **)&h_in, cap, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&h_out, ocap, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void **)&d_in, cap) != hipSuccess || hipMalloc((void **)&d_out, ocap) != hipSuccess)
+            return false;
+        in_cap = cap;
+        out_cap = ocap;
+        return true;
     }
 };
 }   // namespace
@@ -130,6 +166,10 @@ static bool emit(zseek_writer *w, const void *p, size_t n, void *call_data, char
 static bool gpu_flush(zseek_writer *w, char *errbuf)
 {
     GpuLz4 &g = w->gpu;
+    if (g.failed) {
+        set_error(errbuf, "%s: %s", "compress frame", "GPU compression failed");
+        return false;
+    }
     const size_t n = g.desc.size();
     if (n == 0)
         return true;
@@ -172,11 +212,17 @@ static bool gpu_flush(zseek_writer *w, char *errbuf)
     std::vector<void *> cds;
     desc.swap(g.desc);
     cds.swap(g.call_data);
-    g.in_used = g.out_used = 0;
     if (!ok) {
+        // copies already queued may still read the staging: drain the stream
+        // before anything reuses it; the queued frames are lost, so the
+        // writer stays failed (later writes and close return false)
+        (void)hipStreamSynchronize(g.stream);
+        g.in_used = g.out_used = 0;
+        g.failed = true;
         set_error(errbuf, "%s: %s", "compress frame", "GPU compression failed");
         return false;
     }
+    g.in_used = g.out_used = 0;
     // the frame being buffered (ubuf) keeps its counters across the flush
     const size_t uc = w->frame_uc, cm = w->frame_cm;
     for (size_t f = 0; f < n && ok; f++) {
@@ -191,6 +237,8 @@ static bool gpu_flush(zseek_writer *w, char *errbuf)
     }
     w->frame_uc = uc;
     w->frame_cm = cm;
+    if (!ok)   // frames after the failing one are not in the file
+        g.failed = true;
     return ok;
 }
 
@@ -201,9 +249,19 @@ static bool gpu_queue(zseek_writer *w, const void *src, size_t n, bool with_size
 {
     GpuLz4 &g = w->gpu;
     const size_t slot = ZSK_LZ4_COMPRESS_BOUND(n);
-    if ((g.in_used + n > g.in_cap || g.out_used + slot > g.out_cap || g.desc.size() == kGpuMaxBatchFrames) &&
+    if (g.failed)
+        return gpu_flush(w, errbuf);   // (sets the error)
+    if ((g.in_used + n > g.in_cap || g.out_used + slot > g.out_cap || g.desc.size() == g.max_frames) &&
         !gpu_flush(w, errbuf))
         return false;
+    if (g.in_used + n > g.in_cap || g.out_used + slot > g.out_cap) {   // nothing queued: grow
+        DeviceGuard keep;
+        if (hipSetDevice(g.device) != hipSuccess || !g.reserve(g.in_used + n) || g.out_used + slot > g.out_cap) {
+            g.failed = true;
+            set_error(errbuf, "%s: %s", "compress frame", "GPU staging allocation failed");
+            return false;
+        }
+    }
     if (n)
         memcpy(g.h_in + g.in_used, src, n);
     zsk_compress_desc_t d;
@@ -315,19 +373,16 @@ extern "C" ZSEEK_EXPORT bool zsk_writer_set_gpu_compress(zseek_writer_t *w, size
         g = GpuLz4();
         return false;
     }
-    g.in_cap = batch_bytes + kGpuMaxFrame;
-    // a slot per frame: ZSK_LZ4_COMPRESS_BOUND(n) <= n + 39 bytes
-    g.out_cap = g.in_cap + 40 * kGpuMaxBatchFrames;
-    bool ok = hip_stream_get(&g.stream, false) == hipSuccess &&
-              hipHostMalloc((void **)&g.h_in, g.in_cap, hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc((void **)&g.h_out, g.out_cap, hipHostMallocDefault) == hipSuccess &&
-              hipMalloc((void **)&g.d_in, g.in_cap) == hipSuccess &&
-              hipMalloc((void **)&g.d_out, g.out_cap) == hipSuccess;
-    if (!ok) {
+    // staging is allocated at the first queued frame and grows with what is
+    // queued (up to the batch); frames per flush are capped so the table
+    // scratch (64 KiB per frame) stays within batch_bytes, whatever the
+    // frame size
+    g.batch_bytes = batch_bytes;
+    g.max_frames = std::min(kGpuMaxBatchFrames, std::max<size_t>(16, batch_bytes / kGpuTableBytes));
+    if (hip_stream_get(&g.stream, false) != hipSuccess) {
         g.release();
         return false;
     }
-    g.batch_bytes = batch_bytes;
     return true;
 }
 

@@ -76,12 +76,15 @@ def all_gatherv(dist, slab, counts: list[int], out=None, group=None):
     return out
 
 
-def to_frame_order(gathered, shards: list[Shard], d_off: np.ndarray):
+def to_frame_order(gathered, shards: list[Shard], d_off: np.ndarray, chunk_bytes: int = 1 << 28):
     """Permute a rank-major gather back to frame order (round_robin plans).
 
-    Uniform frames use one strided view (a device transpose); ragged frames
-    one vectorised gather: a byte index built from per-frame (source,
-    destination, length) triples with repeat_interleave — no per-frame loop.
+    Uniform frames use one strided view (a device transpose).  Ragged frames
+    are scattered in groups of consecutive gathered frames of at most
+    ~chunk_bytes: each group's byte index (int64 per byte, built from
+    per-frame (source, destination, length) triples with repeat_interleave)
+    lives only for that group, so the index memory is bounded by
+    ~16 x chunk_bytes whatever the gather's size.
     """
     import torch
     sizes = np.diff(d_off.astype(np.int64))
@@ -92,12 +95,20 @@ def to_frame_order(gathered, shards: list[Shard], d_off: np.ndarray):
         return gathered.view(world, n // world, fs).transpose(0, 1).reshape(-1)
     order = np.concatenate([s.frames for s in shards]).astype(np.int64)   # gathered frame order
     lens = sizes[order]
-    src = np.concatenate([[0], np.cumsum(lens)[:-1]])                     # offset in gathered
+    ends = np.cumsum(lens)
+    src = np.concatenate([[0], ends[:-1]])                                # offset in gathered
     dst = d_off[:-1].astype(np.int64)[order]                               # offset in frame order
     dev = gathered.device
-    lens_t = torch.from_numpy(lens).to(dev)
-    base = torch.repeat_interleave(torch.from_numpy(dst - src).to(dev), lens_t)
-    idx = torch.arange(gathered.numel(), device=dev) + base                # destination of each byte
     out = torch.empty_like(gathered)
-    out[idx] = gathered
+    i0 = 0
+    while i0 < len(order):
+        # frames [i0, i1): at least one, then as many as fit chunk_bytes
+        i1 = max(i0 + 1, int(np.searchsorted(ends, src[i0] + chunk_bytes, side="right")))
+        a, b = int(src[i0]), int(ends[i1 - 1])
+        lens_t = torch.from_numpy(lens[i0:i1]).to(dev)
+        base = torch.repeat_interleave(torch.from_numpy(dst[i0:i1] - src[i0:i1]).to(dev), lens_t)
+        idx = torch.arange(a, b, device=dev) + base                        # destination of each byte
+        out[idx] = gathered[a:b]
+        del idx, base
+        i0 = i1
     return out

@@ -209,6 +209,8 @@ def tools() -> C.CDLL:
     T.zsk_tool_lz4_seekable.restype = C.c_int
     T.zsk_tool_lz4_seekable.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_int, C.c_int,
                                         C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
+    T.zsk_tool_zstd_version.restype = C.c_uint
+    T.zsk_tool_zstd_version.argtypes = []
     T.zsk_tool_zstd_seekable_bound.restype = C.c_size_t
     T.zsk_tool_zstd_seekable_bound.argtypes = [C.c_size_t, C.c_size_t]
     T.zsk_tool_zstd_seekable.restype = C.c_int
@@ -283,6 +285,13 @@ def lz4_seekable_ex(data: np.ndarray, frame_size: int, *, level: int = 0, bsid: 
                                   C.byref(n)) != 0:
         raise ZseekError("lz4 seekable compression failed")
     return out[: n.value]
+
+
+def zstd_tool_version() -> str:
+    """The libzstd zstd_seekable compresses with ("1.4.9": the reference
+    writer's pinned version)."""
+    v = int(tools().zsk_tool_zstd_version())
+    return f"{v // 10000}.{v // 100 % 100}.{v % 100}"
 
 
 def zstd_seekable(data: np.ndarray, frame_size: int, level: int = 3, strategy: int = 1,

@@ -44,6 +44,54 @@ ORC_ERROR_TRUNCATED = 102
 
 SYNTH_CHUNK = 64 << 20
 
+# The reference's dependency pins (/root/reference/meson.build:10-11 floors;
+# built against /opt/conda's liblz4 1.9.3 / libzstd 1.4.9).
+REF_ZSTD_VERSION = 10409
+REF_LZ4_VERSION = 10903
+
+_RTLD_NOW = 2
+_LM_ID_NEWLM = -1
+_RTLD_DI_LMID = 1
+_ref_lmid = None
+
+
+def ref_cdll(path: str) -> C.CDLL:
+    """Load a reference build (oracle/_ref/*.so) into the reference's OWN link
+    namespace (dlmopen), shared by every reference library of this process.
+
+    Loaded with a plain dlopen, libzseek_ref.so's DT_NEEDED libzstd.so.1 is
+    satisfied by whichever libzstd.so.1 the process already mapped -- the
+    system 1.4.8 our libzseek.so / libzseek_tools.so link -- so the reference
+    would run against a libzstd it was not compiled for.  In its own namespace
+    its RUNPATH (/opt/conda/lib) decides: liblz4 1.9.3 and libzstd 1.4.9, the
+    versions SURVEY.md §8c pins.  The namespace has its own libc (and malloc
+    arena); the reference never frees memory this process allocated, nor the
+    reverse, so nothing crosses heaps."""
+    global _ref_lmid
+    libc = C.CDLL(None)
+    libc.dlmopen.restype = C.c_void_p
+    libc.dlmopen.argtypes = [C.c_long, C.c_char_p, C.c_int]
+    libc.dlerror.restype = C.c_char_p
+    libc.dlinfo.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    lmid = _LM_ID_NEWLM if _ref_lmid is None else _ref_lmid
+    h = libc.dlmopen(lmid, os.fsencode(path), _RTLD_NOW)
+    if not h:
+        raise OSError(f"dlmopen {path}: {(libc.dlerror() or b'?').decode(errors='replace')}")
+    if _ref_lmid is None:
+        out = C.c_long(0)
+        if libc.dlinfo(h, _RTLD_DI_LMID, C.byref(out)) != 0:
+            raise OSError("dlinfo(RTLD_DI_LMID) failed")
+        _ref_lmid = out.value
+    return C.CDLL(os.path.basename(path), handle=h)
+
+
+def ref_dependency_versions(lib: C.CDLL) -> dict:
+    """The libzstd / liblz4 versions a reference library actually runs
+    against (dlsym through its own dependency tree)."""
+    lib.ZSTD_versionNumber.restype = C.c_uint
+    lib.LZ4_versionNumber.restype = C.c_int
+    return {"zstd": int(lib.ZSTD_versionNumber()), "lz4": int(lib.LZ4_versionNumber())}
+
 
 def _u8p(buf):
     return C.cast(buf.ctypes.data, C.POINTER(C.c_uint8))
@@ -255,7 +303,8 @@ class RefZseek:
     def __init__(self, path: str = REF_SO):
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: run `make -C oracle ref` where /root/reference exists")
-        L = self.lib = C.CDLL(path)
+        L = self.lib = ref_cdll(path)
+        self.versions = ref_dependency_versions(L)
         L.zseek_writer_open_full.restype = C.c_void_p
         L.zseek_writer_open_full.argtypes = [_WriteFile, C.POINTER(_CompParam), C.c_size_t,
                                              C.c_void_p, C.c_char_p]
@@ -359,7 +408,8 @@ class RefBench:
     def __init__(self, path: str = REF_BENCH_SO):
         if not os.path.exists(path):
             raise FileNotFoundError(path)
-        L = self.lib = C.CDLL(path)
+        L = self.lib = ref_cdll(path)
+        self.versions = ref_dependency_versions(L)
         L.ref_bench_run.restype = C.c_int
         L.ref_bench_run.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_uint64, C.c_uint64,
                                     C.c_uint64, C.c_size_t, C.c_size_t, C.c_void_p,

@@ -213,6 +213,27 @@ def test_xxhash_known_answers(oracle):
         assert (oracle.xxh32(img[c0 + 4: c0 + hdr - 1]) >> 8) & 0xFF == img[c0 + hdr - 1]
 
 
+def test_reference_runs_its_pinned_dependencies(zs, ref):
+    """The reference runs against the liblz4 1.9.3 / libzstd 1.4.9 it was
+    compiled for even with our library -- which links the
+    system libzstd 1.4.8 under the same SONAME -- loaded first; and the zstd
+    inputs our tools make come from the same libzstd."""
+    from oracle.oracle import REF_LZ4_VERSION, REF_ZSTD_VERSION, RefBench
+    zs.lib()
+    assert ref.versions == {"zstd": REF_ZSTD_VERSION, "lz4": REF_LZ4_VERSION}
+    assert RefBench().versions == ref.versions
+    assert zs.zstd_tool_version() == "1.4.9"
+
+
+def test_zstd_tool_image_equals_reference_writer(zs, oracle, ref):
+    """Config 5's input path: zstd_seekable (frames compressed in parallel by
+    the tools library) writes the file the reference writer writes for
+    frame-sized zseek_write calls (level 3, strategy 1, compress.c:58-91)."""
+    data = oracle.synth_buffer(3 << 20)
+    img = zs.zstd_seekable(data, 65536, 3, 1)
+    assert img.tobytes() == ref.compress(data.tobytes(), 0, 65536, 65536)
+
+
 def test_oracle_vs_reference_roundtrip(oracle, ref):
     """Fresh inputs through the reference writer, decoded by the oracle."""
     rng = np.random.default_rng(11)

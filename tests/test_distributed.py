@@ -108,3 +108,21 @@ def test_bench_spawns_ranks_harness(partition):
     assert d["verified_bit_exact"] is True
     assert d["reassembly"]["full_range_matches_generator"] is True
     assert (d["reassembly"]["permute_s"] is not None) == (partition == "round_robin")
+
+
+@pytest.mark.parametrize("chunk", [1, 5000, 1 << 28])
+def test_to_frame_order_chunked(chunk):
+    """Ragged round-robin permute in bounded groups (the byte index is built
+    per group of ~chunk bytes): same result for every group size, including
+    groups of one frame."""
+    from libzseek_amd import shard
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(1, 9000, 37)
+    d_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    full = (np.arange(int(d_off[-1]), dtype=np.uint64) * 2654435761 % 251).astype(np.uint8)
+    for world in (2, 3):
+        shards = shard.plan(d_off, world, "round_robin")
+        gathered = np.concatenate([full[int(d_off[i]): int(d_off[i + 1])]
+                                   for s in shards for i in s.frames])
+        got = shard.to_frame_order(torch.from_numpy(gathered), shards, d_off, chunk_bytes=chunk)
+        assert np.array_equal(got.numpy(), full)

@@ -217,3 +217,42 @@ def test_block_route_auto_at_scale(gpu, zs):
     torch.cuda.synchronize()
     assert int((status != 0).sum()) == 0
     assert torch.equal(out, torch.from_numpy(data).to(gpu))
+
+
+_FIRST_CALL = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import libzseek_amd as z
+data = z.synth_buffer(64 << 20)
+img = z.lz4_seekable(data, 1 << 20)
+c_off, d_off = z.seek_table_of(img)
+b = z.frame_batch(c_off, d_off, 0, len(c_off) - 1)
+dev = torch.device("cuda", 0)
+desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
+comp = torch.zeros(b.comp_end + 256, dtype=torch.uint8, device=dev)
+comp[: b.comp_end].copy_(torch.from_numpy(img[: b.comp_end].copy()))
+out = torch.empty(b.out_bytes, dtype=torch.uint8, device=dev)
+status = torch.full((len(b.desc),), -1, dtype=torch.int32, device=dev)
+z.kernel_timing(True)
+z.decode_frames(desc, comp, out, status)      # this process's FIRST device-API call
+torch.cuda.synchronize()
+n, ms = z.kernel_times()
+z.kernel_timing(False)
+assert int((status != 0).sum()) == 0
+assert out.cpu().numpy().tobytes() == data.tobytes()
+print("STAGES", ms)
+assert ms["hand-off"] < 0.25 * ms["execute"], ms
+"""
+
+
+def test_device_api_first_call_big_frames(gpu):
+    """The device API's first call in a process on 1 MiB frames sizes its
+    item scratch from the compressed span, so no frame is handed to the
+    (6x slower) wave kernel: the hand-off stage stays an empty launch."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _FIRST_CALL, root], capture_output=True, text=True,
+                       timeout=110, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

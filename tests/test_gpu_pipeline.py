@@ -196,3 +196,47 @@ def test_parallel_pread_callbacks(gpu, zs, io):
     with zs.Reader(img, 0) as r:
         with pytest.raises(zs.ZseekError):
             r.set_io_threads(0)
+
+
+def test_concurrent_cache_hits_and_stats_during_read(gpu, zs, synth_img):
+    """The reference's reader concurrency (decompress.c:699-706, :850-875):
+    cache hits run under a shared lock, so several threads read one warm
+    frame at once; and zseek_reader_stats answers while a large GPU read on
+    the same reader is in flight."""
+    import threading
+    data, img = synth_img
+    with zs.Reader(img, 4) as r:
+        base = 5 * FRAME
+        assert r.pread(4096, base) == data[base: base + 4096].tobytes()   # warm
+        b0 = r.gpu_stats()["batches"]
+        errors = []
+
+        def hits(seed):
+            rng = np.random.default_rng(seed)
+            for _ in range(300):
+                o = base + int(rng.integers(0, FRAME - 512))
+                n = int(rng.integers(1, 513))
+                if r.pread(n, o) != data[o: o + n].tobytes():
+                    errors.append((o, n))
+
+        th = [threading.Thread(target=hits, args=(s,)) for s in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors
+        assert r.gpu_stats()["batches"] == b0          # every read a hit
+        assert r.stats()["cached_frames"] == 1
+    with zs.Reader(img, 0) as r:
+        r.set_batch_bytes(FRAME)                        # one frame per batch: a long read
+        out = {}
+        t = threading.Thread(target=lambda: out.setdefault("got", r.pread(len(data), 0)))
+        t.start()
+        during = 0
+        while t.is_alive():
+            st = r.stats()
+            assert st["frames"] == 129 and st["decompressed_size"] == len(data)
+            during += t.is_alive()
+        t.join()
+        assert out["got"] == data.tobytes()
+        assert during > 0   # stats calls returned while the read was in flight

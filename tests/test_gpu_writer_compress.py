@@ -112,3 +112,21 @@ def test_gpu_writer_mode_switch(gpu, zs):
         w.write(c)
     assert w.close() == host
     np.testing.assert_equal(len(host) > 0, True)
+
+
+def test_gpu_writer_failure_latches(gpu, zs):
+    """Deferred writes (zseek_hip.h): a queued frame's callback failure is
+    reported by the later zseek_write that flushed it, and every call after
+    it fails too -- the frames queued behind it are never written."""
+    data = bytes(zs.synth_buffer(1 << 20))
+    chunks = _writes(data, [65536])
+    w = zs.Writer(zs.ZSEEK_LZ4, 65536, fail_on_callback=2)
+    assert w.set_gpu_compress(2 * 65536)   # a flush every second frame
+    w.write(chunks[0])
+    with pytest.raises(zs.ZseekError):
+        w.write(chunks[1])                 # flushes frames 1-2; frame 2's callback fails
+    with pytest.raises(zs.ZseekError):
+        w.write(chunks[2])
+    with pytest.raises(zs.ZseekError):
+        w.close()
+    assert w.callbacks == 3                # frames 1, 2 (refused), then close's seek table
