@@ -48,9 +48,8 @@ constexpr uint32_t kStride = 560;        // bytes between lanes' areas
 // 4.02 ms per launch at config 2)
 constexpr uint32_t kFlush = 8;           // item lines written per flush (one store)
 // The fill keeps the ring within [ip, ip + kRing - 16) and moves in 32-byte
-// slots, so bytes up to ip + kRing - 47 always arrive: the fast step takes a
-// literal run only if its offset's 3 bytes lie within that reach
-constexpr uint32_t kLitFast = kRing - 47 - 5;
+// slots; a literal run whose offset lies past what has arrived is taken in
+// two halves (fast())
 constexpr uint32_t kOff = 0x80000000u;   // out-of-range buffer offset: op disabled
 
 enum : uint32_t { P_TOKEN = 0, P_LEXT, P_OFF, P_MEXT, P_BHDR, P_END, P_DONE };
@@ -82,10 +81,13 @@ struct Lane {
     uint32_t kf;                       // items [0, kf) written to HBM (a multiple of 16)
     // the sub-step's item store: slots k0, k0+1 (nk = 0: none)
     uint32_t ia, ibw, ia2, ib2, nk;
-    uint32_t cnt[6];   // DIAG 4: sub-steps fast / exact-needed / waiting / done / slow-run, sequences
+    uint32_t cnt[22];  // DIAG 4: sub-steps fast / exact-needed / waiting / done / slow-run, sequences,
+                       // then per exact-needed sub-step the failed rules (why bits) and the phase
+    uint32_t why;      // DIAG 4: the fast step's failed rules (bit per slack, see fast())
 };
 
-__device__ unsigned long long g_lean_stats[6];
+constexpr int kLeanStats = 22;
+__device__ unsigned long long g_lean_stats[kLeanStats];
 
 __device__ __forceinline__ uint32_t lds_u32(uint32_t a)
 {
@@ -246,22 +248,29 @@ __device__ __forceinline__ int32_t hdr_status(Lane &L)
     return -1;
 }
 
-// ---- fast step: one whole ordinary sequence ----------------------------------
+// ---- fast step: one whole ordinary sequence, or half of one -------------------
 // Every liblz4 rule that an ordinary sequence meets, as one min over signed
 // slacks (no short-circuit branches): the token and offset bytes are in the
-// ring, at most one extension byte each (lit <= 269, ml <= 273) and a
-// literal run the ring can span (lit <= kLitFast; longer: exact step), not the
+// ring, at most one extension byte each (lit <= 269, ml <= 273), not the
 // block's last sequence (input side: the offset and 8 more bytes lie inside
 // the block — which also covers the extension-byte bounds; output side:
 // op + lit <= oend - MFLIMIT), 1 <= off <= op + lit - floor, the match ends
-// by min(oend - LASTLITERALS, dSize), two item slots free.  Returns true when
-// the lane needs the exact step (a rule failed for a reason other than bytes
-// still in flight, or the lane is not at a token).
+// by min(oend - LASTLITERALS, dSize), two item slots free.
+// A sequence whose token passes its rules while its offset bytes are not in
+// the ring yet (a literal run longer than the ring reaches, or bytes still in
+// flight) takes its literal half now: the lane moves to the offset in phase
+// P_OFF (lit_done's state: lsrc, nlit, op past the literals) and the fill
+// restarts the stream there; the match half is then this same step in P_OFF
+// (w is the offset word, the token kept in L.tok).  Round 3 sent such
+// literals (~10 per 64 KiB frame at the frames' starts) to the exact step.
+// Returns true when the lane needs the exact step (a rule failed for a reason
+// other than bytes still in flight, or the lane is in another phase).
 // (fe: the flush-table entry read with the token; the line it names is read
 // with the offset, so the flush adds no LDS round trip of its own)
 __device__ __forceinline__ bool fast(Lane &L, uint32_t fe, uint32_t pc, u32x4 &fv)
 {
-    const uint32_t ip = L.ip;
+    const uint32_t ip = L.ip, ph = L.ph;
+    const bool po = ph == P_OFF;
     const uint32_t w = r4(L, ip);
     const uint32_t tok = w & 0xFF, e = (w >> 8) & 0xFF;
     const bool lext = (tok >> 4) == 15;
@@ -269,43 +278,56 @@ __device__ __forceinline__ bool fast(Lane &L, uint32_t fe, uint32_t pc, u32x4 &f
     const uint32_t p = ip + (lext ? 2 : 1);
     const uint32_t q = p + lit;
     fv = *lp<u32x4>(fe + 16 * pc);
-    const uint32_t o4 = r4(L, q);
+    const uint32_t o4q = r4(L, q);
+    const uint32_t qq = po ? ip : q;
+    const uint32_t o4 = po ? w : o4q;
+    const uint32_t mtok = po ? L.tok : tok;
     const uint32_t off = o4 & 0xFFFF, e2 = (o4 >> 16) & 0xFF;
-    const bool mext = (tok & 15) == 15;
-    const uint32_t ml = (mext ? 15 + e2 : tok & 15) + kMinMatch;
-    const uint32_t nip = q + (mext ? 3 : 2);
-    const uint32_t cop = L.op + lit;
-    const int32_t s_av = (int32_t)(L.avail - (L.cx0 + q + 3));
-    const int32_t s_in = (int32_t)(L.iend - q - 8);
-    // one extension byte at most (lit <= 269, ml <= 273), and token + offset
-    // within the ring's reach together (kLitFast)
-    const int32_t s_lx = (int32_t)(kLitFast - lit), s_mx = (int32_t)(273 - ml);
-    const int32_t s_mf = (int32_t)(L.oend - kMfLimit - cop);
+    const bool mext = (mtok & 15) == 15;
+    const uint32_t ml = (mext ? 15 + e2 : mtok & 15) + kMinMatch;
+    const uint32_t nip = qq + (mext ? 3 : 2);
+    const uint32_t lt = po ? L.nlit : lit, ls = po ? L.lsrc : p;
+    const uint32_t cop = po ? L.op : L.op + lit;
+    const int32_t s_av = (int32_t)(L.avail - (L.cx0 + qq + 3));
+    const int32_t s_in = (int32_t)(L.iend - qq - 8);
+    // one extension byte at most (lit <= 269, ml <= 273); the literal half's
+    // rules hold already in P_OFF
+    const int32_t s_lx = (!po & lext & (e == 255)) ? -1 : 0, s_mx = (int32_t)(273 - ml);
+    const int32_t s_mf = po ? 0 : (int32_t)(L.oend - kMfLimit - cop);
+    const int32_t s_dl = po ? 0 : (int32_t)(L.dlen - cop);
     const int32_t s_off = min((int32_t)(off - 1), (int32_t)(cop - L.floor_ - off));
     const int32_t s_end = (int32_t)(L.mlim - cop - ml);
     const int32_t s_cap = (int32_t)(min(L.cap, L.kf + 32) - L.k - 2);   // slots, and room in the buffer
-    const int32_t s_ph = -(int32_t)L.ph;
-    const int32_t s_t = min(s_in, min(s_lx, s_mf));   // the token's rules
+    const int32_t s_ph = ((ph == P_TOKEN) | po) ? 0 : -1;
+    const int32_t s_t = min(min(s_in, s_dl), min(s_lx, s_mf));   // the literal half's rules
     const int32_t slack = min(min(min(s_av, s_t), min(s_mx, s_off)), min(s_end, min(s_cap, s_ph)));
     const bool go = slack >= 0;
-    const bool big = (lit > 255) | (ml > 258);
-    L.ia = big ? p | kItemExt : p;
-    L.ibw = big ? off : off | (lit << 16) | ((ml - 3) << 24);
-    L.ia2 = lit;
+    const bool tok_av = (int32_t)(L.avail - (L.cx0 + ip + 2)) >= 0;
+    // the literal half alone: a token whose rules hold, offset bytes not in
+    const bool half = (ph == P_TOKEN) & tok_av & (s_t >= 0) & (s_av < 0);
+    L.why = (s_av < 0) | (s_in < 0) << 1 | (s_lx < 0) << 2 | (s_mf < 0) << 3 | (s_mx < 0) << 4 |
+            (s_off < 0) << 5 | (s_end < 0) << 6 | (s_cap < 0) << 7 | (!po & (ph != P_TOKEN)) << 8;
+    const bool big = (lt > 255) | (ml > 258);
+    L.ia = big ? ls | kItemExt : ls;
+    L.ibw = big ? off : off | (lt << 16) | ((ml - 3) << 24);
+    L.ia2 = lt;
     L.ib2 = ml;
     L.nk = go ? (big ? 2 : 1) : 0;
-    L.ip = go ? nip : ip;
-    L.op = go ? cop + ml : L.op;
+    L.ip = go ? nip : (half ? q : ip);
+    L.op = go ? cop + ml : (half ? cop : L.op);
+    L.lsrc = half ? p : L.lsrc;
+    L.nlit = half ? lit : L.nlit;
+    L.tok = half ? tok : L.tok;
+    L.ph = go ? (uint32_t)P_TOKEN : (half ? (uint32_t)P_OFF : ph);
     // waiting, not failing: the token bytes are not in yet (and exist), or
-    // the token is ordinary and only the offset bytes are not in yet
-    const bool tok_av = (int32_t)(L.avail - (L.cx0 + ip + 2)) >= 0;
-    const bool t_ok = s_t >= 0;
-    const bool full = L.k + 2 > L.kf + 32;   // the item buffer waits for a flush
-    const bool wait = (!tok_av & (ip + 2 <= L.clen)) | (tok_av & t_ok & (s_av < 0)) | full;
-    // the exact step's phases wait here too while their next bytes are in
-    // flight (4 from ip, or the frame's end), rather than run to find out
-    const bool x_wait = (L.ph != P_END) & ((int32_t)(L.avail - (L.cx0 + ip + 4)) < 0) & (ip + 4 <= L.clen);
-    return !go & (L.ph != P_DONE) & ((L.ph != P_TOKEN) ? !x_wait : !wait);
+    // the item buffer waits for a flush
+    const bool full = L.k + 2 > L.kf + 32;
+    const bool wait = (!tok_av & (ip + 2 <= L.clen)) | full;
+    // the exact step's phases (P_OFF included) wait here too while their
+    // next bytes are in flight (4 from ip, or the frame's end), rather than
+    // run to find out
+    const bool x_wait = (ph != P_END) & ((int32_t)(L.avail - (L.cx0 + ip + 4)) < 0) & (ip + 4 <= L.clen);
+    return !go & !half & (ph != P_DONE) & (((ph != P_TOKEN) | po) ? !x_wait & !(po & full) : !wait);
 }
 
 // ---- exact step: byte at a time, every rule (parse_block / parse_frame) ------
@@ -567,6 +589,11 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
         L.cnt[1] += need;
         L.cnt[2] += L.nk == 0 && !need && L.ph != P_DONE;
         L.cnt[3] += L.ph == P_DONE;
+        if (need) {
+            for (int b = 0; b < 9; b++)
+                L.cnt[6 + b] += (L.why >> b) & 1;
+            L.cnt[15 + min(L.ph, 6u)] += 1;
+        }
     }
     flush_store<DIAG>(L, fe, fv, g, pc, fcnt);
     if (SLOW && __builtin_expect(__ballot(need) != 0, 0)) {
@@ -691,8 +718,9 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     L.stop = 0xFFFFFFFFu;
     L.cap = cap;
     L.ia = L.ibw = L.ia2 = L.ib2 = L.nk = 0;
-    for (int i = 0; i < 6; i++)
+    for (int i = 0; i < kLeanStats; i++)
         L.cnt[i] = 0;
+    L.why = 0;
     if (!act || cspan >= 0x7FFFFF00ull || ispan >= 0x7FFFFF00ull || d.c_size > kItemPos ||
         rb0 + cap > capacity) {
         finish(L, ST_NOT_RUN);
@@ -773,7 +801,7 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     if ((DIAG & 4) && act) {
         L.cnt[5] = L.k;
-        for (int i = 0; i < 6; i++)
+        for (int i = 0; i < kLeanStats; i++)
             atomicAdd(&g_lean_stats[i], (unsigned long long)L.cnt[i]);
     }
     if (!act)
@@ -805,7 +833,7 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                        nullptr)
 #ifdef ZSK_TUNING
     if (diag & 4) {
-        unsigned long long z[6] = {0};
+        unsigned long long z[kLeanStats] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lean_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
         ZSK_LEAN(4, 2);
         (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_lean_stats), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
@@ -813,6 +841,10 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
         const double fr = nframes;
         fprintf(stderr, "lean parse per frame: sub-steps fast %.1f exact-needed %.1f waiting %.1f done %.1f "
                         "exact-step runs %.1f items %.1f\n", z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr);
+        fprintf(stderr, "  exact-needed rules per frame: av %.1f in %.1f lx %.1f mf %.1f mx %.1f off %.1f end %.1f cap %.1f "
+                        "phase %.1f; by phase TOKEN %.1f LEXT %.1f OFF %.1f MEXT %.1f BHDR %.1f END %.1f DONE %.1f\n",
+                z[6] / fr, z[7] / fr, z[8] / fr, z[9] / fr, z[10] / fr, z[11] / fr, z[12] / fr, z[13] / fr, z[14] / fr,
+                z[15] / fr, z[16] / fr, z[17] / fr, z[18] / fr, z[19] / fr, z[20] / fr, z[21] / fr);
     } else if (diag & 2)
         ZSK_LEAN(2, 2);
     else if (diag & 1)

@@ -227,6 +227,94 @@ __device__ __forceinline__ void copy_desc3(const Stage &S, const uint8_t *lbase,
     }
 }
 
+// Round 0 with the pieces split by size: a run of 16 bytes or more is covered
+// by whole 16-byte pieces only (its last piece overlaps the one before), so
+// only runs under 16 bytes need an exact-length stage write.  Whole pieces
+// (descriptors [0, TF)) are dealt as in copy_desc3 and written with one
+// 16-byte LDS store each, no length branches; the short ones (at most two per
+// lane, descriptors [TF, TF + TS)) follow in their own deal with the exact
+// write.  One DPP scan counts both (whole pieces in the low half-word).
+template <int DIAG>
+__device__ __forceinline__ void copy_desc4(const Stage &S, const uint8_t *lbase, const Span &lsp,
+                                           uint32_t llen, const uint8_t *obase, uint32_t descs,
+                                           uint32_t flushed, uint32_t lane, uint32_t src, uint32_t op,
+                                           uint32_t lit, uint32_t msrc, uint32_t mb, uint32_t mn)
+{
+    const bool ltail = lit != 0 && lit < 16 && src + 16 > llen;
+    if (__ballot(ltail)) {
+        if (ltail)
+            lds_put(saddr(S, op), bload16(lsp.r, lsp.s0 + src), lit);
+    }
+    const bool ls = lit != 0 && lit < 16 && !ltail, ms = mn != 0 && mn < 16;
+    const uint32_t lpn = lit < 16 ? 0 : npieces(lit), mpn = mn < 16 ? 0 : npieces(mn);
+    const uint32_t nf = lpn + mpn, ns = (uint32_t)ls + (uint32_t)ms;
+    const uint32_t inc = wave_incl_add(nf | ns << 16);
+    const uint32_t T = lane_val(inc, 63);
+    if (T == 0)
+        return;
+    const uint32_t TF = T & 0xFFFF, TS = T >> 16;
+    const uint32_t xf = (inc & 0xFFFF) - nf, xs = TF + (inc >> 16) - ns;
+    const uint64_t dl = ((uint64_t)((saddr(S, op) - S.base) | (lit < 16 ? lit : 16) << 16 | K_LIT << 24) << 32) | src;
+    const uint64_t dm = ((uint64_t)((saddr(S, mb) - S.base) | (mn < 16 ? mn : 16) << 16 | K_HBM << 24) << 32) | msrc;
+    const uint64_t kst = (uint64_t)(K_STAGE - K_HBM) << 56;
+    // the short pieces: one descriptor each
+    if (ls)
+        *lp<uint64_t>(descs + 8 * xs) = dl;
+    if (ms)
+        *lp<uint64_t>(descs + 8 * (xs + ls)) = msrc + 16 > flushed ? dm + kst : dm;
+    const uint32_t lm = lit < 16 ? 0 : lit - 16, mm = mn < 16 ? 0 : mn - 16;
+    const uint32_t al = descs + 8 * xf;
+    for (uint32_t i = 0; __ballot(i < lpn || i < mpn); i++) {
+        if (i < lpn) {
+            const uint32_t o = min(16 * i, lm);
+            *lp<uint64_t>(al + 8 * i) = dl + (uint64_t)o * 0x100000001ull;
+        }
+        if (i < mpn) {
+            const uint32_t o = min(16 * i, mm);
+            uint64_t D = dm + (uint64_t)o * 0x100000001ull;
+            if (msrc + o + 16 > flushed)
+                D += kst;
+            *lp<uint64_t>(al + 8 * (lpn + i)) = D;
+        }
+    }
+    wave_lds_sync();
+    // one deal over [0, TF + TS): four slots' loads in flight, then the
+    // writes -- a slot holding short pieces (at most the last two) writes
+    // exact lengths, every other slot plain 16-byte stores
+    const uint32_t TT = TF + TS;
+    for (uint32_t t0 = 0; t0 < TT; t0 += 256) {
+        u32x4 v[4];
+        uint32_t dw[4], sx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t t = t0 + 64 * j + lane;
+            const bool on = t < TT;
+            const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
+            sx[j] = on ? (uint32_t)D : 0;
+            dw[j] = on ? (uint32_t)(D >> 32) : 0;
+            const uint32_t kind = dw[j] >> 24;
+            const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);
+            v[j] = (DIAG & 1) ? (u32x4){0, 0, 0, 0} : *reinterpret_cast<const u32x4_l *>(p);
+            if (t0 + 64 * j + 64 >= TT)
+                break;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (dw[j]) {
+                u32x4 w = v[j];
+                if ((dw[j] >> 24) == K_STAGE)
+                    w = lds16(saddr(S, sx[j]));
+                if (t0 + 64 * j + 64 <= TF)
+                    *lp<u32x4_l>(S.base + (dw[j] & 0xFFFF)) = w;
+                else
+                    lds_put(S.base + (dw[j] & 0xFFFF), w, (dw[j] >> 16) & 0xFF);
+            }
+            if (t0 + 64 * j + 64 >= TT)
+                break;
+        }
+    }
+}
+
 // A ready match (mn bytes, msrc -> mb, no overlap) whose source lies in this
 // batch: lane-owned pieces, two per step, from the stage (the HBM path only
 // runs when some lane's piece lies below `flushed`).
@@ -301,6 +389,32 @@ template <int DIAG>
 __device__ __forceinline__ void flush_chunks4(const Stage &S, const Out &O, uint32_t fc, uint32_t end_c,
                                               uint32_t lane)
 {
+    // every chunk inside the frame (the usual batch: neither the frame's
+    // first chunk when the output is not 16-byte aligned, nor its partial
+    // last one): plain 16-byte stores through a resource based at chunk 0
+    if (!(DIAG & 64) && (fc > 0 || S.a0 == 0) && 16 * end_c <= O.dlen + S.a0) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(O.o - S.a0), 0, (int)((O.dlen + S.a0 + 15) & ~15u), kRsrcDw3);
+        for (uint32_t c0 = fc; c0 < end_c; c0 += 256) {
+            u32x4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t c = c0 + 64 * j + lane;
+                v[j] = *lp<u32x4>(c < end_c ? S.base + 16u * (c - S.cb) : S.base);
+                if (c0 + 64 * j + 64 >= end_c)
+                    break;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t c = c0 + 64 * j + lane;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[j]), r,
+                                                       c < end_c ? 16 * c : 0x80000000u, 0, 0);
+                if (c0 + 64 * j + 64 >= end_c)
+                    break;
+            }
+        }
+        return;
+    }
     for (uint32_t c0 = fc; c0 < end_c; c0 += 256) {
         u32x4 v[4];
 #pragma unroll
@@ -311,9 +425,7 @@ __device__ __forceinline__ void flush_chunks4(const Stage &S, const Out &O, uint
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t c = c0 + 64 * j + lane;
-            if ((DIAG & 64) && c < end_c && v[j].x == 0x9E3779B9u && v[j].y == c)
-                O.o[0] = 0;   // (never: keeps the stage reads live without the stores)
-            else if (!(DIAG & 64) && c < end_c)
+            if (c < end_c)
                 put_chunk(O, S.a0, c, v[j]);
         }
     }
@@ -374,7 +486,8 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 
 // DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores, 4 = no
 // dependency rounds, 8 = no round 0, 16 = section timers and counters
-// (g_xstats), 32 = no flush at all, 64 = flush stage reads without stores.
+// (g_xstats), 32 = no flush at all, 64 = round 3's flush (every chunk through
+// put_chunk), 128 = round 3's round 0 (copy_desc3).
 // Tried and dropped (same-box A/B, config 2): short runs'
 // partial pieces dealt after the full pieces; each batch's flush deferred past
 // the next batch's item decode; the rounds' readiness from an LDS bitmap; six
@@ -627,7 +740,10 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if (!(DIAG & 8))
+        if ((DIAG & 8) == 0 && (DIAG & 128) == 0)
+            copy_desc4<DIAG>(S, lbase, lsp, llen, O.o, descs, flushed, lane, src, op, lit_n, msrc, mb,
+                             early ? ml : 0);
+        else if ((DIAG & 8) == 0)
             copy_desc3<DIAG>(S, lbase, lsp, llen, O.o, descs, flushed, lane, src, op, lit_n, msrc, mb,
                              early ? ml : 0);
         wave_lds_sync();   // stage bytes of other lanes from here on
@@ -751,6 +867,8 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x108: ZSK_X(8); break;
     case 0x122: ZSK_X(34); break;
     case 0x140: ZSK_X(64); break;
+    case 0x180: ZSK_X(128); break;
+    case 0x1C0: ZSK_X(192); break;
     case 0x110: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
