@@ -487,7 +487,13 @@ __device__ __forceinline__ void hbm_match(const Out &O, uint32_t dst, uint32_t o
 // DIAG (tuning builds only): 1 = no piece loads, 2 = no flush stores, 4 = no
 // dependency rounds, 8 = no round 0, 16 = section timers and counters
 // (g_xstats), 32 = no flush at all, 64 = round 3's flush (every chunk through
-// put_chunk), 128 = round 3's round 0 (copy_desc3).
+// put_chunk), 128 = round 3's round 0 (copy_desc3); inside the dependency
+// rounds: 256 = no copy_round, 512 = no copy_overlap, 1024 = no readiness
+// search (every pending match ready at once).  Tried and dropped in round 4:
+// the pending matches one at a time in destination order over the whole wave
+// (no readiness search; execute 4.23 vs 2.79 ms -- each match a serial LDS
+// read-then-write), and round 0 / the rounds dealt from one table entry per
+// run with a DPP max-scan (3.86 vs 2.71 ms: two dependent LDS reads per slot).
 // Tried and dropped (same-box A/B, config 2): short runs'
 // partial pieces dealt after the full pieces; each batch's flush deferred past
 // the next batch's item decode; the rounds' readiness from an LDS bitmap; six
@@ -769,7 +775,7 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
                 *lp<uint64_t>(descs + 8 * below) = ((uint64_t)me << 32) | mb;
             wave_lds_sync();
             uint32_t lo = 0, hi = mine ? below : 0;
-            while (__ballot(lo < hi)) {
+            while (!(DIAG & 1024) && __ballot(lo < hi)) {
                 const uint32_t mid = (lo + hi) >> 1;
                 const uint32_t mem = lo < hi ? (uint32_t)(*lp<uint64_t>(descs + 8 * mid) >> 32) : 0;
                 if (lo < hi) {
@@ -782,9 +788,10 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
             const uint32_t mbl = (uint32_t)*lp<uint64_t>(descs + 8 * (mine && lo < below ? lo : 0));
             const bool ready = mine && !(lo < below && mbl < need);
             wave_lds_sync();
-            if (ready && overlap)
+            if (!(DIAG & 512) && ready && overlap)
                 copy_overlap(S, O, flushed, mb, off, ml);
-            copy_round(S, O, flushed, msrc, mb, ready && !overlap ? ml : 0);
+            if (!(DIAG & 256))
+                copy_round(S, O, flushed, msrc, mb, ready && !overlap ? ml : 0);
             pending &= ~__ballot(ready);
             wave_lds_sync();
             if (DIAG & 16)
@@ -869,6 +876,10 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x140: ZSK_X(64); break;
     case 0x180: ZSK_X(128); break;
     case 0x1C0: ZSK_X(192); break;
+    case 0x301: ZSK_X(256); break;    // rounds without copy_round
+    case 0x302: ZSK_X(512); break;    // rounds without copy_overlap
+    case 0x304: ZSK_X(1024); break;   // rounds without the readiness search
+    case 0x307: ZSK_X(1792); break;   // rounds: compaction and ballots only
     case 0x110: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);

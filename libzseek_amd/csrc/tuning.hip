@@ -40,6 +40,8 @@ int staged(int stages, int route, int tune, const FrameDesc *d_desc, uint32_t nf
 //   20         execute only, over the items the previous launch left
 //   0x1xx      execute diagnostic DIAG = xx alone (seq_exec.hip; 0x110 prints
 //              section timers)
+//   0x3xx      execute diagnostic version 0x3xx alone (seq_exec.hip: parts of
+//              the dependency rounds removed)
 //   0x2xx      plan + lean parse with diagnostic bits xx (lz4_lean.hip;
 //              0x204 prints sub-step counters)
 int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
@@ -59,6 +61,8 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
     if ((variant & 0xF00) == 0x100)
         return staged(4, ROUTE_AUTO, (variant & 0x1FF) << 8, d_desc, nframes, d_comp, d_out, d_status,
                       stream);
+    if ((variant & 0xF00) == 0x300)   // execute diagnostics DIAG >= 256 (seq_exec.hip)
+        return staged(4, ROUTE_AUTO, (variant & 0x3FF) << 8, d_desc, nframes, d_comp, d_out, d_status, stream);
     if ((variant & 0xF00) == 0x200)
         return staged(3, ROUTE_LEAN, variant & 0xFF, d_desc, nframes, d_comp, d_out, d_status, stream);
     return -1;
