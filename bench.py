@@ -526,13 +526,13 @@ def main():
 
 def main_compress(args, torch, dist, z, dev, world, rank):
     """--codec lz4c: every rank compresses its own --size bytes of the §8d
-    synthetic into --frame (<= 64 KiB) LZ4 frames on its GPU, input resident
+    synthetic into --frame (<= 4 MiB; linked blocks above 64 KiB) LZ4 frames on its GPU, input resident
     in HBM (weak scaling).  One step = one zsk_lz4_compress_frames launch over
     every frame (memset of the position tables, lz4_compress_kernel,
     lz4_store_kernel).  Output: byte-identical to liblz4's frames (checked
     against the writer-identical seekable image after the timed region)."""
-    if args.frame > 65536:
-        raise SystemExit("--codec lz4c: frames of at most 64 KiB")
+    if args.frame > 1 << 22:
+        raise SystemExit("--codec lz4c: frames of at most 4 MiB (ZSK_LZ4_COMPRESS_MAX_FRAME)")
     t0 = time.time()
     size = args.size - args.size % args.frame
     data = z.synth_buffer(size, args.threads)

@@ -24,7 +24,7 @@
  *                            per-frame LZ4F_compressFrame call
  *                            (compress.c:750 direct frames, :483 buffered
  *                            ones; prefs compress.c:203-207), batched over
- *                            frames of <= 64 KiB in one grid.
+ *                            frames of <= 4 MiB in one grid.
  */
 #ifndef ZSEEK_HIP_H
 #define ZSEEK_HIP_H
@@ -225,7 +225,8 @@ ZSEEK_EXPORT int zsk_reader_devices(zseek_reader_t *reader, int *devices,
  * LZ4 frame compression, byte-identical to the reference
  * writer's frames: LZ4F_compressFrame(level, autoFlush = 1, 64 KiB blocks) of
  * liblz4 1.9.3, as compress.c:737-786 / :463-518 call it.  One frame per
- * descriptor, src_size <= 65536 (one block; larger frames are refused with
+ * descriptor, src_size <= ZSK_LZ4_COMPRESS_MAX_FRAME (one independent block
+ * up to 64 KiB, linked 64 KiB blocks above; larger frames are refused with
  * c_size 0).  ZSK_COMPRESS_CONTENT_SIZE = the writer's contentSize != 0 case
  * (a buffered frame flushed by end_frame_lz4, compress.c:472): the header
  * then carries the frame's size.
@@ -234,11 +235,13 @@ typedef struct {
     uint64_t src_off;   /* frame input start in d_src                        */
     uint64_t dst_off;   /* output slot start in d_dst: 16-byte aligned, at    */
                         /* least ZSK_LZ4_COMPRESS_BOUND(src_size) bytes       */
-    uint32_t src_size;  /* <= 65536                                           */
+    uint32_t src_size;  /* <= ZSK_LZ4_COMPRESS_MAX_FRAME                      */
     uint32_t flags;     /* ZSK_COMPRESS_CONTENT_SIZE                          */
 } zsk_compress_desc_t;
 #define ZSK_COMPRESS_CONTENT_SIZE 1u
-#define ZSK_LZ4_COMPRESS_BOUND(n) ((((uint64_t)(n)) + 24 + 15) & ~(uint64_t)15)
+#define ZSK_LZ4_COMPRESS_MAX_FRAME (1u << 22)
+#define ZSK_LZ4_COMPRESS_BOUND(n) \
+    ((((uint64_t)(n)) + 4 * (((uint64_t)(n)) >> 16) + 24 + 15) & ~(uint64_t)15)
 
 /* Device scratch bytes zsk_lz4_compress_frames needs for @nframes frames
  * (a 64 KiB table of position + input-word entries per frame); size scratch
@@ -259,12 +262,12 @@ ZSEEK_EXPORT int zsk_lz4_compress_frames(const zsk_compress_desc_t *d_desc,
     int level, void *d_scratch, void *stream);
 
 /*
- * Writer GPU mode: an LZ4 writer's frames of <= 64 KiB are compressed on the
+ * Writer GPU mode: an LZ4 writer's frames of <= 4 MiB are compressed on the
  * GPU (zsk_lz4_compress_frames, on the calling thread's current device) in
  * batches of @batch_bytes input bytes (0: 1 GiB; (size_t)-1: GPU mode off,
  * after writing what is queued).  The file is byte-identical to host
  * compression.  Frames are written and logged when their batch is compressed:
- * when it fills, when a frame the GPU does not take (> 64 KiB) arrives, at
+ * when it fills, when a frame the GPU does not take (> 4 MiB) arrives, at
  * zseek_writer_stats and at zseek_writer_close; each write callback gets the
  * call_data of the zseek_write that produced the frame.  Deferred writes:
  * zseek_write returns true once its frame is QUEUED, so a compression or

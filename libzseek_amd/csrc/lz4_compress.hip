@@ -26,6 +26,23 @@
 // counts they would see.  Frames that do not fit are flagged and their raw
 // block written by a second, wave-per-frame kernel (coalesced copy).
 //
+// Frames above 64 KiB (the reference example's 1 MiB frames, test/example.c)
+// are linked: LZ4F_compressFrame then runs LZ4_compress_fast_continue over
+// 64 KiB blocks on one stream.  The stream differs from the one-block state:
+// a 2^12-entry table of 32-bit positions counted from the frame start, the
+// 5-byte hash of an 8-byte read ((read64 << 24) * 889523592379 >> 52, the
+// 64-bit build's byU32 hash), candidates more than 65535 back skipped without
+// a compare, backward extension down to the frame start, match lengths
+// stopping 5 bytes before the block end, and a stored block (capacity n - 1
+// exceeded) still advancing the stream.  One lane walks the frame's blocks in
+// order; a stored block rewinds the lane's packer and is copied inline.
+//
+// Lanes per wave: the parse is a serial chain of dependent table and input
+// loads, so the launch spreads frames over about 2048 waves (2 per SIMD:
+// fewer frames per wave, more independent chains) instead of filling every
+// wave's 64 lanes; a batch of 1 MiB frames is 16 times fewer chains than
+// the same bytes in 64 KiB frames.
+//
 // Algorithmic bytes per frame: n read + the frame's compressed size written.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,14 +56,18 @@ namespace zsk {
 namespace {
 
 typedef uint32_t u32_ua __attribute__((aligned(1)));
+typedef uint64_t u64_ua __attribute__((aligned(1)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_ua __attribute__((aligned(1)));
 
 constexpr uint32_t kHashLog = 13;
 constexpr uint32_t kTable = 1u << kHashLog;   // u16 entries per frame
-constexpr uint32_t kMaxFrame = 65536;
+constexpr uint32_t kMaxFrame = 65536;          // one block, independent
+constexpr uint32_t kMaxLinkedFrame = 1u << 22;  // linked frames: ZSK_LZ4_COMPRESS_MAX_FRAME
+constexpr uint32_t kLinkedHashLog = 12;
 constexpr uint32_t kStoredFlag = 0x80000000u;
 constexpr bool kDefaultVal = true;   // position + word entries: 103.7 ms against 125.8 (u16, 4 GiB)
+constexpr uint32_t kDefaultWaves = 2048;   // 2 per SIMD (see "Lanes per wave")
 constexpr int kDefaultProbe = 8;   // 8 / 16 / 32 measured 125.7 / 134.0 / 169.8 ms (4 GiB)
 
 __device__ __forceinline__ uint32_t rd32(const uint8_t *p)
@@ -54,9 +75,35 @@ __device__ __forceinline__ uint32_t rd32(const uint8_t *p)
     return *reinterpret_cast<const u32_ua *>(p);
 }
 
+__device__ __forceinline__ uint64_t rd64(const uint8_t *p)
+{
+    return *reinterpret_cast<const u64_ua *>(p);
+}
+
 __device__ __forceinline__ uint32_t hash4(uint32_t v)
 {
     return (v * 2654435761u) >> (32 - kHashLog);
+}
+
+// liblz4's byU32 hash on a 64-bit build: the low 5 bytes of an 8-byte read
+__device__ __forceinline__ uint32_t hash5(uint64_t v)
+{
+    return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - kLinkedHashLog));
+}
+
+// Input word at p and the table index of the sequence starting there.
+template <bool kLinked>
+__device__ __forceinline__ uint32_t word_hash(const uint8_t *p, uint32_t &h)
+{
+    if constexpr (kLinked) {
+        const uint64_t v = rd64(p);
+        h = hash5(v);
+        return (uint32_t)v;
+    } else {
+        const uint32_t v = rd32(p);
+        h = hash4(v);
+        return v;
+    }
 }
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r)
@@ -215,26 +262,33 @@ __device__ __forceinline__ uint32_t count_eq(const uint8_t *s, uint32_t a, uint3
 // liblz4's LZ4_compress_generic (byU16, noDict, limitedOutput, capacity n-1)
 // on s[0..n); writes the block payload through o and returns its size, or
 // 0 when it does not fit (the frame's block is then stored raw).
+// kLinked: one block s[b0, b0 + n) of a linked frame starting at s, on the
+// frame's stream table (byU32, positions from s, 65535 distance limit).
 // Table layouts: kVal = false is liblz4's (u16 positions; a candidate's word
 // is loaded from the input); kVal = true keeps each entry's input word beside
 // its position (u64: word << 32 | position + 1; 0 = liblz4's zeroed entry,
 // position 0), so a probe compares without loading the candidate's word.
-template <uint32_t kProbe, bool kVal>   // search probes per batch, table layout
-__device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, void *__restrict__ table,
-                                   Packer &o, uint32_t accel)
+template <uint32_t kProbe, bool kVal, bool kLinked = false>   // probes per batch, table layout
+__device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t b0, uint32_t n,
+                                   void *__restrict__ table, Packer &o, uint32_t accel)
 {
+    static_assert(kVal || !kLinked, "linked frames use the position + word table");
     uint16_t *__restrict__ T = static_cast<uint16_t *>(table);
     uint64_t *__restrict__ V = static_cast<uint64_t *>(table);
     const uint32_t cap = n - 1;
-    uint32_t op = 0, anchor = 0;
+    uint32_t op = 0, anchor = b0;
     if (n >= 13) {
-        const uint32_t mflimit1 = n - 11, matchlimit = n - 5;
-        const uint32_t first4 = rd32(s);
-        if constexpr (kVal)
-            V[hash4(first4)] = (uint64_t)first4 << 32 | 1u;
-        else
-            T[hash4(first4)] = 0;
-        uint32_t ip = 1;
+        const uint32_t mflimit1 = b0 + n - 11, matchlimit = b0 + n - 5;
+        const uint32_t first4 = rd32(s);   // word at position 0: what a zeroed entry points to
+        {
+            uint32_t h0;
+            const uint32_t w = word_hash<kLinked>(s + b0, h0);
+            if constexpr (kVal)
+                V[h0] = (uint64_t)w << 32 | (b0 + 1);
+            else
+                T[h0] = 0;
+        }
+        uint32_t ip = b0 + 1;
         for (;;) {
             uint32_t m;
             {
@@ -257,21 +311,18 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, vo
                     }
 #pragma unroll
                     for (uint32_t k = 0; k < kProbe; k++)
-                        in[k] = rd32(s + min(pk[k], mflimit1));
+                        in[k] = word_hash<kLinked>(s + min(pk[k], mflimit1), hk[k]);
                     if constexpr (kVal) {
 #pragma unroll
                         for (uint32_t k = 0; k < kProbe; k++) {
-                            hk[k] = hash4(in[k]);
                             const uint64_t e = V[hk[k]];
                             ck[k] = e ? (uint32_t)e - 1 : 0;
                             cw[k] = e ? (uint32_t)(e >> 32) : first4;
                         }
                     } else {
 #pragma unroll
-                        for (uint32_t k = 0; k < kProbe; k++) {
-                            hk[k] = hash4(in[k]);
+                        for (uint32_t k = 0; k < kProbe; k++)
                             ck[k] = T[hk[k]];
-                        }
                     }
 #pragma unroll
                     for (uint32_t k = 1; k < kProbe; k++)
@@ -288,8 +339,8 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, vo
                     }
                     uint32_t hit = kProbe;
 #pragma unroll
-                    for (uint32_t k = kProbe; k-- > 0;)
-                        hit = (k < nvalid && cw[k] == in[k]) ? k : hit;
+                    for (uint32_t k = kProbe; k-- > 0;)   // linked: a candidate > 65535 back is not compared
+                        hit = (k < nvalid && cw[k] == in[k] && (!kLinked || ck[k] + 65535 >= pk[k])) ? k : hit;
 #pragma unroll
                     for (uint32_t k = 0; k < kProbe; k++)   // the probes that ran, in order
                         if (k < nvalid && k <= hit) {
@@ -340,22 +391,22 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, vo
                 anchor = ip;
                 if (ip >= mflimit1)
                     goto last_literals;
-                const uint32_t w2 = rd32(s + ip - 2), w0 = rd32(s + ip);
-                const uint32_t h = hash4(w0);
+                uint32_t h2, h;
+                const uint32_t w2 = word_hash<kLinked>(s + ip - 2, h2), w0 = word_hash<kLinked>(s + ip, h);
                 uint32_t cand, cval;
                 if constexpr (kVal) {
-                    V[hash4(w2)] = (uint64_t)w2 << 32 | (ip - 1);
+                    V[h2] = (uint64_t)w2 << 32 | (ip - 1);
                     const uint64_t e = V[h];
                     cand = e ? (uint32_t)e - 1 : 0;
                     cval = e ? (uint32_t)(e >> 32) : first4;
                     V[h] = (uint64_t)w0 << 32 | (ip + 1);
                 } else {
-                    T[hash4(w2)] = (uint16_t)(ip - 2);
+                    T[h2] = (uint16_t)(ip - 2);
                     cand = T[h];
                     T[h] = (uint16_t)ip;
                     cval = rd32(s + cand);
                 }
-                if (cval != w0)
+                if (cval != w0 || (kLinked && cand + 65535 < ip))
                     break;
                 m = cand;   // immediate match: no literals, no literal check
                 lit = 0;
@@ -365,7 +416,7 @@ __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t n, vo
     }
 last_literals:
     {
-        const uint32_t run = n - anchor;
+        const uint32_t run = b0 + n - anchor;
         if (op + run + 1 + (run + 240) / 255 > cap)
             return 0;
         o.put((run >= 15 ? 15u : run) << 4);
@@ -377,31 +428,65 @@ last_literals:
     return op;
 }
 
+// The linked blocks of one frame of n > 64 KiB after its header; returns the
+// bytes written after the header (block words + blocks).
+__device__ uint32_t compress_linked(const uint8_t *__restrict__ s, uint32_t n, uint64_t *__restrict__ table,
+                                    uint8_t *__restrict__ out, uint32_t hlen, Packer &o, uint32_t accel)
+{
+    uint32_t at = hlen;
+    for (uint32_t b0 = 0; b0 < n; b0 += kMaxFrame) {
+        const uint32_t m = min(n - b0, kMaxFrame);
+        const Packer save = o;
+        o.put4(0);   // block word, patched below
+        uint32_t c = compress_block<8, true, true>(s, b0, m, table, o, accel);
+        if (c == 0) {   // did not fit: raw, the stream already advanced
+            o = save;
+            o.put4(m | kStoredFlag);
+            o.copy(s + b0, m);
+            c = m;
+        } else {
+            // the word's bytes: in memory if the packer flushed them, else in acc
+            const uint32_t flushed = 4u * (uint32_t)(o.w - reinterpret_cast<uint32_t *>(out));
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t p = at + i, v = (c >> (8 * i)) & 0xFF;
+                if (p < flushed)
+                    out[p] = (uint8_t)v;
+                else
+                    o.acc |= v << (8 * (p - flushed));
+            }
+        }
+        at += 4 + c;
+    }
+    return at - hlen;
+}
+
 template <uint32_t kProbe, bool kVal>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_desc_t *__restrict__ desc,
                                                           uint32_t nframes, const uint8_t *__restrict__ src,
                                                           uint8_t *__restrict__ dst,
                                                           uint32_t *__restrict__ csize,
                                                           uint8_t *__restrict__ tables,
-                                                          uint32_t *__restrict__ stored, uint32_t accel)
+                                                          uint32_t *__restrict__ stored, uint32_t accel,
+                                                          uint32_t per_wave)
 {
-    const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-    if (f >= nframes)
+    const uint32_t f = blockIdx.x * per_wave + threadIdx.x;
+    if (threadIdx.x >= per_wave || f >= nframes)
         return;
     const zsk_compress_desc_t d = desc[f];
     stored[f] = 0;
-    if (d.src_size > kMaxFrame || (d.dst_off & 15)) {
+    if (d.src_size > kMaxLinkedFrame || (d.dst_off & 15)) {
         csize[f] = 0;
         return;
     }
     const uint32_t n = d.src_size;
+    const bool linked = n > kMaxFrame;
     const bool with_size = (d.flags & ZSK_COMPRESS_CONTENT_SIZE) && n > 0;
     uint8_t hdr[15];
     hdr[0] = 0x04;
     hdr[1] = 0x22;
     hdr[2] = 0x4D;
     hdr[3] = 0x18;
-    hdr[4] = with_size ? 0x68 : 0x60;
+    hdr[4] = (linked ? 0x40 : 0x60) | (with_size ? 0x08 : 0);
     hdr[5] = 0x40;
     uint32_t hlen = 6;
     if (with_size) {
@@ -423,10 +508,22 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_des
         csize[f] = hlen + 4;
         return;
     }
+    uint8_t *const table = tables + (size_t)f * kTable * (kVal ? 8 : 2);
+    if (linked) {
+        if constexpr (kVal) {
+            const uint32_t body = compress_linked(src + d.src_off, n, reinterpret_cast<uint64_t *>(table), out,
+                                                  hlen, o, accel);
+            o.put4(0);   // end mark
+            o.flush();
+            csize[f] = hlen + body + 4;
+        } else {
+            csize[f] = 0;   // (tuning layout only: linked frames need the word table)
+        }
+        return;
+    }
     for (int i = 0; i < 4; i++)   // block word, patched below
         o.put(0);
-    const uint32_t c = compress_block<kProbe, kVal>(src + d.src_off, n,
-                                                    tables + (size_t)f * kTable * (kVal ? 8 : 2), o, accel);
+    const uint32_t c = compress_block<kProbe, kVal>(src + d.src_off, 0, n, table, o, accel);
     if (c == 0) {
         // the header stays; block word, raw block and end mark come from
         // lz4_store_kernel
@@ -499,8 +596,15 @@ int launch_lz4_compress(const zsk_compress_desc_t *d_desc, uint32_t nframes, con
                     : probe == 16 ? lz4_compress_kernel<16, false>
                     : probe == 32 ? lz4_compress_kernel<32, false>
                                   : lz4_compress_kernel<8, false>;
-    hipLaunchKernelGGL(kern, dim3((nframes + 63) / 64), dim3(64), 0, stream, d_desc, nframes, d_src, d_dst,
-                       d_csize, tables, stored, accel);
+    // frames per wave: about kWaves waves (env ZSEEK_LZ4C_WAVES, tuning only)
+    static const uint32_t waves = [] {
+        const char *e = getenv("ZSEEK_LZ4C_WAVES");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? (uint32_t)v : kDefaultWaves;
+    }();
+    const uint32_t per_wave = min(64u, max(1u, (nframes + waves - 1) / waves));
+    hipLaunchKernelGGL(kern, dim3((nframes + per_wave - 1) / per_wave), dim3(64), 0, stream, d_desc, nframes,
+                       d_src, d_dst, d_csize, tables, stored, accel, per_wave);
     hipLaunchKernelGGL(lz4_store_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes, d_src,
                        d_dst, stored);
     return hipGetLastError() == hipSuccess ? 0 : -1;

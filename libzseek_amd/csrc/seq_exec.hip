@@ -264,17 +264,43 @@ __device__ __forceinline__ void copy_desc4(const Stage &S, const uint8_t *lbase,
         *lp<uint64_t>(descs + 8 * (xs + ls)) = msrc + 16 > flushed ? dm + kst : dm;
     const uint32_t lm = lit < 16 ? 0 : lit - 16, mm = mn < 16 ? 0 : mn - 16;
     const uint32_t al = descs + 8 * xf;
-    for (uint32_t i = 0; __ballot(i < lpn || i < mpn); i++) {
-        if (i < lpn) {
-            const uint32_t o = min(16 * i, lm);
-            *lp<uint64_t>(al + 8 * i) = dl + (uint64_t)o * 0x100000001ull;
+    if (DIAG & 4096) {
+        // two pieces of each run per step (one 16-byte descriptor store)
+        for (uint32_t i = 0; __ballot(i < lpn || i < mpn); i += 2) {
+            if (i < lpn) {
+                const uint32_t o0 = min(16 * i, lm), o1 = min(16 * i + 16, lm);
+                const uint64_t d0 = dl + (uint64_t)o0 * 0x100000001ull, d1 = dl + (uint64_t)o1 * 0x100000001ull;
+                if (i + 1 < lpn)
+                    *lp<u32x4_l>(al + 8 * i) = (u32x4){(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1,
+                                                       (uint32_t)(d1 >> 32)};
+                else
+                    *lp<uint64_t>(al + 8 * i) = d0;
+            }
+            if (i < mpn) {
+                const uint32_t o0 = min(16 * i, mm), o1 = min(16 * i + 16, mm);
+                uint64_t d0 = dm + (uint64_t)o0 * 0x100000001ull, d1 = dm + (uint64_t)o1 * 0x100000001ull;
+                d0 += msrc + o0 + 16 > flushed ? kst : 0;
+                d1 += msrc + o1 + 16 > flushed ? kst : 0;
+                if (i + 1 < mpn)
+                    *lp<u32x4_l>(al + 8 * (lpn + i)) = (u32x4){(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1,
+                                                               (uint32_t)(d1 >> 32)};
+                else
+                    *lp<uint64_t>(al + 8 * (lpn + i)) = d0;
+            }
         }
-        if (i < mpn) {
-            const uint32_t o = min(16 * i, mm);
-            uint64_t D = dm + (uint64_t)o * 0x100000001ull;
-            if (msrc + o + 16 > flushed)
-                D += kst;
-            *lp<uint64_t>(al + 8 * (lpn + i)) = D;
+    } else {
+        for (uint32_t i = 0; __ballot(i < lpn || i < mpn); i++) {
+            if (i < lpn) {
+                const uint32_t o = min(16 * i, lm);
+                *lp<uint64_t>(al + 8 * i) = dl + (uint64_t)o * 0x100000001ull;
+            }
+            if (i < mpn) {
+                const uint32_t o = min(16 * i, mm);
+                uint64_t D = dm + (uint64_t)o * 0x100000001ull;
+                if (msrc + o + 16 > flushed)
+                    D += kst;
+                *lp<uint64_t>(al + 8 * (lpn + i)) = D;
+            }
         }
     }
     wave_lds_sync();
@@ -342,29 +368,40 @@ __device__ __forceinline__ void copy_round(const Stage &S, const Out &O, uint32_
     }
 }
 
-// Overlapping match (off < n), this lane alone: out[x] = out[x - off], 16
-// bytes at a time from distance eoff >= 16 (a multiple of off).
-__device__ __forceinline__ void copy_overlap(const Stage &S, const Out &O, uint32_t flushed,
-                                             uint32_t dst, uint32_t off, uint32_t n)
+// Overlapping match (off < n) over the whole wave (uniform arguments; round
+// 3's copy_overlap ran it on its own lane: 26 % of the execute's VALU at
+// config 2 for 0.18 such matches per batch): out[mb + j] = out[mb + j - off]
+// in phases of e bytes, phase p copying [p e, (p + 1) e) from the e bytes
+// before it in 16-byte pieces, one per lane.  e = off when off >= 16 (the
+// first phase reads the final bytes before mb); for off < 16, phase 0 writes
+// the first e = off * ceil(16 / off) (16..30) bytes one byte per lane from
+// the pattern out[mb - off, mb), which lies in the stage (mb - off > bstart -
+// 16 >= flushed - 16, the stage's kept chunk).
+__device__ __forceinline__ void copy_overlap_wave(const Stage &S, const Out &O, uint32_t flushed,
+                                                  uint32_t mb, uint32_t off, uint32_t n, uint32_t lane)
 {
-    uint32_t k = 0, eoff = off;
+    uint32_t e = off, done = 0;
     if (off < 16) {
-        const u32x4 pat = src16(S, O, flushed, dst - off, true);
-        uint32_t w[4] = {0, 0, 0, 0};
-        uint32_t m = 0;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            w[i >> 2] |= vbyte(pat, m) << (8 * (i & 3));
-            m = m + 1 == off ? 0 : m + 1;
+        e = off * ((16 + off - 1) / off);
+        done = e < n ? e : n;
+        if (lane < done) {
+            const uint32_t q = (lane * ((1024 + off - 1) / off)) >> 10;   // lane / off (lane < 32, off < 16)
+            *lp<uint8_t>(saddr(S, mb + lane)) = *lp<uint8_t>(saddr(S, mb - off + (lane - q * off)));
         }
-        lds_put(saddr(S, dst), (u32x4){w[0], w[1], w[2], w[3]}, n < 16 ? n : 16);
-        k = 16;
-        eoff = off * ((16 + off - 1) / off);
+        wave_lds_sync();
     }
-    for (; k < n; k += 16) {
-        const u32x4 v = src16(S, O, flushed, dst + k - eoff, true);
-        const uint32_t r = n - k;
-        lds_put(saddr(S, dst + k), v, r < 16 ? r : 16);
+    while (done < n) {
+        const uint32_t len = n - done < e ? n - done : e;
+        const uint32_t np = npieces(len);
+        for (uint32_t k0 = 0; k0 < np; k0 += 64) {
+            const bool on = k0 + lane < np;
+            const uint32_t o = piece_off(len, k0 + lane);
+            const u32x4 v = src16(S, O, flushed, mb + done - e + o, on);
+            if (on)
+                lds_put(saddr(S, mb + done + o), v, len < 16 ? len : 16);
+        }
+        done += len;
+        wave_lds_sync();
     }
 }
 
@@ -592,8 +629,13 @@ struct JobMap<true> {
 // slots with a uniform job cursor, so batches run across jobs unchanged.
 // (SEG runs at 4 waves per SIMD: its batches have <= 32,767 frames -- config
 // 3's 4,096 fill 4 per SIMD -- and the job cursor's registers fit no spill)
+// The LZ4 route's stage: 3,584 bytes -> 25.9 KB of LDS per 4-wave group,
+// six waves per SIMD (78 VGPRs fit 6); a batch of config 2 averages 2.7 KB,
+// so the smaller stage rarely cuts one, and the sixth wave hides latency.
+constexpr uint32_t kExecStage = 3584;
+
 template <int DIAG, uint32_t OUTB, bool SEG>
-__global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 4 : 5))) void seq_exec_kernel(
+__global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 4 : (OUTB <= 3584 ? 6 : 5)))) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
@@ -788,8 +830,12 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
             const uint32_t mbl = (uint32_t)*lp<uint64_t>(descs + 8 * (mine && lo < below ? lo : 0));
             const bool ready = mine && !(lo < below && mbl < need);
             wave_lds_sync();
-            if (!(DIAG & 512) && ready && overlap)
-                copy_overlap(S, O, flushed, mb, off, ml);
+            if (!(DIAG & 512)) {
+                for (uint64_t ov = __ballot(ready && overlap); ov; ov &= ov - 1) {
+                    const int i = (int)__builtin_ctzll(ov);
+                    copy_overlap_wave(S, O, flushed, lane_val(mb, i), lane_val(off, i), lane_val(ml, i), lane);
+                }
+            }
             if (!(DIAG & 256))
                 copy_round(S, O, flushed, msrc, mb, ready && !overlap ? ml : 0);
             pending &= ~__ballot(ready);
@@ -864,8 +910,8 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     if (blk)   // the block route (production kernel only)
         return launch_seq_exec_seg(d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status, stream, blk);
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
-#define ZSK_X(D)                                                                                          \
-    hipLaunchKernelGGL((seq_exec_kernel<D, 4096, false>), grid, block, 0, stream, d_desc, nframes, d_comp, \
+#define ZSK_X(D)                                                                                               \
+    hipLaunchKernelGGL((seq_exec_kernel<D, kExecStage, false>), grid, block, 0, stream, d_desc, nframes, d_comp, \
                        d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr, stop_last)
 #ifdef ZSK_TUNING
     switch (version) {
@@ -875,11 +921,17 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x122: ZSK_X(34); break;
     case 0x140: ZSK_X(64); break;
     case 0x180: ZSK_X(128); break;
+    case 0x141:   // the 4,096-byte stage: five waves per SIMD (2.554 ms against 2.437, config 2)
+        hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), grid, block, 0, stream, d_desc, nframes, d_comp,
+                           d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           stop_last);
+        break;
     case 0x1C0: ZSK_X(192); break;
     case 0x301: ZSK_X(256); break;    // rounds without copy_round
     case 0x302: ZSK_X(512); break;    // rounds without copy_overlap
     case 0x304: ZSK_X(1024); break;   // rounds without the readiness search
     case 0x307: ZSK_X(1792); break;   // rounds: compaction and ballots only
+    case 0x310: ZSK_X(4096); break;   // round 0: two descriptors per step
     case 0x110: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);

@@ -11,7 +11,7 @@
 // here buffered bytes always end their frame first.
 //
 // GPU mode (zsk_writer_set_gpu_compress, env ZSEEK_GPU_COMPRESS; LZ4 frames
-// of <= 64 KiB, levels < 3): lz4_frame queues the frame instead of
+// of <= 4 MiB, levels < 3): lz4_frame queues the frame instead of
 // compressing it, and a batch of queued frames is compressed by
 // zsk_lz4_compress_frames (csrc/lz4_compress.hip, byte-identical to
 // LZ4F_compressFrame) and then written and logged in queue order, each with
@@ -45,7 +45,8 @@ struct FrameLogEntry {
 };
 
 constexpr size_t kGpuDefaultBatch = 1u << 30;   // 16,384 frames of 64 KiB: ~20 GB/s per launch (bench launch_by_frames)
-constexpr size_t kGpuMaxFrame = 65536;      // one LZ4 block: the GPU compressor's limit
+constexpr size_t kGpuMaxFrame = ZSK_LZ4_COMPRESS_MAX_FRAME;   // the GPU compressor's limit
+constexpr size_t kGpuMinBatch = 65536;   // smallest batch: one 64 KiB frame
 constexpr size_t kGpuMaxBatchFrames = 65536;
 constexpr size_t kGpuTableBytes = 65536;      // compressor scratch per queued frame
 constexpr size_t kGpuFirstStaging = 64u << 20;   // staging starts here, grows x2 to the batch
@@ -106,8 +107,8 @@ struct GpuLz4 {
                 (void)hipHostFree(p);
         d_in = d_out = h_in = h_out = nullptr;
         in_cap = out_cap = 0;
-        // a slot per frame: ZSK_LZ4_COMPRESS_BOUND(n) <= n + 39 bytes
-        const size_t ocap = cap + 40 * std::min(max_frames, cap / 16 + 1);
+        // a slot per frame: ZSK_LZ4_COMPRESS_BOUND(n) <= n + n / 16384 + 39 bytes
+        const size_t ocap = cap + cap / 16384 + 40 * std::min(max_frames, cap / 16 + 1);
         if (hipHostMalloc((void **)&h_in, cap, hipHostMallocDefault) != hipSuccess ||
             hipHostMalloc((void **)&h_out, ocap, hipHostMallocDefault) != hipSuccess ||
             hipMalloc((void **)&d_in, cap) != hipSuccess || hipMalloc((void **)&d_out, ocap) != hipSuccess)
@@ -366,7 +367,7 @@ extern "C" ZSEEK_EXPORT bool zsk_writer_set_gpu_compress(zseek_writer_t *w, size
         return true;
     if (batch_bytes == 0)
         batch_bytes = kGpuDefaultBatch;
-    batch_bytes = batch_bytes < kGpuMaxFrame ? kGpuMaxFrame : batch_bytes;
+    batch_bytes = batch_bytes < kGpuMinBatch ? kGpuMinBatch : batch_bytes;
     GpuLz4 &g = w->gpu;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || hipGetDevice(&g.device) != hipSuccess) {

@@ -349,7 +349,7 @@ class Writer:
             raise ZseekError(self._err.value.decode())
 
     def set_gpu_compress(self, batch_bytes: int = 0) -> bool:
-        """zsk_writer_set_gpu_compress: LZ4 frames of <= 64 KiB compressed on
+        """zsk_writer_set_gpu_compress: LZ4 frames of <= 4 MiB compressed on
         the GPU in batches (0 = 1 GiB, -1 = off)."""
         return bool(lib().zsk_writer_set_gpu_compress(self._h, batch_bytes & ((1 << 64) - 1)))
 
@@ -629,7 +629,7 @@ def lz4_compress_layout(sizes, src_offsets=None, flags=None) -> tuple[np.ndarray
     if src_offsets is None:
         src_offsets = np.concatenate(([0], np.cumsum(sizes)[:-1])) if n else sizes
     d["src_off"] = src_offsets
-    slots = (sizes + 24 + 15) & ~np.uint64(15)
+    slots = (sizes + 4 * (sizes >> np.uint64(16)) + 24 + 15) & ~np.uint64(15)   # ZSK_LZ4_COMPRESS_BOUND
     d["dst_off"] = np.concatenate(([0], np.cumsum(slots)[:-1])) if n else slots
     if flags is not None:
         d["flags"] = flags

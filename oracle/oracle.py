@@ -129,10 +129,10 @@ class Oracle:
 
     # -- LZ4 frame compression (the reference writer's, lz4c_oracle.c) ------
     def lz4f_compress_frame(self, data, level: int = 0, content_size: bool = False) -> bytes:
-        """LZ4F_compressFrame(level, autoFlush, 64 KiB blocks) of one frame of
-        <= 64 KiB, as compress.c:750 / :483 call it."""
+        """LZ4F_compressFrame(level, autoFlush, 64 KiB blocks) of one frame,
+        as compress.c:750 / :483 call it (linked blocks above 64 KiB)."""
         s = np.frombuffer(bytes(data), np.uint8)
-        out = np.empty(s.size + 32, np.uint8)
+        out = np.empty(s.size + 4 * (s.size // 65536 + 1) + 32, np.uint8)
         r = self.lib.orc_lz4f_compress_frame(s.ctypes.data if s.size else None, s.size,
                                              out.ctypes.data, out.size, level, int(content_size))
         if r < 0:

@@ -2,8 +2,9 @@
 against the oracle restatement (pinned to liblz4 1.9.3 and the reference
 writer in test_lz4_compress.py): byte-identical frames for edge sizes and
 contents, levels, the content-size flag, stored (incompressible) blocks and
-refused descriptors; at full size, a 64 KiB-frame seekable file identical to
-the one liblz4 makes, and a round trip through the GPU decoder."""
+refused descriptors; linked frames above 64 KiB (the reference example's
+1 MiB frames); at full size, 64 KiB- and 1 MiB-frame seekable files identical
+to the ones liblz4 makes, and a round trip through the GPU decoder."""
 from __future__ import annotations
 
 import numpy as np
@@ -70,9 +71,67 @@ def test_gpu_frames_unaligned_sources(gpu, zs, oracle):
         assert got[f] == oracle.lz4f_compress_frame(chunk, 0, True), f
 
 
+def _linked_batch(oracle):
+    rng = np.random.default_rng(12)
+    syn = oracle.synth_buffer(1 << 22)
+    noise = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    blk = rng.integers(0, 256, 65536, dtype=np.uint8)
+    chunks = [syn[:1 << 20], syn[777:777 + (1 << 20)], syn[:65537], syn[:65536 + 12], syn[:65536 + 13],
+              syn[:3 * 65536 + 999], noise[:200000],
+              np.concatenate([noise[:65536], syn[:65536], noise[:70000], syn[5:5 + 2 * 65536]]),
+              np.tile(syn[:100000], 3), np.zeros(300000, np.uint8), rng.integers(0, 4, 400000, dtype=np.uint8),
+              np.tile(blk[:65535], 3), np.tile(blk, 3),
+              np.concatenate([blk, [122], blk, [122, 122], blk]).astype(np.uint8),
+              syn[: 4 << 20]]   # ZSK_LZ4_COMPRESS_MAX_FRAME
+    for _ in range(12):
+        n = int(rng.integers(65537, 1 << 21))
+        o = int(rng.integers(0, syn.size - n))
+        chunks.append(syn[o: o + n])
+    return chunks
+
+
+@pytest.mark.parametrize("level", [0, -2])
+def test_gpu_linked_frames_match_oracle(gpu, zs, oracle, level):
+    """Frames above 64 KiB: linked 64 KiB blocks on one stream, stored blocks
+    in between, short last blocks, the 65535 distance limit, 4 MiB frames."""
+    chunks = _linked_batch(oracle)
+    sizes = [c.size for c in chunks]
+    flags = np.arange(len(chunks), dtype=np.uint32) % 2
+    got, cs = _run(zs, gpu, np.concatenate(chunks), sizes, flags=flags, level=level)
+    for f, c in enumerate(chunks):
+        want = oracle.lz4f_compress_frame(c.tobytes(), level, bool(flags[f]))
+        assert got[f] == want, (f, c.size, level, int(cs[f]), len(want))
+
+
+def test_gpu_1mib_frames_match_liblz4(gpu, zs):
+    """256 MiB in the reference example's 1 MiB frames (test/example.c): every
+    GPU frame equals the one liblz4 wrote into the writer-identical image, and
+    the frames decode back to the input on the GPU."""
+    import torch
+    data = zs.synth_buffer(256 << 20)
+    img = np.asarray(zs.lz4_seekable(data, 1 << 20))
+    c_off, d_off = zs.seek_table_of(img)
+    n = len(c_off) - 1
+    got, cs = _run(zs, gpu, data, np.diff(d_off))
+    for f in range(n):
+        assert got[f] == img[c_off[f]: c_off[f + 1]].tobytes(), f
+    ddesc = np.zeros(n, zs.FRAME_DESC_DTYPE)
+    ddesc["c_off"] = c_off[:-1]
+    ddesc["d_off"] = d_off[:-1]
+    ddesc["c_size"] = np.diff(c_off)
+    ddesc["d_size"] = np.diff(d_off)
+    out = torch.empty(data.size, dtype=torch.uint8, device=gpu)
+    status = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    zs.decode_frames(torch.from_numpy(ddesc.view(np.uint8).copy()).to(gpu),
+                     torch.from_numpy(np.concatenate([img, np.zeros(16, np.uint8)])).to(gpu), out, status)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    assert np.array_equal(out.cpu().numpy(), data)
+
+
 def test_gpu_refused_descriptors(gpu, zs):
     import torch
-    desc, _ = zs.lz4_compress_layout([100, 65537, 100])
+    desc, _ = zs.lz4_compress_layout([100, (4 << 20) + 1, 100])
     desc["dst_off"][2] += 4   # not 16-byte aligned
     d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(gpu)
     src = torch.zeros(1 << 18, dtype=torch.uint8, device=gpu)

@@ -1,7 +1,8 @@
 """The writer's GPU mode (zsk_writer_set_gpu_compress):
 files byte-identical to host compression and to the compiled reference
-writer for direct, buffered and mixed write sequences, frames > 64 KiB on
-the host in order, per-frame call_data, stats, callback failures, and the
+writer for direct, buffered and mixed write sequences, linked frames above
+64 KiB (the reference example's 1 MiB frames), frames > 4 MiB on the host in
+order, per-frame call_data, stats, callback failures, and the
 file decoding back through the reader."""
 from __future__ import annotations
 
@@ -35,14 +36,16 @@ CASES = [
     (4096, [4096], 0, 65536),             # small direct frames, batch flushed every 16
     (4096, [1000], 0, 0),                 # buffered frames (content size)
     (60000, [7000, 300, 65536], -2, 0),   # mixed buffered / direct, negative level
-    (20000, [30000, 200000, 100], 0, 0),  # frames > 64 KiB go to the host, in order
+    (20000, [30000, 200000, 100], 0, 0),  # linked frames > 64 KiB on the GPU
+    (1 << 20, [1 << 20], 0, 0),           # the reference example's 1 MiB frames
+    (20000, [30000, 5 << 20, 100], 0, 0), # frames > 4 MiB go to the host, in order
     (1, [1, 2, 3], 0, 65536),             # tiny frames
 ]
 
 
 @pytest.mark.parametrize("min_frame,sizes,level,batch", CASES)
 def test_gpu_writer_matches_host(gpu, zs, min_frame, sizes, level, batch):
-    data = bytes(zs.synth_buffer(3 << 20)) + b"end" * 1000
+    data = bytes(zs.synth_buffer((12 if max(sizes) > 1 << 20 else 3) << 20)) + b"end" * 1000
     if min_frame == 1:
         data = data[:20000]
     chunks = _writes(data, sizes)
@@ -54,9 +57,12 @@ def test_gpu_writer_matches_host(gpu, zs, min_frame, sizes, level, batch):
         assert r.read_all(len(data), 0) == data
 
 
-@pytest.mark.parametrize("min_frame,write", [(65536, 65536), (4096, 1000)])
+@pytest.mark.parametrize("min_frame,write", [(65536, 65536), (4096, 1000), (1 << 20, 1 << 16),
+                                             (1 << 20, 1 << 20)])
 def test_gpu_writer_matches_reference(gpu, zs, ref, min_frame, write):
-    data = bytes(zs.synth_buffer(2 << 20)) + b"tail" * 333
+    """Byte-identical to the compiled reference writer, including the
+    reference example's 1 MiB frames (test/example.c)."""
+    data = bytes(zs.synth_buffer((6 if min_frame > 65536 else 2) << 20)) + b"tail" * 333
     dev, _ = _file(zs, _writes(data, [write]), min_frame, gpu_batch=0)
     assert dev == ref.compress(data, zs.ZSEEK_LZ4, min_frame, write)
 

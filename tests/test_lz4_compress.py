@@ -37,7 +37,7 @@ def liblz4():
         p.frame_info.content_size = content_size  # compress.c:741 / :472
         p.compression_level = level               # compress.c:203
         p.auto_flush = 1                          # compress.c:205
-        out = C.create_string_buffer(len(data) + 64)
+        out = C.create_string_buffer(len(data) + 4 * (len(data) // 65536) + 64)
         r = L.LZ4F_compressFrame(out, len(out), data, len(data), C.byref(p))
         assert r < (1 << 63)
         return out.raw[:r]
@@ -71,6 +71,28 @@ def test_restatement_matches_liblz4(oracle, liblz4, level):
             assert got == want, (i, len(b), level, cs)
 
 
+@pytest.mark.parametrize("level", [0, -2])
+def test_linked_restatement_matches_liblz4(oracle, liblz4, level):
+    """Frames above 64 KiB: linked 64 KiB blocks on one stream (the reference
+    example's 1 MiB frames, test/example.c), with stored blocks in between
+    (whose stream state still advances) and a short last block."""
+    rng = np.random.default_rng(11)
+    syn = oracle.synth_buffer(1 << 22).tobytes()
+    noise = bytes(rng.integers(0, 256, 1 << 20, dtype=np.uint8))
+    cases = [syn[:1 << 20], syn[12345:12345 + (1 << 20)], syn[:65537], syn[:65536 + 12],
+             syn[:65536 + 13], syn[:3 * 65536 + 999], noise[:200000],
+             noise[:65536] + syn[:65536] + noise[:70000] + syn[5:65536 * 2],
+             syn[:100000] * 3, b"\0" * 300000, bytes(rng.integers(0, 4, 400000, dtype=np.uint8))]
+    # a pattern repeating at 65535 / 65536 / 65537 bytes: distance-limit edge
+    blk = bytes(rng.integers(0, 256, 65536, dtype=np.uint8))
+    cases += [blk[:65535] * 3, blk * 3, blk + b"z" + blk + b"zz" + blk]
+    for i, b in enumerate(cases):
+        for cs in (0, 1):
+            want = liblz4(b, level, cs)
+            assert want[4] & 0x20 == 0, "linked"
+            assert oracle.lz4f_compress_frame(b, level, bool(cs)) == want, (i, len(b), cs)
+
+
 def test_incompressible_frame_is_stored(oracle, liblz4):
     b = bytes(np.random.default_rng(3).integers(0, 256, 65536, dtype=np.uint8))
     f = oracle.lz4f_compress_frame(b, 0, False)
@@ -81,11 +103,14 @@ def test_incompressible_frame_is_stored(oracle, liblz4):
 
 
 @pytest.mark.parametrize("min_frame,write,level", [(65536, 65536, 0), (4096, 4096, 0), (4096, 1000, 0),
-                                                   (60000, 7000, 0), (20000, 20000, -3)])
+                                                   (60000, 7000, 0), (20000, 20000, -3),
+                                                   (1 << 20, 1 << 16, 0), (1 << 20, 1 << 20, 0),
+                                                   (300000, 300000, -1)])
 def test_restatement_matches_reference_writer(oracle, ref, min_frame, write, level):
     """Every frame of a file the compiled reference writer made: direct frames
     (write >= min_frame) without content size, buffered ones with it."""
-    data = oracle.synth_buffer(1 << 20).tobytes() + b"tail" * 333
+    size = 1 << 20 if min_frame <= 65536 else 5 << 20
+    data = oracle.synth_buffer(size).tobytes() + b"tail" * 333
     img = ref.compress(data, 1, min_frame, write, level=level)   # ZSEEK_LZ4
     st = oracle.seek_table(img)
     n, c_off, d_off = st["frames"], [int(x) for x in st["c_off"]], [int(x) for x in st["d_off"]]
