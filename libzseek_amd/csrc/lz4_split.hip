@@ -7,7 +7,7 @@
 //
 //   plan     lz4_plan_direct_kernel (lane per frame): each frame's slots in
 //            the item scratch, straight from its compressed offset; frames out
-//            of file order fall back to lz4_plan_kernel (one-workgroup scan);
+//            of file order fall back to a scan by its last workgroup;
 //   parse    ONE LANE PER FRAME for 64 KiB-class frames (lz4_lean.hip,
 //            lz4_scan.hip for short frames) or ONE WAVE PER FRAME for big
 //            frames and small batches (lz4_chunk.hip): the serial token chain
@@ -45,7 +45,11 @@ using namespace lz4d;
 // in the input (c_off[f+1] >= c_off[f] + c_size[f], as in every batch the
 // reader builds), frame f's slots start at ceil4((c_off[f] - c_off[0]) / 8 +
 // 40 f), and the gap to frame f+1 is >= c_size/8 + 37 > slots_of(c_size).  A
-// frame out of order sets *redo, and lz4_plan_kernel scans instead.
+// frame out of order sets redo[0]; the workgroup that finishes last (redo[1]
+// counts finished workgroups) then lays the slots out by a scan of
+// slots_of(c_size) instead, and clears both words for the next launch on this
+// scratch (zeroed at allocation).  Round 3 ran the scan as its own launch
+// behind a flag memset: two launches that did nothing in the usual batch.
 __global__ __launch_bounds__(256) void lz4_plan_direct_kernel(const FrameDesc *__restrict__ desc,
                                                                uint32_t n, uint64_t *__restrict__ rec_base,
                                                                uint64_t *__restrict__ total,
@@ -53,56 +57,64 @@ __global__ __launch_bounds__(256) void lz4_plan_direct_kernel(const FrameDesc *_
                                                                int32_t *__restrict__ status,
                                                                uint32_t *__restrict__ fail_at)
 {
+    __shared__ uint64_t part[256];
+    __shared__ uint32_t last;
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
-    if (f >= n)
+    if (f < n) {
+        // every frame starts as not run (a parse kernel then owns it), with no
+        // failing block: the reader needs no fills of its own
+        status[f] = ST_NOT_RUN;
+        if (fail_at)
+            fail_at[f] = 0;
+        const FrameDesc d = desc[f];
+        const uint64_t c0 = desc[0].c_off;
+        const uint64_t r = (((d.c_off - c0) >> 3) + 40ull * f + 3) & ~3ull;
+        rec_base[f] = r;
+        if (d.c_off < c0 || (f + 1 < n && desc[f + 1].c_off < d.c_off + d.c_size))
+            atomicOr(&redo[0], 1u);
+        if (f + 1 == n)
+            *total = r + slots_of(d.c_size);
+    }
+    if (n == 1)   // one frame is always in order
         return;
-    // every frame starts as not run (a parse kernel then owns it), with no
-    // failing block: the reader needs no fills of its own
-    status[f] = ST_NOT_RUN;
-    if (fail_at)
-        fail_at[f] = 0;
-    const FrameDesc d = desc[f];
-    const uint64_t c0 = desc[0].c_off;
-    const uint64_t r = (((d.c_off - c0) >> 3) + 40ull * f + 3) & ~3ull;
-    rec_base[f] = r;
-    if (d.c_off < c0 || (f + 1 < n && desc[f + 1].c_off < d.c_off + d.c_size))
-        *redo = 1;
-    if (f + 1 == n)
-        *total = r + slots_of(d.c_size);
-}
-
-// Slot offsets by an exclusive scan of slots_of(c_size), one workgroup; runs
-// only when lz4_plan_direct_kernel flagged the batch (*redo != 0).
-__global__ __launch_bounds__(1024) void lz4_plan_kernel(const FrameDesc *__restrict__ desc,
-                                                        uint32_t n, uint64_t *__restrict__ rec_base,
-                                                        uint64_t *__restrict__ total,
-                                                        const uint32_t *__restrict__ redo)
-{
-    __shared__ uint64_t part[1024];
-    if (*redo == 0)
-        return;
-    const uint32_t t = threadIdx.x;
-    const uint32_t chunk = (n + 1023) / 1024;
-    const uint32_t i0 = t * chunk < n ? t * chunk : n;
-    const uint32_t i1 = i0 + chunk < n ? i0 + chunk : n;
-    uint64_t s = 0;
-    for (uint32_t i = i0; i < i1; i++)
-        s += slots_of(desc[i].c_size);
-    part[t] = s;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        uint64_t v = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&redo[1], 1u) == gridDim.x - 1 ? 1u : 0u;
     }
-    uint64_t run = part[t] - s;
-    for (uint32_t i = i0; i < i1; i++) {
-        rec_base[i] = run;
-        run += slots_of(desc[i].c_size);
+    __syncthreads();
+    if (!last)
+        return;
+    __threadfence();
+    if (atomicOr(&redo[0], 0u)) {
+        const uint32_t t = threadIdx.x;
+        const uint32_t chunk = (n + 255) / 256;
+        const uint32_t i0 = t * chunk < n ? t * chunk : n;
+        const uint32_t i1 = i0 + chunk < n ? i0 + chunk : n;
+        uint64_t sum = 0;
+        for (uint32_t i = i0; i < i1; i++)
+            sum += slots_of(desc[i].c_size);
+        part[t] = sum;
+        __syncthreads();
+        for (uint32_t k = 1; k < 256; k <<= 1) {
+            const uint64_t v = t >= k ? part[t - k] : 0;
+            __syncthreads();
+            part[t] += v;
+            __syncthreads();
+        }
+        uint64_t run = part[t] - sum;
+        for (uint32_t i = i0; i < i1; i++) {
+            rec_base[i] = run;
+            run += slots_of(desc[i].c_size);
+        }
+        if (t == 255)
+            *total = part[t];
     }
-    if (t == 1023)
-        *total = part[t];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        redo[0] = 0;
+        redo[1] = 0;
+    }
 }
 
 // ---- block route plan ---------------------------------------------------------
@@ -331,8 +343,15 @@ int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipS
             return -1;
         *s->total = 0;
     }
-    if (!s->redo && hipMalloc((void **)&s->redo, sizeof(uint32_t)) != hipSuccess)
-        return -1;
+    if (!s->redo) {   // [out-of-order flag, plan workgroups done]: zero between launches
+        if (hipMalloc((void **)&s->redo, 2 * sizeof(uint32_t)) != hipSuccess)
+            return -1;
+        if (hipMemsetAsync(s->redo, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) {
+            (void)hipFree(s->redo);
+            s->redo = nullptr;
+            return -1;
+        }
+    }
     if (frames > s->frames_cap) {
         uint32_t cap = frames < 4096 ? 4096 : frames;
         (void)hipStreamSynchronize(stream);
@@ -499,14 +518,8 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     SplitScratch *blk = br.on ? s : nullptr;
     stage_mark(0, stream);
     if (stages & 1) {
-        // (one frame is always in order: no redo flag, no scan)
-        if (nframes > 1)
-            (void)hipMemsetAsync(s->redo, 0, sizeof(uint32_t), stream);
         hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, s->rec_base, total_dev, s->redo, d_status, d_fail_at);
-        if (nframes > 1)
-            hipLaunchKernelGGL(lz4_plan_kernel, dim3(1), dim3(1024), 0, stream, d_desc, nframes,
-                               s->rec_base, total_dev, s->redo);
         if (blk) {
             (void)hipMemsetAsync(s->njobs, 0, sizeof(uint32_t), stream);
             hipLaunchKernelGGL(lz4_block_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,

@@ -311,6 +311,29 @@ __device__ __forceinline__ void copy_desc4(const Stage &S, const uint8_t *lbase,
     for (uint32_t t0 = 0; t0 < TT; t0 += 256) {
         u32x4 v[4];
         uint32_t dw[4], sx[4];
+        if (DIAG & 8192) {
+            // the step's descriptors read together (one LDS wait), then the
+            // loads: slots past the step's count are skipped uniformly
+            const uint32_t ns = min(4u, (TT - t0 + 63) >> 6);
+            uint64_t D[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t t = t0 + 64 * j + lane;
+                D[j] = (uint32_t)j < ns ? *lp<uint64_t>(descs + 8 * (t < TT ? t : 0)) : 0;
+                if (t >= TT)
+                    D[j] = 0;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                sx[j] = (uint32_t)D[j];
+                dw[j] = (uint32_t)(D[j] >> 32);
+                if ((uint32_t)j < ns) {
+                    const uint32_t kind = dw[j] >> 24;
+                    const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);
+                    v[j] = (DIAG & 1) ? (u32x4){0, 0, 0, 0} : *reinterpret_cast<const u32x4_l *>(p);
+                }
+            }
+        } else
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t t = t0 + 64 * j + lane;
@@ -811,6 +834,19 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
             // (lane order) into the descriptor area, then binary-search the
             // first one below this lane that ends after msrc; blocked iff it
             // also starts before need
+            bool ready;
+            if (DIAG & 16384) {
+                // every pending lane's destination broadcast in turn (no LDS
+                // round trips): blocked iff a lower pending destination meets
+                // this lane's source range
+                bool blocked = false;
+                for (uint64_t pm = pending; pm; pm &= pm - 1) {
+                    const int j = (int)__builtin_ctzll(pm);
+                    const uint32_t mbj = lane_val(mb, j), mej = lane_val(me, j);
+                    blocked |= (uint32_t)j < lane && mej > msrc && mbj < need;
+                }
+                ready = mine && !blocked;
+            } else {
             const uint32_t below = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(pending >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pending, 0u));
             if (mine)
@@ -828,8 +864,9 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
                 }
             }
             const uint32_t mbl = (uint32_t)*lp<uint64_t>(descs + 8 * (mine && lo < below ? lo : 0));
-            const bool ready = mine && !(lo < below && mbl < need);
+            ready = mine && !(lo < below && mbl < need);
             wave_lds_sync();
+            }
             if (!(DIAG & 512)) {
                 for (uint64_t ov = __ballot(ready && overlap); ov; ov &= ov - 1) {
                     const int i = (int)__builtin_ctzll(ov);
@@ -932,6 +969,9 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x304: ZSK_X(1024); break;   // rounds without the readiness search
     case 0x307: ZSK_X(1792); break;   // rounds: compaction and ballots only
     case 0x310: ZSK_X(4096); break;   // round 0: two descriptors per step
+    case 0x320: ZSK_X(8192); break;   // round 0: the deal's descriptor reads together
+    case 0x340: ZSK_X(16384); break;  // rounds: readiness by broadcast instead of the LDS search
+    case 0x360: ZSK_X(24576); break;  // both
     case 0x110: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);

@@ -35,7 +35,7 @@ bench = json.load(open(os.path.join(src, "bench.json")))
 KERNEL = bench["roofline"]["kernel"]   # the dominant kernel bench.py reports
 # kernels of one decode launch (zsk_lz4_decode_frames): the two-phase decoder
 # runs plan + parse + execute + the (normally empty) hand-off pass
-LAUNCH = ("lz4_plan_direct_kernel", "lz4_plan_kernel", "lz4_block_plan_kernel", "lz4_lean_kernel", "lz4_chunk_kernel",
+LAUNCH = ("lz4_plan_direct_kernel", "lz4_block_plan_kernel", "lz4_lean_kernel", "lz4_chunk_kernel",
           "lz4_scan_kernel",
           "seq_exec_kernel", "lz4_wave_kernel",
           "lz4_lane_kernel", "lz4_parse_kernel", "lz4_exec_kernel")
