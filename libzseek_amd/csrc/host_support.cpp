@@ -359,9 +359,23 @@ hipError_t hip_stream_get(hipStream_t *s, bool low)
     return e;
 }
 
+// Streams and events are destroyed when released.  Env ZSEEK_HIP_POOL=1
+// keeps them in the process-wide pool instead (round 3's workaround, kept as
+// the control arm of scripts/hang_probe.py; see DESIGN.md §7 "Teardown").
+static bool hip_destroy_handles()
+{
+    static const bool on = [] {
+        const char *v = getenv("ZSEEK_HIP_POOL");
+        return !(v && !strcmp(v, "1"));
+    }();
+    return on;
+}
+
 void hip_stream_put(hipStream_t s)
 {
-    if (s)
+    if (s && hip_destroy_handles())
+        (void)hipStreamDestroy(s);
+    else if (s)
         handle_give(s);
 }
 
@@ -378,7 +392,9 @@ hipError_t hip_event_get(hipEvent_t *ev)
 
 void hip_event_put(hipEvent_t e)
 {
-    if (e)
+    if (e && hip_destroy_handles())
+        (void)hipEventDestroy(e);
+    else if (e)
         handle_give(e);
 }
 
@@ -439,12 +455,10 @@ bool Slot::reserve(size_t comp, size_t out, size_t host_out, size_t nframes, boo
 // Teardown order: every stream drained (the slot's, its host copies, the
 // zstd scratch's side streams); then all memory, while every stream that used
 // it still exists; then the streams and the events recorded on them go back
-// to the process-wide pool (hip_stream_put / hip_event_put: never destroyed).
-// Round 2 saw the host heap corrupted when events went before streams; round
-// 3 saw hipFree fault (and, in later runs, the host heap left corrupted) when
-// device buffers were freed after the streams whose kernels last used them
-// had been destroyed (scripts/hang_probe.py reproduced it within ~25
-// open/read/close cycles).
+// go (hip_stream_put / hip_event_put destroy them).  Rounds 2-3 saw the host
+// heap corrupted under reader churn; the cause was the compiled reference's
+// libzstd 1.4.9 sharing one link namespace with the system libzstd in test
+// processes, not HIP object lifetimes (DESIGN.md §7 "Teardown").
 void Slot::destroy()
 {
     if (!stream)

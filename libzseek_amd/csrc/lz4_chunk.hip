@@ -483,7 +483,7 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
     uint32_t min_csize, uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
     const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, const uint32_t *__restrict__ njobs,
-    uint32_t min_jobs)
+    uint32_t min_jobs, uint64_t *__restrict__ solo_total)
 {
     __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
     __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
@@ -523,6 +523,13 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
         __syncthreads();
         if (threadIdx.x >= 64)
             return;
+        // a batch of one frame launches no plan kernel (solo_total != null):
+        // its slots start at 0 and the total the plan would report is this
+        // frame's; status and fail_at are written below whatever happens
+        if (solo_total && lane == 0) {
+            const_cast<uint64_t *>(rec_base)[0] = 0;
+            *solo_total = slots_of(d.c_size);
+        }
         ZSK_CT(0)
     }
     if (uni(d.c_size) < min_csize)
@@ -561,7 +568,7 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
                 bfirst[f] = kNoJob;
         }
     }
-    const uint64_t rb0 = rec_base[f];
+    const uint64_t rb0 = (ONE && solo_total) ? 0 : rec_base[f];
     const uint32_t cap = slots_of(d.c_size);
     const uint32_t clen = d.c_size, dlen = d.d_size;
     const uint32_t mapbase = (uint32_t)(uintptr_t)(maps) + w * (64 * kMapW * 4);
@@ -722,14 +729,14 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
-                     SplitScratch *blk, uint32_t min_jobs, bool one)
+                     SplitScratch *blk, uint32_t min_jobs, bool one, uint64_t *solo_total)
 {
     if (nframes == 0)
         return 0;
     if (one) {
         hipLaunchKernelGGL(lz4_chunk_kernel<true>, dim3(nframes), dim3(64 * kOneWaves), 0, stream, d_desc, nframes,
                            d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0u);
+                           nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr);
 #ifdef ZSK_TUNING
         if (getenv("ZSEEK_CHUNK_TIMERS")) {
             unsigned long long z[16];
@@ -756,7 +763,7 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                            d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
                            min_csize, blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr,
                            blk ? blk->jobs : nullptr, blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr,
-                           min_jobs);
+                           min_jobs, nullptr);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -517,7 +517,9 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         br.on = false;   // no room: the chunk parse takes the frames as before
     SplitScratch *blk = br.on ? s : nullptr;
     stage_mark(0, stream);
-    if (stages & 1) {
+    // one frame on the one-frame route: the chunk kernel does the plan's work
+    const bool solo = one && nframes == 1 && (stages & 3) == 3;
+    if ((stages & 1) && !solo) {
         hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream,
                            d_desc, nframes, s->rec_base, total_dev, s->redo, d_status, d_fail_at);
         if (blk) {
@@ -543,7 +545,8 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                             s->nitems, d_status, d_fail_at, stream, r.lean_min < r.chunk_min ? r.lean_min : r.chunk_min);
         if (r.chunk_min != 0xFFFFFFFFu)
             launch_lz4_chunk(d_desc, nframes, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items,
-                             s->nitems, d_status, d_fail_at, stream, r.chunk_min, blk, br.min_jobs, one);
+                             s->nitems, d_status, d_fail_at, stream, r.chunk_min, blk, br.min_jobs, one,
+                             solo ? total_dev : nullptr);
     }
     stage_mark(2, stream);
     if (stages & 4)

@@ -174,12 +174,10 @@ enum : int { ENGINE_AUTO = 0, ENGINE_SPLIT, ENGINE_WAVE };
 constexpr int kTimedStages = 4;
 void stage_mark(int boundary, hipStream_t stream);
 
-// HIP streams and events are recycled process-wide, never destroyed: a
-// reader's slots take them at open and give them back (drained) at close.
-// Destroying them per reader let the runtime's own threads touch freed
-// objects after hipStreamSynchronize had returned (host heap corruption under
-// reader open/close churn, scripts/hang_probe.py).  On the current device;
-// low = the lowest stream priority.
+// HIP streams and events of reader slots and writers: created on the current
+// device (low = the lowest stream priority), destroyed drained at release;
+// env ZSEEK_HIP_POOL=1 recycles them process-wide instead (round 3's
+// workaround for a heap corruption whose cause was elsewhere).
 hipError_t hip_stream_get(hipStream_t *s, bool low);
 void hip_stream_put(hipStream_t s);
 hipError_t hip_event_get(hipEvent_t *e);
@@ -294,7 +292,10 @@ int launch_lz4_lean_blocks(const FrameDesc *d_desc, const uint8_t *d_comp, const
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
-                     SplitScratch *blk = nullptr, uint32_t min_jobs = 0, bool one = false);
+                     SplitScratch *blk = nullptr, uint32_t min_jobs = 0, bool one = false,
+                     uint64_t *solo_total = nullptr);
+// (one && nframes == 1 && solo_total: the batch has no plan launch; the
+// kernel lays the frame's slots out itself and reports their total there)
 // Frames of at least chunk_parse_min(nframes) compressed bytes go to the
 // chunk parse: with >= 32768 frames the lane-per-frame scan has a lane for
 // every frame it needs and wins on 64 KiB frames (2.07 vs 4.18 ms parse at

@@ -13,6 +13,9 @@ timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err && cat $O/benc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -- python bench.py --profile --steps 5 --warmup 1 > $O/trace.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -- python bench.py --profile --steps 2 --warmup 1 > $O/pmc_fetch.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -- python bench.py --profile --steps 2 --warmup 1 > $O/pmc_write.log 2>&1 &&
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $O/p1 -- python bench.py --profile --steps 2 --warmup 1 > $O/p1.log 2>&1 &&
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_BUSY_CYCLES --output-format csv -d $O/p2 -- python bench.py --profile --steps 2 --warmup 1 > $O/p2.log 2>&1 &&
+python3 scripts/pmc_summary.py $O > $O/sq_summary.txt 2>&1 &&
 echo "config 2 profiles done" &&
 timeout -k 10 600 python bench.py --codec zstd > $Z/bench.json 2> $Z/bench.err && cat $Z/bench.json &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $Z/trace -- python bench.py --codec zstd --profile --steps 5 --warmup 1 > $Z/trace.log 2>&1 &&
@@ -22,6 +25,8 @@ echo "config 5 profiles done" &&
 timeout -k 10 400 python bench.py --frame 4096 --steps 5 --warmup 2 --no-e2e > $S/f4096.json 2> $S/f4096.err && cat $S/f4096.json &&
 timeout -k 10 400 python bench.py --frame 1048576 --steps 5 --warmup 2 --no-e2e > $S/f1048576.json 2> $S/f1048576.err && cat $S/f1048576.json &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $S/trace1m -- python bench.py --frame 1048576 --profile --steps 5 --warmup 1 > $S/trace1m.log 2>&1 &&
+timeout -k 10 400 python bench.py --codec lz4c --steps 3 --warmup 1 > $S/lz4c.json 2> $S/lz4c.err && cat $S/lz4c.json &&
+timeout -k 10 400 python bench.py --codec lz4c --frame 1048576 --size 1073741824 --steps 3 --warmup 1 > $S/lz4c_1m.json 2> $S/lz4c_1m.err && cat $S/lz4c_1m.json &&
 timeout -k 10 200 python scripts/pcie_probe.py > $O/pcie.json 2> $O/pcie.err && cat $O/pcie.json
 rc=$?
 exit $rc
