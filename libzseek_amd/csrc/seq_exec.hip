@@ -42,6 +42,7 @@ constexpr uint32_t x_wave(uint32_t outb) { return x_buf(outb) + 8 * x_pieces(out
 constexpr uint32_t kBad = 0x80000000u;      // buffer offset past any range: load returns 0
 
 typedef u32x4 u32x4_l __attribute__((aligned(1)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint64_t u64_l __attribute__((aligned(1)));
 typedef uint32_t u32_l __attribute__((aligned(1)));
 typedef uint16_t u16_l __attribute__((aligned(1)));
@@ -286,6 +287,43 @@ __device__ __forceinline__ void copy_desc4(const Stage &S, const uint8_t *lbase,
                                                                (uint32_t)(d1 >> 32)};
                 else
                     *lp<uint64_t>(al + 8 * (lpn + i)) = d0;
+            }
+        }
+    } else if (DIAG & 32768) {
+        // (tuning) runs of at most kShortRun pieces: the lane writes its own (at most
+        // kShortRun steps, both descriptor halves advanced by 32-bit adds);
+        // longer runs: the whole wave writes one run's pieces per step
+        constexpr uint32_t kShortRun = 6;
+        const uint32_t lq = lpn <= kShortRun ? lpn : 0, mq = mpn <= kShortRun ? mpn : 0;
+        const uint32_t dl0 = (uint32_t)dl, dl1 = (uint32_t)(dl >> 32);
+        const uint32_t dm0 = (uint32_t)dm, dm1 = (uint32_t)(dm >> 32);
+        constexpr uint32_t kst1 = (K_STAGE - K_HBM) << 24;
+        for (uint32_t i = 0; __ballot(i < lq || i < mq); i++) {
+            if (i < lq) {
+                const uint32_t o = min(16 * i, lm);
+                *lp<u32x2>(al + 8 * i) = (u32x2){dl0 + o, dl1 + o};
+            }
+            if (i < mq) {
+                const uint32_t o = min(16 * i, mm);
+                *lp<u32x2>(al + 8 * (lpn + i)) = (u32x2){dm0 + o, dm1 + o + (msrc + o + 16 > flushed ? kst1 : 0)};
+            }
+        }
+        for (uint64_t L = __ballot(lpn > kShortRun); L; L &= L - 1) {
+            const int j = (int)__builtin_ctzll(L);
+            const uint32_t n = lane_val(lpn, j), m = lane_val(lm, j), a = lane_val(al, j);
+            const uint32_t d0 = lane_val(dl0, j), d1 = lane_val(dl1, j);
+            for (uint32_t i = lane; i < n; i += 64) {
+                const uint32_t o = min(16 * i, m);
+                *lp<u32x2>(a + 8 * i) = (u32x2){d0 + o, d1 + o};
+            }
+        }
+        for (uint64_t M = __ballot(mpn > kShortRun); M; M &= M - 1) {
+            const int j = (int)__builtin_ctzll(M);
+            const uint32_t n = lane_val(mpn, j), m = lane_val(mm, j), a = lane_val(al + 8 * lpn, j);
+            const uint32_t d0 = lane_val(dm0, j), d1 = lane_val(dm1, j), sm = lane_val(msrc, j);
+            for (uint32_t i = lane; i < n; i += 64) {
+                const uint32_t o = min(16 * i, m);
+                *lp<u32x2>(a + 8 * i) = (u32x2){d0 + o, d1 + o + (sm + o + 16 > flushed ? kst1 : 0)};
             }
         }
     } else {
@@ -652,13 +690,15 @@ struct JobMap<true> {
 // slots with a uniform job cursor, so batches run across jobs unchanged.
 // (SEG runs at 4 waves per SIMD: its batches have <= 32,767 frames -- config
 // 3's 4,096 fill 4 per SIMD -- and the job cursor's registers fit no spill)
-// The LZ4 route's stage: 3,584 bytes -> 25.9 KB of LDS per 4-wave group,
-// six waves per SIMD (78 VGPRs fit 6); a batch of config 2 averages 2.7 KB,
-// so the smaller stage rarely cuts one, and the sixth wave hides latency.
-constexpr uint32_t kExecStage = 3584;
+// The LZ4 route's stage: 3,072 bytes -> 22.8 KB of LDS per 4-wave group,
+// seven waves per SIMD (72 VGPRs); a batch of config 2 averages 2.7 KB, so
+// the smaller stage cuts few, and the extra waves hide latency (config 2,
+// execute alone, interleaved: 4,096 bytes / 5 waves 2.554 ms, 3,584 / 6
+// 2.438, 3,072 / 7 2.411; 2,560 / 8 needs 64 VGPRs and spills: 2.897).
+constexpr uint32_t kExecStage = 3072;
 
 template <int DIAG, uint32_t OUTB, bool SEG>
-__global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 4 : (OUTB <= 3584 ? 6 : 5)))) void seq_exec_kernel(
+__global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 4 : (OUTB <= 2560 ? 8 : OUTB <= 3072 ? 7 : OUTB <= 3584 ? 6 : 5)))) void seq_exec_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ out, const uint64_t *__restrict__ rec_base,
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
@@ -958,8 +998,18 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x122: ZSK_X(34); break;
     case 0x140: ZSK_X(64); break;
     case 0x180: ZSK_X(128); break;
-    case 0x141:   // the 4,096-byte stage: five waves per SIMD (2.554 ms against 2.437, config 2)
+    case 0x141:   // the 4,096-byte stage: five waves per SIMD
         hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), grid, block, 0, stream, d_desc, nframes, d_comp,
+                           d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           stop_last);
+        break;
+    case 0x142:   // the 3,584-byte stage, six waves per SIMD
+        hipLaunchKernelGGL((seq_exec_kernel<0, 3584, false>), grid, block, 0, stream, d_desc, nframes, d_comp,
+                           d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           stop_last);
+        break;
+    case 0x143:   // a 2,560-byte stage, eight waves per SIMD (64 VGPRs: spills)
+        hipLaunchKernelGGL((seq_exec_kernel<0, 2560, false>), grid, block, 0, stream, d_desc, nframes, d_comp,
                            d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr,
                            stop_last);
         break;
@@ -972,6 +1022,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x320: ZSK_X(8192); break;   // round 0: the deal's descriptor reads together
     case 0x340: ZSK_X(16384); break;  // rounds: readiness by broadcast instead of the LDS search
     case 0x360: ZSK_X(24576); break;  // both
+    case 0x380: ZSK_X(32768); break;  // round 0: long runs' descriptors by the whole wave (-0.8 % at 6 waves, +0.5 % at 7)
     case 0x110: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
