@@ -235,9 +235,12 @@ ZSK_TOOL int zsk_tool_lz4_seekable_ex(const uint8_t *in, size_t n, size_t frame_
 
 namespace {
 // The compressor's libzstd: the reference's pinned 1.4.9 (SURVEY.md §8c,
-// /root/reference/meson.build:10-11) by full path -- a path dlopen maps its
-// own copy beside the system libzstd.so.1 this library links -- else the
-// linked one.
+// /root/reference/meson.build:10-11) by full path in a link namespace of its
+// own (dlmopen), else the linked one.  A plain dlopen mapped the 1.4.9 copy
+// beside the system libzstd.so.1 this library links, but left the copy's
+// calls to its own exported functions to the global scope, where 1.4.8's
+// definitions come first: a 1.4.9 CCtx reset by 1.4.8 code (a SIGSEGV in
+// free under ZSTD_CCtx_reset, round 4, config-5 input under rocprofv3).
 struct ZstdApi {
     unsigned (*version)(void) = ZSTD_versionNumber;
     size_t (*bound)(size_t) = ZSTD_compressBound;
@@ -253,7 +256,7 @@ const ZstdApi &zstd_api()
     static const ZstdApi api = [] {
         ZstdApi a;
         const char *path = getenv("ZSEEK_TOOLS_LIBZSTD");
-        void *h = dlopen(path ? path : "/opt/conda/lib/libzstd.so.1.4.9", RTLD_NOW | RTLD_LOCAL);
+        void *h = dlmopen(LM_ID_NEWLM, path ? path : "/opt/conda/lib/libzstd.so.1.4.9", RTLD_NOW | RTLD_LOCAL);
         if (!h)
             return a;
         ZstdApi b;
