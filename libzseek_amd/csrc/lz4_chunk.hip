@@ -483,7 +483,7 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
     uint32_t min_csize, uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
     const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, const uint32_t *__restrict__ njobs,
-    uint32_t min_jobs, uint64_t *__restrict__ solo_total)
+    uint32_t min_jobs, uint64_t *__restrict__ solo_total, uint32_t per_wave)
 {
     __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
     __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
@@ -491,9 +491,8 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
     __shared__ __attribute__((aligned(16))) uint64_t recs[ONE ? 64 * kRec : 1];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t w = ONE ? 0 : threadIdx.x >> 6;
-    const uint32_t f = ONE ? blockIdx.x : uni(blockIdx.x * kCW + w);
-    if (f >= n)
-        return;
+    // one frame (wave-uniform f); a return ends that frame
+    auto frame = [&](const uint32_t f) {
     const FrameDesc d = desc[f];
 #ifdef ZSK_TUNING
     uint64_t tmark_ = __builtin_readcyclecounter();
@@ -722,6 +721,22 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
         if (fail_at)
             fail_at[f] = fail_op;
     }
+    };
+    if constexpr (ONE) {
+        if (blockIdx.x < n)
+            frame(blockIdx.x);
+    } else {
+        // per_wave consecutive frames per wave, their sizes read at once: the
+        // ones of this route are parsed in turn (a batch whose frames all
+        // take another parse costs one descriptor load per wave, not one
+        // wave per frame)
+        const uint32_t f0 = uni((blockIdx.x * kCW + w) * per_wave);
+        if (f0 >= n)
+            return;
+        for (uint64_t todo = __ballot(lane < per_wave && f0 + lane < n && desc[f0 + lane].c_size >= min_csize);
+             todo; todo &= todo - 1)
+            frame(f0 + (uint32_t)__builtin_ctzll(todo));
+    }
 }
 
 }   // namespace
@@ -736,7 +751,7 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     if (one) {
         hipLaunchKernelGGL(lz4_chunk_kernel<true>, dim3(nframes), dim3(64 * kOneWaves), 0, stream, d_desc, nframes,
                            d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr);
+                           nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u);
 #ifdef ZSK_TUNING
         if (getenv("ZSEEK_CHUNK_TIMERS")) {
             unsigned long long z[16];
@@ -759,11 +774,15 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         }
 #endif
     } else {
-        hipLaunchKernelGGL(lz4_chunk_kernel<false>, dim3((nframes + kCW - 1) / kCW), dim3(64 * kCW), 0, stream,
+        // frames per wave: >= 16,384 waves whatever the batch (every frame may
+        // take this parse), at most 64
+        const uint32_t per = min(64u, max(1u, nframes / 16384));
+        const uint32_t waves = (nframes + per - 1) / per;
+        hipLaunchKernelGGL(lz4_chunk_kernel<false>, dim3((waves + kCW - 1) / kCW), dim3(64 * kCW), 0, stream,
                            d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
                            min_csize, blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr,
                            blk ? blk->jobs : nullptr, blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr,
-                           min_jobs, nullptr);
+                           min_jobs, nullptr, per);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
