@@ -48,6 +48,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "../../include/zseek_hip.h"
 #include "zsk_internal.h"
 
@@ -268,13 +270,19 @@ __device__ __forceinline__ uint32_t count_eq(const uint8_t *s, uint32_t a, uint3
 // is loaded from the input); kVal = true keeps each entry's input word beside
 // its position (u64: word << 32 | position + 1; 0 = liblz4's zeroed entry,
 // position 0), so a probe compares without loading the candidate's word.
-template <uint32_t kProbe, bool kVal, bool kLinked = false>   // probes per batch, table layout
+// VPtr: the position + word table's pointer type (HBM scratch, or LDS for
+// the linked kernel: vtab).
+template <uint32_t kProbe, bool kVal, bool kLinked = false, typename VPtr = uint64_t *>
 __device__ uint32_t compress_block(const uint8_t *__restrict__ s, uint32_t b0, uint32_t n,
-                                   void *__restrict__ table, Packer &o, uint32_t accel)
+                                   void *__restrict__ table, Packer &o, uint32_t accel, VPtr vtab = VPtr())
 {
     static_assert(kVal || !kLinked, "linked frames use the position + word table");
     uint16_t *__restrict__ T = static_cast<uint16_t *>(table);
-    uint64_t *__restrict__ V = static_cast<uint64_t *>(table);
+    VPtr V;
+    if constexpr (std::is_same<VPtr, uint64_t *>::value)
+        V = static_cast<uint64_t *>(table);
+    else
+        V = vtab;
     const uint32_t cap = n - 1;
     uint32_t op = 0, anchor = b0;
     if (n >= 13) {
@@ -430,7 +438,32 @@ last_literals:
 
 // The linked blocks of one frame of n > 64 KiB after its header; returns the
 // bytes written after the header (block words + blocks).
-__device__ uint32_t compress_linked(const uint8_t *__restrict__ s, uint32_t n, uint64_t *__restrict__ table,
+// The frame header through o (magic, FLG, BD, [content size], HC); returns
+// its length.  One independent block up to 64 KiB, linked blocks above.
+__device__ uint32_t frame_header(Packer &o, uint32_t n, bool with_size)
+{
+    uint8_t hdr[15];
+    hdr[0] = 0x04;
+    hdr[1] = 0x22;
+    hdr[2] = 0x4D;
+    hdr[3] = 0x18;
+    hdr[4] = (n > kMaxFrame ? 0x40 : 0x60) | (with_size ? 0x08 : 0);
+    hdr[5] = 0x40;
+    uint32_t hlen = 6;
+    if (with_size) {
+        for (int i = 0; i < 8; i++)
+            hdr[6 + i] = i < 4 ? (uint8_t)(n >> (8 * i)) : 0;
+        hlen = 14;
+    }
+    hdr[hlen] = (uint8_t)(xxh32_short(hdr + 4, hlen - 4) >> 8);
+    hlen++;
+    for (uint32_t i = 0; i < hlen; i++)
+        o.put(hdr[i]);
+    return hlen;
+}
+
+template <typename VPtr>
+__device__ uint32_t compress_linked(const uint8_t *__restrict__ s, uint32_t n, VPtr table,
                                     uint8_t *__restrict__ out, uint32_t hlen, Packer &o, uint32_t accel)
 {
     uint32_t at = hlen;
@@ -438,7 +471,7 @@ __device__ uint32_t compress_linked(const uint8_t *__restrict__ s, uint32_t n, u
         const uint32_t m = min(n - b0, kMaxFrame);
         const Packer save = o;
         o.put4(0);   // block word, patched below
-        uint32_t c = compress_block<8, true, true>(s, b0, m, table, o, accel);
+        uint32_t c = compress_block<8, true, true, VPtr>(s, b0, m, nullptr, o, accel, table);
         if (c == 0) {   // did not fit: raw, the stream already advanced
             o = save;
             o.put4(m | kStoredFlag);
@@ -479,28 +512,11 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_des
         return;
     }
     const uint32_t n = d.src_size;
-    const bool linked = n > kMaxFrame;
-    const bool with_size = (d.flags & ZSK_COMPRESS_CONTENT_SIZE) && n > 0;
-    uint8_t hdr[15];
-    hdr[0] = 0x04;
-    hdr[1] = 0x22;
-    hdr[2] = 0x4D;
-    hdr[3] = 0x18;
-    hdr[4] = (linked ? 0x40 : 0x60) | (with_size ? 0x08 : 0);
-    hdr[5] = 0x40;
-    uint32_t hlen = 6;
-    if (with_size) {
-        for (int i = 0; i < 8; i++)
-            hdr[6 + i] = i < 4 ? (uint8_t)(n >> (8 * i)) : 0;
-        hlen = 14;
-    }
-    hdr[hlen] = (uint8_t)(xxh32_short(hdr + 4, hlen - 4) >> 8);
-    hlen++;
-
+    if (n > kMaxFrame)
+        return;   // linked: lz4_compress_linked_kernel's frame
     uint8_t *out = dst + d.dst_off;
     Packer o{reinterpret_cast<uint32_t *>(out), 0, 0};
-    for (uint32_t i = 0; i < hlen; i++)
-        o.put(hdr[i]);
+    const uint32_t hlen = frame_header(o, n, (d.flags & ZSK_COMPRESS_CONTENT_SIZE) && n > 0);
     if (n == 0) {
         for (int i = 0; i < 4; i++)
             o.put(0);
@@ -509,18 +525,6 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_des
         return;
     }
     uint8_t *const table = tables + (size_t)f * kTable * (kVal ? 8 : 2);
-    if (linked) {
-        if constexpr (kVal) {
-            const uint32_t body = compress_linked(src + d.src_off, n, reinterpret_cast<uint64_t *>(table), out,
-                                                  hlen, o, accel);
-            o.put4(0);   // end mark
-            o.flush();
-            csize[f] = hlen + body + 4;
-        } else {
-            csize[f] = 0;   // (tuning layout only: linked frames need the word table)
-        }
-        return;
-    }
     for (int i = 0; i < 4; i++)   // block word, patched below
         o.put(0);
     const uint32_t c = compress_block<kProbe, kVal>(src + d.src_off, 0, n, table, o, accel);
@@ -538,6 +542,41 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(const zsk_compress_des
     for (int i = 0; i < 4; i++)
         out[hlen + i] = (uint8_t)(c >> (8 * i));
     csize[f] = hlen + 4 + c + 4;
+}
+
+// Linked frames (> 64 KiB): one frame per single-wave workgroup, the stream's
+// 4,096-entry position + word table in LDS (32 KiB: five frames per CU), so a
+// probe batch waits on LDS instead of an HBM round trip (the HBM-table lane
+// ran at ~5 MB/s: 1 GiB of 1 MiB frames in 208 ms).  Lane 0 compresses; the
+// wave zeroes the table first (the stream's fresh state).
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+
+__global__ __launch_bounds__(64) void lz4_compress_linked_kernel(const zsk_compress_desc_t *__restrict__ desc,
+                                                                 uint32_t nframes, const uint8_t *__restrict__ src,
+                                                                 uint8_t *__restrict__ dst,
+                                                                 uint32_t *__restrict__ csize, uint32_t accel)
+{
+    __shared__ __attribute__((aligned(16))) uint64_t tab[1u << kLinkedHashLog];
+    const uint32_t f = blockIdx.x;
+    if (f >= nframes)
+        return;
+    const zsk_compress_desc_t d = desc[f];
+    const uint32_t n = d.src_size;
+    if (n <= kMaxFrame || n > kMaxLinkedFrame || (d.dst_off & 15))
+        return;   // lz4_compress_kernel's frame (or refused there)
+    for (uint32_t i = threadIdx.x; i < (1u << kLinkedHashLog); i += 64)
+        tab[i] = 0;
+    __syncthreads();
+    if (threadIdx.x != 0)
+        return;
+    lds_u64 *const V = (lds_u64 *)(uintptr_t)(uint32_t)(uintptr_t)tab;
+    uint8_t *out = dst + d.dst_off;
+    Packer o{reinterpret_cast<uint32_t *>(out), 0, 0};
+    const uint32_t hlen = frame_header(o, n, (d.flags & ZSK_COMPRESS_CONTENT_SIZE) != 0);
+    const uint32_t body = compress_linked(src + d.src_off, n, V, out, hlen, o, accel);
+    o.put4(0);   // end mark
+    o.flush();
+    csize[f] = hlen + body + 4;
 }
 
 // Raw blocks of the frames lz4_compress_kernel flagged: one wave per frame.
@@ -605,6 +644,8 @@ int launch_lz4_compress(const zsk_compress_desc_t *d_desc, uint32_t nframes, con
     const uint32_t per_wave = min(64u, max(1u, (nframes + waves - 1) / waves));
     hipLaunchKernelGGL(kern, dim3((nframes + per_wave - 1) / per_wave), dim3(64), 0, stream, d_desc, nframes,
                        d_src, d_dst, d_csize, tables, stored, accel, per_wave);
+    hipLaunchKernelGGL(lz4_compress_linked_kernel, dim3(nframes), dim3(64), 0, stream, d_desc, nframes, d_src, d_dst,
+                       d_csize, accel);
     hipLaunchKernelGGL(lz4_store_kernel, dim3((nframes + 3) / 4), dim3(256), 0, stream, d_desc, nframes, d_src,
                        d_dst, stored);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -252,9 +252,22 @@ static bool gpu_queue(zseek_writer *w, const void *src, size_t n, bool with_size
     const size_t slot = ZSK_LZ4_COMPRESS_BOUND(n);
     if (g.failed)
         return gpu_flush(w, errbuf);   // (sets the error)
-    if ((g.in_used + n > g.in_cap || g.out_used + slot > g.out_cap || g.desc.size() == g.max_frames) &&
-        !gpu_flush(w, errbuf))
-        return false;
+    if (g.in_used + n > g.in_cap || g.out_used + slot > g.out_cap || g.desc.size() == g.max_frames) {
+        // a full staging below the batch size doubles after the flush: the
+        // batch then reaches batch_bytes (a flush of linked 1 MiB frames costs
+        // one frame's chain, ~0.1 s, whatever the batch holds)
+        const bool full = g.in_used > 0 && g.in_used + n > g.in_cap && g.in_cap < g.batch_bytes;
+        if (!gpu_flush(w, errbuf))
+            return false;
+        if (full) {
+            DeviceGuard keep;
+            if (hipSetDevice(g.device) != hipSuccess || !g.reserve(g.in_cap + 1)) {
+                g.failed = true;
+                set_error(errbuf, "%s: %s", "compress frame", "GPU staging allocation failed");
+                return false;
+            }
+        }
+    }
     if (g.in_used + n > g.in_cap || g.out_used + slot > g.out_cap) {   // nothing queued: grow
         DeviceGuard keep;
         if (hipSetDevice(g.device) != hipSuccess || !g.reserve(g.in_used + n) || g.out_used + slot > g.out_cap) {

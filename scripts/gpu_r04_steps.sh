@@ -13,3 +13,9 @@ ZSEEK_AMD_LIB=$PWD/libzseek_amd/lib/libzseek_tune.so timeout -k 10 300 python be
 for f in b1 b2; do python3 -c "
 import json; d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1]); r=d['roofline']
 print('$f', d['value'], d['ms_per_step'], {k:v['avg_ms'] for k,v in (r.get('stages') or {}).items()})"; done
+# zstd's execute on the seven-wave 3,072-byte stage against the 4,096 one
+timeout -k 10 400 python bench.py --codec zstd --steps 10 --warmup 3 --no-e2e --no-cpu-baseline --no-verify --no-latency > $O/z1.json 2> $O/z1.err || { tail -5 $O/z1.err; exit 1; }
+ZSEEK_ZSTD_STAGE=3072 timeout -k 10 400 python bench.py --codec zstd --steps 10 --warmup 3 --no-e2e --no-cpu-baseline --no-verify --no-latency > $O/z2.json 2> $O/z2.err || { tail -5 $O/z2.err; exit 1; }
+for f in z1 z2; do python3 -c "
+import json; d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1]); r=d['roofline']
+print('$f', d['value'], d['ms_per_step'])"; done
