@@ -503,7 +503,8 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route)
 
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
-                     hipStream_t stream, SplitScratch *s, int route, int stages, int tune, uint32_t stop_last)
+                     hipStream_t stream, SplitScratch *s, int route, int stages, int tune, uint32_t stop_last,
+                     uint32_t max_dsize)
 {
     if (nframes == 0)
         return 0;
@@ -554,9 +555,24 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                              solo ? total_dev : nullptr);
     }
     stage_mark(2, stream);
-    if (stages & 4)
-        launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                        stream, (tune >> 8) & 0xFFF, blk, stop_last);
+    if (stages & 4) {
+        // the one-frame route executes a frame of <= 64 KiB per workgroup
+        // (env ZSEEK_ONE_EXEC=wave: the wave kernel, as round 3)
+        static const bool wave_exec = [] {
+            const char *v = getenv("ZSEEK_ONE_EXEC");
+            return v && !strcmp(v, "wave");
+        }();
+        if (one && !wave_exec && ((tune >> 8) & 0xFFF) == 0) {
+            launch_seq_exec_frames(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
+                                   stream, stop_last);
+            if (max_dsize > 65536)
+                launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status, stream,
+                                0, blk, stop_last, 65537);
+        } else {
+            launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status, stream,
+                            (tune >> 8) & 0xFFF, blk, stop_last);
+        }
+    }
     stage_mark(3, stream);
     if (hipGetLastError() != hipSuccess) {
         stage_mark(4, stream);

@@ -436,12 +436,14 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     }
     FrameDesc *const h_desc = reinterpret_cast<FrameDesc *>(s.h_comp + doff);
     const FrameDesc *const d_desc = reinterpret_cast<const FrameDesc *>(s.d_comp + doff);
+    uint32_t max_dsize = 0;
     for (size_t i = 0; i < n; i++) {
         FrameDesc &d = h_desc[i];
         d.c_off = st.c_off[f0 + i] - c0;
         d.d_off = st.d_off[f0 + i] - d0;
         d.c_size = (uint32_t)st.csize(f0 + i);
         d.d_size = (uint32_t)st.dsize(f0 + i);
+        max_dsize = std::max(max_dsize, d.d_size);
     }
     s.f0 = f0;
     s.f1 = f1;
@@ -469,7 +471,7 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
                                          s.stream) != 0) {
             e = hipErrorOutOfMemory;
         } else if (launch_lz4_split(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, d_fail,
-                                    s.stream, &s.split, ROUTE_AUTO, 15, 0, stop_last) != 0) {
+                                    s.stream, &s.split, ROUTE_AUTO, 15, 0, stop_last, max_dsize) != 0) {
             e = hipErrorLaunchFailure;
         }
     }

@@ -704,7 +704,8 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
     const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     const int32_t *__restrict__ status, const uint8_t *__restrict__ lit,
     const uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
-    const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, uint32_t stop_last)
+    const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, uint32_t stop_last,
+    uint32_t min_dsize)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kXW * x_wave(OUTB) + (SEG ? kXW * 8 * 65 : 0)];
     const uint32_t lane = threadIdx.x & 63;
@@ -720,6 +721,8 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
     if (fst == ST_NOT_RUN)
         return;
     const FrameDesc d = desc[f];
+    if (d.d_size < min_dsize)
+        return;   // seq_exec_frame_kernel's frame (the one-frame route)
     JobMap<SEG> J;
     uint32_t ispan = 0;   // item slots the resource covers (SEG)
     const uint32_t nit = SEG ? J.init(bfirst, bcount, jobs, jres, f, nitems,
@@ -958,6 +961,176 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
             atomicAdd(&g_xstats[4 + i], (unsigned long long)cnt[i]);
 }
 
+#ifndef ZSK_EXEC_SEG_TU
+// ---- the one-frame route's execute: one frame per 1,024-thread workgroup ----
+// A lone wave executes a 64 KiB frame in ~24 dependent batches (~67 us at a
+// 4 KiB cache-0 read).  Here the frame's whole output is staged in LDS and
+// every thread takes two sequences of a window of 2,048: an exclusive scan
+// over the workgroup places them, literal runs are copied at once, and the
+// matches resolve in rounds -- a match copies once every byte it reads is
+// marked done (a bit per output byte, set after the bytes are written, with
+// release / acquire at workgroup scope), one barrier per round.  The earliest
+// pending match always reads only done bytes, so every round makes progress;
+// the synthetic's match-dependency depth is ~18 per frame (28 at most).
+// Frames of more than 64 KiB decoded go to seq_exec_kernel (min_dsize).
+constexpr uint32_t kFT = 1024;
+constexpr uint32_t kFMax = 65536;
+
+__global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
+    const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
+    const int32_t *__restrict__ status, uint32_t stop_last)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t ob[kFMax + 48];
+    __shared__ uint32_t done[kFMax / 32 + 2];
+    __shared__ uint32_t wsum[kFT / 64];
+    __shared__ uint32_t hi_end;
+    const uint32_t f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (f >= n)
+        return;
+    if (status[f] == ST_NOT_RUN)
+        return;   // the hand-off decodes it
+    const FrameDesc d = desc[f];
+    if (d.d_size > kFMax)
+        return;   // seq_exec_kernel's frame
+    const uint32_t nit = nitems[f];
+    const uint32_t stop = f + 1 == n ? min(stop_last, d.d_size) : d.d_size;
+    const uint64_t *it = items + rec_base[f];
+    const Span lsp = make_span(comp + d.c_off, d.c_size);
+    const uint32_t ob0 = (uint32_t)(uintptr_t)ob;
+    for (uint32_t i = t; i < kFMax / 32 + 2; i += kFT)
+        done[i] = 0;
+    if (t == 0)
+        hi_end = 0;
+    __syncthreads();
+
+    auto scan = [&](uint32_t v, uint32_t &total) -> uint32_t {   // exclusive, in thread order
+        const uint32_t inc = wave_incl_add(v);
+        if (lane == 63)
+            wsum[wv] = inc;
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+        for (uint32_t k = 0; k < kFT / 64; k++) {
+            const uint32_t x = wsum[k];
+            before += k < wv ? x : 0;
+            tot += x;
+        }
+        __syncthreads();
+        total = tot;
+        return before + inc - v;
+    };
+    auto mark = [&](uint32_t a, uint32_t len) {   // output bytes [a, a + len) written
+        for (const uint32_t e = a + len; a < e;) {
+            const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
+            __hip_atomic_fetch_or(&done[a >> 5], nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0, __ATOMIC_RELEASE,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            a += nb;
+        }
+    };
+    auto ready = [&](uint32_t a, uint32_t len) -> bool {
+        for (const uint32_t e = a + len; a < e;) {
+            const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
+            const uint32_t m = nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0;
+            if ((__hip_atomic_load(&done[a >> 5], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & m) != m)
+                return false;
+            a += nb;
+        }
+        return true;
+    };
+
+    uint32_t base_op = 0;
+    for (uint32_t w0 = 0; w0 < nit && base_op < stop; w0 += 2 * kFT) {
+        uint32_t lit[2], ml[2], off[2], src[2], op[2], tot[2];
+        for (int j = 0; j < 2; j++) {
+            const uint32_t i = w0 + j * kFT + t;
+            lit[j] = ml[j] = off[j] = src[j] = 0;
+            if (i < nit) {
+                const uint64_t cur = it[i];
+                const uint32_t c0 = (uint32_t)cur, c1 = (uint32_t)(cur >> 32);
+                const bool second = i > 0 && ((uint32_t)it[i - 1] & kItemExt);   // an extended item's second half
+                if (!second) {
+                    src[j] = c0 & kItemPos;
+                    if (c0 & kItemExt) {
+                        const uint64_t nx = it[i + 1];
+                        lit[j] = (uint32_t)nx;
+                        ml[j] = (uint32_t)(nx >> 32);
+                        off[j] = c1;
+                    } else {
+                        lit[j] = (c1 >> 16) & 0xFF;
+                        const uint32_t mc = c1 >> 24;
+                        ml[j] = mc ? mc + 3 : 0;
+                        off[j] = c1 & 0xFFFF;
+                    }
+                }
+            }
+        }
+        const uint32_t x0 = scan(lit[0] + ml[0], tot[0]);
+        const uint32_t x1 = scan(lit[1] + ml[1], tot[1]);
+        op[0] = base_op + x0;
+        op[1] = base_op + tot[0] + x1;
+        bool pend[2];
+        for (int j = 0; j < 2; j++) {
+            const bool on = op[j] < stop && lit[j] + ml[j] != 0;
+            if (on && lit[j]) {
+                for (uint32_t k = 0; k < lit[j]; k += 16)
+                    lds_put(ob0 + op[j] + k, load16u(lsp.r, lsp.s0 + src[j] + k), min(16u, lit[j] - k));
+                mark(op[j], lit[j]);
+            }
+            pend[j] = on && ml[j] != 0;
+            if (on)
+                atomicMax(&hi_end, op[j] + lit[j] + ml[j]);
+        }
+        __syncthreads();
+        for (;;) {
+            for (int j = 0; j < 2; j++) {
+                if (!pend[j])
+                    continue;
+                const uint32_t mb = op[j] + lit[j], o = off[j], m = ml[j];
+                if (!ready(mb - o, o >= m ? m : o))
+                    continue;
+                if (o >= m) {   // source and destination apart: pieces in any order
+                    for (uint32_t k = 0; k < m; k += 16)
+                        lds_put(ob0 + mb + k, lds16(ob0 + mb - o + k), min(16u, m - k));
+                } else {
+                    // overlapping: the first e = o * ceil(16 / o) bytes one at a
+                    // time, then 16-byte pieces trailing by e (each reads bytes
+                    // an earlier step of this thread wrote)
+                    const uint32_t e = o >= 16 ? o : o * ((16 + o - 1) / o);
+                    const uint32_t h = o >= 16 ? 0 : min(e, m);
+                    for (uint32_t k = 0; k < h; k++) {
+                        ob[mb + k] = ob[mb - o + k];
+                        wave_lds_sync();
+                    }
+                    for (uint32_t k = h; k < m; k += 16) {
+                        lds_put(ob0 + mb + k, lds16(ob0 + mb + k - e), min(16u, m - k));
+                        wave_lds_sync();
+                    }
+                }
+                mark(mb, m);
+                pend[j] = false;
+            }
+            if (!__syncthreads_or(pend[0] || pend[1]))
+                break;
+        }
+        base_op += tot[0] + tot[1];
+    }
+    __syncthreads();
+    // the decoded bytes [0, hi_end) out: a byte head to 16-byte alignment,
+    // whole 16-byte stores, a byte tail
+    const uint32_t E = min(hi_end, d.d_size);
+    uint8_t *o = out + d.d_off;
+    const uint32_t head = min(E, (uint32_t)((16 - ((uintptr_t)o & 15)) & 15));
+    if (t < head)
+        o[t] = ob[t];
+    const uint32_t nchunks = (E - head) / 16;
+    for (uint32_t c = t; c < nchunks; c += kFT)
+        *reinterpret_cast<u32x4 *>(o + head + 16 * c) = lds16(ob0 + head + 16 * c);
+    const uint32_t tail0 = head + 16 * nchunks;
+    if (tail0 + t < E)
+        o[tail0 + t] = ob[tail0 + t];
+}
+#endif
+
 }   // namespace
 
 #ifdef ZSK_EXEC_SEG_TU
@@ -971,7 +1144,7 @@ int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
         return 0;
     hipLaunchKernelGGL((seq_exec_kernel<0, 4096, true>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0, stream,
                        d_desc, nframes, d_comp, d_out, rec_base, items, nitems, d_status, nullptr, blk->bfirst,
-                       blk->bcount, blk->jobs, blk->jres, 0xFFFFFFFFu);
+                       blk->bcount, blk->jobs, blk->jres, 0xFFFFFFFFu, 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #else
@@ -980,7 +1153,7 @@ int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                    int version, const SplitScratch *blk, uint32_t stop_last)
+                    int version, const SplitScratch *blk, uint32_t stop_last, uint32_t min_dsize)
 {
     if (nframes == 0)
         return 0;
@@ -989,7 +1162,8 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     const dim3 grid((nframes + kXW - 1) / kXW), block(64 * kXW);
 #define ZSK_X(D)                                                                                               \
     hipLaunchKernelGGL((seq_exec_kernel<D, kExecStage, false>), grid, block, 0, stream, d_desc, nframes, d_comp, \
-                       d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr, stop_last)
+                       d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr, stop_last, \
+                       min_dsize)
 #ifdef ZSK_TUNING
     switch (version) {
     case 0x101: ZSK_X(1); break;
@@ -1001,17 +1175,17 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x141:   // the 4,096-byte stage: five waves per SIMD
         hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), grid, block, 0, stream, d_desc, nframes, d_comp,
                            d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           stop_last);
+                           stop_last, min_dsize);
         break;
     case 0x142:   // the 3,584-byte stage, six waves per SIMD
         hipLaunchKernelGGL((seq_exec_kernel<0, 3584, false>), grid, block, 0, stream, d_desc, nframes, d_comp,
                            d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           stop_last);
+                           stop_last, min_dsize);
         break;
     case 0x143:   // a 2,560-byte stage, eight waves per SIMD (64 VGPRs: spills)
         hipLaunchKernelGGL((seq_exec_kernel<0, 2560, false>), grid, block, 0, stream, d_desc, nframes, d_comp,
                            d_out, rec_base, items, nitems, d_status, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           stop_last);
+                           stop_last, min_dsize);
         break;
     case 0x1C0: ZSK_X(192); break;
     case 0x301: ZSK_X(256); break;    // rounds without copy_round
@@ -1047,6 +1221,17 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                           const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
+                           const int32_t *d_status, hipStream_t stream, uint32_t stop_last)
+{
+    if (nframes == 0)
+        return 0;
+    hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
+                       rec_base, items, nitems, d_status, stop_last);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *lit,
                         uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                         const uint32_t *nitems, const int32_t *d_status, hipStream_t stream)
@@ -1055,7 +1240,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
         return 0;
     hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit, nullptr,
-                       nullptr, nullptr, nullptr, 0xFFFFFFFFu);
+                       nullptr, nullptr, nullptr, 0xFFFFFFFFu, 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -153,7 +153,9 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route = ROU
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                      hipStream_t stream, SplitScratch *s, int route = ROUTE_AUTO, int stages = 15,
-                     int tune = 0, uint32_t stop_last = 0xFFFFFFFFu);
+                     int tune = 0, uint32_t stop_last = 0xFFFFFFFFu, uint32_t max_dsize = 0xFFFFFFFFu);
+// (max_dsize: the batch's largest decoded frame when the caller knows it --
+// the one-frame route then skips the wave execute for frames of <= 64 KiB)
 
 // Item slots of a frame in the split decoder's scratch.  An item is 8 bytes;
 // a sequence takes one (two when extended), a stored block two.  LZ4 data
@@ -195,7 +197,14 @@ int lz4_pick_engine(uint32_t nframes);   // never ENGINE_AUTO
 int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                     uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                     const uint32_t *nitems, const int32_t *d_status, hipStream_t stream,
-                    int version = 0, const SplitScratch *blk = nullptr, uint32_t stop_last = 0xFFFFFFFFu);
+                    int version = 0, const SplitScratch *blk = nullptr, uint32_t stop_last = 0xFFFFFFFFu,
+                    uint32_t min_dsize = 0);
+// The one-frame route's execute (seq_exec.hip): one frame of <= 64 KiB
+// decoded per 1,024-thread workgroup, output staged whole in LDS; bigger
+// frames are left to launch_seq_exec(..., min_dsize = 65537).
+int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                           const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
+                           const int32_t *d_status, hipStream_t stream, uint32_t stop_last);
 int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         const int32_t *d_status, hipStream_t stream, const SplitScratch *blk);
