@@ -277,6 +277,12 @@ __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B
 // lane's total through pass 2 minus the record at its entry -- no count pass
 // (a lane whose entry is past its records counts as before).
 constexpr uint32_t kRec = 64;
+// The one-frame route parses over all kOneWaves waves of its workgroup: lane
+// j of 256 takes chunk j (at least kOneMinChunk bytes), kOneRec records each
+constexpr uint32_t kOneLanes = 256;
+constexpr uint32_t kOneMinChunk = 128;
+constexpr uint32_t kOneRec = 32;
+constexpr uint32_t kOneMapW = 4;   // map dwords per lane: a 128-bit chunk prefix
 
 #ifdef ZSK_TUNING
 // tuning builds: the one-frame route's phase cycles ([0] staging, [1]
@@ -304,24 +310,61 @@ __device__ unsigned long long g_ctime[16];
 
 // One compressed block over the wave.  Returns -1 (block done: *op and *k
 // advanced) or a frame status.
+// ONE: the workgroup's kOneLanes lanes (lane = thread index) take the block,
+// the wave-wide steps (owners, scans, the first failure) going through LDS
+// scratch at `coll` (3 x 256 + 16 words) with workgroup barriers.
 template <bool ONE>
 __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane, uint32_t mapbase,
-                               uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op, uint32_t recbase)
+                               uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op, uint32_t recbase,
+                               uint32_t coll)
 {
+    constexpr uint32_t NL = ONE ? kOneLanes : 64;
+    constexpr uint32_t kR = ONE ? kOneRec : kRec;
     const uint32_t bsize = B.iend - B.ib;
-    // chunking: C bytes per lane (>= kMinChunk), nl lanes
-    uint32_t C = (bsize + 63) / 64;
-    C = C < kMinChunk ? kMinChunk : (C + 3) & ~3u;
+    // chunking: C bytes per lane (>= the minimum chunk), nl lanes
+    uint32_t C = (bsize + NL - 1) / NL;
+    C = C < (ONE ? kOneMinChunk : kMinChunk) ? (ONE ? kOneMinChunk : kMinChunk) : (C + 3) & ~3u;
     const uint32_t nl = (bsize + C - 1) / C;
+    // LDS scratch of the ONE route's workgroup steps
+    auto cw = [&](uint32_t i) { return lp<uint32_t>(coll + 4 * i); };   // word i
+    constexpr uint32_t cY = 0, cN = 256, cE = 512, cWS = 768, cM = 776, cBad = 777, cFirst = 778;
+    auto sync = [&]() {
+        if constexpr (ONE)
+            __syncthreads();
+        else
+            wave_lds_sync();
+    };
+    // inclusive sum over the NL lanes, and the total
+    auto scan = [&](uint32_t v, uint32_t &total) -> uint32_t {
+        const uint32_t inc = wave_incl_add(v);
+        if constexpr (!ONE) {
+            total = lane_val(inc, 63);
+            return inc;
+        } else {
+            if ((lane & 63) == 63)
+                *cw(cWS + (lane >> 6)) = inc;
+            __syncthreads();
+            uint32_t before = 0, tot = 0;
+            for (uint32_t q = 0; q < NL / 64; q++) {
+                const uint32_t x = *cw(cWS + q);
+                before += q < (lane >> 6) ? x : 0;
+                tot += x;
+            }
+            __syncthreads();
+            total = tot;
+            return before + inc;
+        }
+    };
     const uint32_t s = B.ib + lane * C;
     const uint32_t t = s + C < B.iend ? s + C : B.iend;
     const bool act = lane < nl;
-    const uint32_t mlen = C < kMap ? C : kMap;
-    const uint32_t mymap = mapbase + lane * (kMapW * 4);
+    constexpr uint32_t MW = ONE ? kOneMapW : kMapW;   // map dwords per lane
+    const uint32_t mlen = C < 32 * MW ? C : 32 * MW;
+    const uint32_t mymap = mapbase + lane * (MW * 4);
 
     uint32_t entry = kNone, y = B.iend;
     uint32_t tout = 0, tnit = 0, nrec = 0;   // ONE: counts from s through pass 2, records
-    const uint32_t myrec = recbase + lane * (kRec * 8);
+    const uint32_t myrec = recbase + lane * (kR * 8);
 #ifdef ZSK_TUNING
     uint64_t tmark_ = __builtin_readcyclecounter();
     uint32_t n1_ = 0, n2_ = 0;
@@ -331,9 +374,9 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
     } else {
         // pass 1: speculate over the own chunk, marking visited tokens
 #pragma unroll
-        for (uint32_t i = 0; i < kMapW; i += 4)
+        for (uint32_t i = 0; i < MW; i += 4)
             *lp<u32x4>(mymap + 4 * i) = (u32x4){0, 0, 0, 0};
-        wave_lds_sync();
+        sync();
         uint32_t p = s;
         if (act) {
             while (p < t) {
@@ -341,7 +384,7 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
                 if (r < mlen)
                     __hip_atomic_fetch_or(lp<uint32_t>(mymap + 4 * (r >> 5)), 1u << (r & 31),
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                if (ONE && r < mlen && nrec < kRec) {
+                if (ONE && r < mlen && nrec < kR) {
                     *lp<uint64_t>(myrec + 8 * nrec) = ((uint64_t)tout << 32) | (tnit << 16) | r;
                     nrec++;
                 }
@@ -351,14 +394,14 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
 #endif
             }
         }
-        wave_lds_sync();
+        sync();
         ZSK_CT(2)
         // pass 2: continue to the first position another lane visited
         if (act) {
             while (p < B.iend) {
                 const uint32_t c = (p - B.ib) / C;
                 const uint32_t r = p - (B.ib + c * C);
-                if (r < mlen && ((*lp<uint32_t>(mapbase + c * (kMapW * 4) + 4 * (r >> 5)) >> (r & 31)) & 1))
+                if (r < mlen && ((*lp<uint32_t>(mapbase + c * (MW * 4) + 4 * (r >> 5)) >> (r & 31)) & 1))
                     break;
                 skel(S, W, p, B.iend, tout, tnit);
 #ifdef ZSK_TUNING
@@ -368,27 +411,82 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
         }
         y = p;
         // owners: lane j's successor is the lane whose chunk holds y_j
-        const uint32_t nxt = act ? (y >= B.iend ? 64u : (y - B.ib) / C) : 64u;
-        const uint64_t ends = __ballot(act && nxt == 64);
-        const uint32_t m = (uint32_t)__builtin_ctzll(ends | (1ull << 63));   // first lane ending the block
-        const uint64_t bad = __ballot(lane < m && nxt != lane + 1);
-        if (bad == 0 && (ends >> m) & 1) {
-            // the usual case: lanes 0..m, each starting where the previous stops
-            const uint32_t yp = dpp_prev(y, B.ib);
-            entry = lane <= m ? (lane == 0 ? B.ib : yp) : kNone;
-        } else {
-            // follow the owner chain from lane 0
-            uint32_t j = 0, x = B.ib;
-            for (;;) {
-                if (lane == j)
-                    entry = x;
-                const uint32_t yj = lane_val(y, (int)j);
-                const uint32_t nj = lane_val(nxt, (int)j);
-                if (nj >= 64)
-                    break;
-                x = yj;
-                j = nj;
+        const uint32_t nxt = act ? (y >= B.iend ? NL : (y - B.ib) / C) : NL;
+        if constexpr (!ONE) {
+            const uint64_t ends = __ballot(act && nxt == 64);
+            const uint32_t m = (uint32_t)__builtin_ctzll(ends | (1ull << 63));   // first lane ending the block
+            const uint64_t bad = __ballot(lane < m && nxt != lane + 1);
+            if (bad == 0 && (ends >> m) & 1) {
+                // the usual case: lanes 0..m, each starting where the previous stops
+                const uint32_t yp = dpp_prev(y, B.ib);
+                entry = lane <= m ? (lane == 0 ? B.ib : yp) : kNone;
+            } else {
+                // follow the owner chain from lane 0
+                uint32_t j = 0, x = B.ib;
+                for (;;) {
+                    if (lane == j)
+                        entry = x;
+                    const uint32_t yj = lane_val(y, (int)j);
+                    const uint32_t nj = lane_val(nxt, (int)j);
+                    if (nj >= 64)
+                        break;
+                    x = yj;
+                    j = nj;
+                }
             }
+        } else {
+            // the same over the workgroup: y and successors in LDS, the first
+            // lane ending the block by atomicMin, any break in 0..m by atomicOr
+            *cw(cY + lane) = y;
+            *cw(cN + lane) = nxt;
+            *cw(cE + lane) = kNone;
+            if (lane == 0) {
+                *cw(cM) = NL;
+                *cw(cBad) = 0;
+            }
+            __syncthreads();
+            if (act && nxt == NL)
+                __hip_atomic_fetch_min(cw(cM), lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __syncthreads();
+            const uint32_t m = *cw(cM);
+            if (lane < m && nxt != lane + 1)
+                __hip_atomic_fetch_or(cw(cBad), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __syncthreads();
+            if (*cw(cBad) == 0 && m < NL) {
+                entry = lane <= m ? (lane == 0 ? B.ib : *cw(cY + lane - 1)) : kNone;
+            } else {
+                // the owner chain from lane 0 by pointer jumping (successors
+                // only increase): J_r = 2^r successor steps; a lane on the
+                // chain at distance d marks the lane at d + 2^r, top bit
+                // first, so every distance is reached; then each chain lane
+                // gives its successor the entry it stopped at
+                uint32_t J[8];
+                J[0] = nxt;
+                for (int r = 1; r < 8; r++) {
+                    *cw(cE + lane) = J[r - 1];
+                    __syncthreads();
+                    J[r] = J[r - 1] < NL ? *cw(cE + J[r - 1]) : NL;
+                    __syncthreads();
+                }
+                *cw(cE + lane) = lane == 0 ? 1u : 0u;   // on the chain
+                __syncthreads();
+                for (int r = 7; r >= 0; r--) {
+                    const bool on = *cw(cE + lane) != 0;
+                    __syncthreads();
+                    if (on && J[r] < NL)
+                        *cw(cE + J[r]) = 1u;
+                    __syncthreads();
+                }
+                const bool on = *cw(cE + lane) != 0;
+                __syncthreads();
+                *cw(cE + lane) = lane == 0 ? B.ib : kNone;
+                __syncthreads();
+                if (on && nxt < NL)
+                    *cw(cE + nxt) = y;
+                __syncthreads();
+                entry = *cw(cE + lane);
+            }
+            __syncthreads();
         }
     }
     ZSK_CT(3)
@@ -422,8 +520,8 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
             skel(S, W, p, B.iend, out, nit);
     }
     ZSK_CT(4)
-    const uint32_t oinc = wave_incl_add(out), kinc = wave_incl_add(nit);
-    const uint32_t ktot = lane_val(kinc, 63);
+    uint32_t otot, ktot;
+    const uint32_t oinc = scan(out, otot), kinc = scan(nit, ktot);
     if (k + ktot > cap)
         return ST_NOT_RUN;
     // emit: the validated parse, items in place
@@ -437,12 +535,28 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
     if (ONE && lane == 0)
         atomicAdd(&g_ctime[12], 1ull);
 #endif
-    const uint64_t fails = __ballot(st >= 0);
-    if (fails) {
-        const int32_t fs = (int32_t)lane_val((uint32_t)st, __builtin_ctzll(fails));
-        return fs;
+    if constexpr (!ONE) {
+        const uint64_t fails = __ballot(st >= 0);
+        if (fails) {
+            const int32_t fs = (int32_t)lane_val((uint32_t)st, __builtin_ctzll(fails));
+            return fs;
+        }
+    } else {
+        // the first failing lane's status (lane order = block order)
+        if (lane == 0)
+            *cw(cFirst) = NL;
+        *cw(cE + lane) = (uint32_t)st;
+        __syncthreads();
+        if (st >= 0)
+            __hip_atomic_fetch_min(cw(cFirst), lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        const uint32_t first = *cw(cFirst);
+        const int32_t fs = first < NL ? (int32_t)*cw(cE + first) : -1;
+        __syncthreads();
+        if (first < NL)
+            return fs;
     }
-    op += lane_val(oinc, 63);
+    op += otot;
     k += ktot;
     return -1;
 }
@@ -485,11 +599,12 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
     const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, const uint32_t *__restrict__ njobs,
     uint32_t min_jobs, uint64_t *__restrict__ solo_total, uint32_t per_wave)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t maps[kCW * 64 * kMapW];
+    __shared__ __attribute__((aligned(16))) uint32_t maps[ONE ? kOneLanes * kOneMapW : kCW * 64 * kMapW];
     __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
     __shared__ __attribute__((aligned(16))) u32x4 stage[ONE ? kOneStage / 16 : 1];
-    __shared__ __attribute__((aligned(16))) uint64_t recs[ONE ? 64 * kRec : 1];
-    const uint32_t lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) uint64_t recs[ONE ? kOneLanes * kOneRec : 1];
+    __shared__ uint32_t coll[ONE ? 3 * 256 + 16 : 1];
+    const uint32_t lane = ONE ? threadIdx.x : threadIdx.x & 63;   // ONE: the workgroup's lanes
     const uint32_t w = ONE ? 0 : threadIdx.x >> 6;
     // one frame (wave-uniform f); a return ends that frame
     auto frame = [&](const uint32_t f) {
@@ -520,8 +635,6 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
             }
         }
         __syncthreads();
-        if (threadIdx.x >= 64)
-            return;
         // a batch of one frame launches no plan kernel (solo_total != null):
         // its slots start at 0 and the total the plan would report is this
         // frame's; status and fail_at are written below whatever happens
@@ -703,7 +816,8 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
                 break;
             }
             const int32_t bs =
-                chunk_block<ONE>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs);
+                chunk_block<ONE>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
+                                 (uint32_t)(uintptr_t)coll);
             if (bs == ST_BLOCK_ERR)
                 st = block_fail(B, bsid, max_block);
             else if (bs >= 0)
