@@ -604,7 +604,7 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
     }
     // the item(s) into the lane's buffer (slots k, k + 1 mod 32): after the
     // handed-over line was read
-    {
+    auto put_items = [&]() {
         const uint32_t ibuf = L.ring + kIBuf;
         const uint32_t a0 = L.nk ? ibuf + 8 * (L.k & 31) : L.ring + kSink;
         const uint32_t a1 = L.nk == 2 ? ibuf + 8 * ((L.k + 1) & 31) : L.ring + kSink + 8;
@@ -612,6 +612,15 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
         *lp<uint64_t>(a1) = ((uint64_t)L.ib2 << 32) | L.ia2;
         L.k += L.nk;
         L.nk = 0;
+    };
+    put_items();
+    if (!(DIAG & 32)) {
+        // a second sequence in the same sub-step when its bytes are in the
+        // ring: the fill, flush and loop work then serve two (config 2, plan +
+        // parse: 1.085 -> 1.032 ms; DIAG 32, tuning: one sequence, as round 3)
+        u32x4 dv;
+        (void)fast(L, L.ring + kSink, 0, dv);
+        put_items();
     }
     wave_lds_sync();
     fcnt = flush_hand(L, tab);
@@ -640,7 +649,9 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
 }
 
 // DIAG (tuning builds): 1 = no line stores, 2 = every line to the wave's first line,
-// 4 = sub-step outcome counters (printed), 8 / 16 = a 4- / 1-deep fill pipeline
+// 4 = sub-step outcome counters (printed), 8 / 16 = a 4- / 1-deep fill pipeline,
+// 32 = one sequence per sub-step (round 3), 64 = every sub-step fills (D = 4:
+// 1.260 ms against 1.085, not kept)
 // (default 2: at ~1,400 cycles per sub-step, 4 sub-steps cover the loads)
 // D: fill pipeline depth (slots of up to 64 bytes, retired every other sub-step)
 // BLK: the block route -- lane t parses job t of `jobs` (one LZ4 block from
@@ -768,11 +779,21 @@ __global__ __launch_bounds__(64 * kLW) __attribute__((amdgpu_waves_per_eu(1, 1))
     wave_lds_sync();
     for (;;) {
         // two sub-steps per slot: the first retires and refills it, the
-        // second may run the exact step
+        // second may run the exact step (DIAG 64, tuning: every sub-step
+        // retires and refills its own slot, every other one may run the exact
+        // step -- twice the fill rate at the same latency budget with D = 4)
+        if (DIAG & 64) {
 #pragma unroll
-        for (int i = 0; i < D; i++) {
-            sub<false, true, DIAG>(L, sl[i], lane, tab, fcnt);
-            sub<true, false, DIAG>(L, sl[i], lane, tab, fcnt);
+            for (int i = 0; i < D; i += 2) {
+                sub<false, true, DIAG>(L, sl[i], lane, tab, fcnt);
+                sub<true, true, DIAG>(L, sl[i + 1], lane, tab, fcnt);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < D; i++) {
+                sub<false, true, DIAG>(L, sl[i], lane, tab, fcnt);
+                sub<true, false, DIAG>(L, sl[i], lane, tab, fcnt);
+            }
         }
         const bool busy = L.ph != P_DONE;
         if (!__any(busy))
@@ -845,7 +866,13 @@ int launch_lz4_lean(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                         "phase %.1f; by phase TOKEN %.1f LEXT %.1f OFF %.1f MEXT %.1f BHDR %.1f END %.1f DONE %.1f\n",
                 z[6] / fr, z[7] / fr, z[8] / fr, z[9] / fr, z[10] / fr, z[11] / fr, z[12] / fr, z[13] / fr, z[14] / fr,
                 z[15] / fr, z[16] / fr, z[17] / fr, z[18] / fr, z[19] / fr, z[20] / fr, z[21] / fr);
-    } else if (diag & 2)
+    } else if ((diag & 96) == 96)
+        ZSK_LEAN(96, 4);
+    else if (diag & 64)
+        ZSK_LEAN(64, 4);
+    else if (diag & 32)
+        ZSK_LEAN(32, 2);
+    else if (diag & 2)
         ZSK_LEAN(2, 2);
     else if (diag & 1)
         ZSK_LEAN(1, 2);
