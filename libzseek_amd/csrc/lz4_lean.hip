@@ -651,7 +651,8 @@ __device__ __forceinline__ void sub(Lane &L, Fill &S, uint32_t lane, uint32_t ta
 // DIAG (tuning builds): 1 = no line stores, 2 = every line to the wave's first line,
 // 4 = sub-step outcome counters (printed), 8 / 16 = a 4- / 1-deep fill pipeline,
 // 32 = one sequence per sub-step (round 3), 64 = every sub-step fills (D = 4:
-// 1.260 ms against 1.085, not kept)
+// 1.260 ms against 1.085, not kept); a third sequence per sub-step measured
+// 1.265 against 1.031 (removed)
 // (default 2: at ~1,400 cycles per sub-step, 4 sub-steps cover the loads)
 // D: fill pipeline depth (slots of up to 64 bytes, retired every other sub-step)
 // BLK: the block route -- lane t parses job t of `jobs` (one LZ4 block from

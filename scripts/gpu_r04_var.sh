@@ -6,5 +6,5 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r04var
 mkdir -p $O
-timeout -k 10 300 python scripts/kbench.py --variants 12,544,576,608 --rounds 5 > $O/kb.log 2>&1 || { tail -20 $O/kb.log; exit 1; }
+timeout -k 10 300 python scripts/kbench.py --variants 12,640,704 --rounds 5 > $O/kb.log 2>&1 || { tail -20 $O/kb.log; exit 1; }
 grep -v amdgpu.ids $O/kb.log | grep "median\|MISMATCH\|bit-exact"
