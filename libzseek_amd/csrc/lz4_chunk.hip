@@ -316,7 +316,7 @@ __device__ unsigned long long g_ctime[16];
 template <bool ONE>
 __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane, uint32_t mapbase,
                                uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op, uint32_t recbase,
-                               uint32_t coll)
+                               uint32_t coll, uint32_t lead)
 {
     constexpr uint32_t NL = ONE ? kOneLanes : 64;
     constexpr uint32_t kR = ONE ? kOneRec : kRec;
@@ -377,7 +377,10 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
         for (uint32_t i = 0; i < MW; i += 4)
             *lp<u32x4>(mymap + 4 * i) = (u32x4){0, 0, 0, 0};
         sync();
-        uint32_t p = s;
+        // (ONE) pass 1 starts `lead` bytes before the chunk, so its chain has
+        // usually met the true one when it enters the chunk and pass 2's join
+        // after the chunk is short; the lead-in marks and records nothing
+        uint32_t p = (ONE && lane > 0) ? (s - B.ib > lead ? s - lead : B.ib) : s;
         if (act) {
             while (p < t) {
                 const uint32_t r = p - s;
@@ -597,7 +600,7 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
     uint32_t min_csize, uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount,
     const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, const uint32_t *__restrict__ njobs,
-    uint32_t min_jobs, uint64_t *__restrict__ solo_total, uint32_t per_wave)
+    uint32_t min_jobs, uint64_t *__restrict__ solo_total, uint32_t per_wave, uint32_t lead)
 {
     __shared__ __attribute__((aligned(16))) uint32_t maps[ONE ? kOneLanes * kOneMapW : kCW * 64 * kMapW];
     __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
@@ -817,7 +820,7 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
             }
             const int32_t bs =
                 chunk_block<ONE>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
-                                 (uint32_t)(uintptr_t)coll);
+                                 (uint32_t)(uintptr_t)coll, lead);
             if (bs == ST_BLOCK_ERR)
                 st = block_fail(B, bsid, max_block);
             else if (bs >= 0)
@@ -855,6 +858,18 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
 
 }   // namespace
 
+// the one-frame parse's lead-in (bytes before each chunk): env ZSEEK_ONE_LEAD
+// (tuning), default kOneLead
+constexpr uint32_t kOneLead = 64;
+uint32_t one_lead()
+{
+    static const uint32_t v = [] {
+        const char *e = getenv("ZSEEK_ONE_LEAD");
+        return e ? (uint32_t)atoi(e) : kOneLead;
+    }();
+    return v;
+}
+
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
@@ -865,7 +880,8 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     if (one) {
         hipLaunchKernelGGL(lz4_chunk_kernel<true>, dim3(nframes), dim3(64 * kOneWaves), 0, stream, d_desc, nframes,
                            d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u);
+                           nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u,
+                           one_lead());
 #ifdef ZSK_TUNING
         if (getenv("ZSEEK_CHUNK_TIMERS")) {
             unsigned long long z[16];
@@ -896,7 +912,7 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                            d_desc, nframes, d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at,
                            min_csize, blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr,
                            blk ? blk->jobs : nullptr, blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr,
-                           min_jobs, nullptr, per);
+                           min_jobs, nullptr, per, 0u);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
