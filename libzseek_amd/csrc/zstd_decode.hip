@@ -1770,6 +1770,13 @@ __device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 // cell loaded one sequence ahead; the others are staged in LDS.  More tables
 // from the slot lose: OF + ML (288 cells, eight workgroups per CU) 4.71 ms
 // alone, all three 6.45 ms, against 2.43 (pipeline 9.70 / 10.15 vs 9.26).
+// Round 4: the bitstream through a per-lane LDS ring (64 dwords, refilled 4
+// per sequence two sequences ahead, so the window is an LDS read and no load
+// is waited on per sequence) loses -- the loop is issue-bound, not waiting on
+// the window: same-box config 5, 3 chunks, 8.52 ms as here against 9.18 / 9.45
+// with the ring beside these tables, 10.9 with the ring and all three tables in
+// LDS (11.2 at 64 frames per wave); 4 chunks 8.85 against 9.05 / 10.6
+// (profiles/r04_zstd_ring_ab.txt; the variant since removed).
 constexpr uint32_t kSeqLanes = 32;
 constexpr uint32_t kSeqCells = 544;   // u16 cells per frame (LL + ML 512 + copy slack)
 constexpr uint32_t kSeqGm = 2;        // OF from the slot
