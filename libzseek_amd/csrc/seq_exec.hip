@@ -976,13 +976,36 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
 // Frames of more than 64 KiB decoded go to seq_exec_kernel (min_dsize).
 constexpr uint32_t kFT = 1024;
 constexpr uint32_t kFMax = 65536;
+constexpr uint32_t kFCStage = 65536;   // compressed bytes staged in LDS (literal source)
+constexpr uint32_t kFLong = 128;       // literal runs longer than this: copied by the whole wave
+
+#ifdef ZSK_TUNING
+// tuning builds: the one-frame execute's phase cycles (thread 0, at the
+// workgroup barriers): [0] staging + init, [1] items + scans, [2] literal
+// runs, [3] match passes, [4] output; [5] windows, [6] sum over waves of
+// their pass counts, [7] frames; printed under ZSEEK_FRAME_TIMERS
+__device__ unsigned long long g_ftime[8];
+__device__ uint32_t g_fdiag;   // ZSEEK_FRAME_DIAG: 1 no literal copies, 2 no literal marks, 4 no matches
+#define ZSK_FD(b) ((__builtin_amdgcn_readfirstlane(g_fdiag) & (b)) != 0)
+#define ZSK_FT(i)                                                             \
+    {                                                                         \
+        const uint64_t tn_ = __builtin_readcyclecounter();                    \
+        if (t == 0)                                                           \
+            atomicAdd(&g_ftime[i], (unsigned long long)(tn_ - tmark_));       \
+        tmark_ = tn_;                                                         \
+    }
+#else
+#define ZSK_FD(b) false
+#define ZSK_FT(i)
+#endif
 
 __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     const int32_t *__restrict__ status, uint32_t stop_last)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t ob[kFMax + 48];
+    __shared__ __attribute__((aligned(16))) uint8_t ob[kFMax + 80];
+    __shared__ __attribute__((aligned(16))) uint8_t cs[kFCStage + 80];
     __shared__ uint32_t done[kFMax / 32 + 2];
     __shared__ uint32_t wsum[kFT / 64];
     __shared__ uint32_t hi_end;
@@ -998,12 +1021,37 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const uint32_t stop = f + 1 == n ? min(stop_last, d.d_size) : d.d_size;
     const uint64_t *it = items + rec_base[f];
     const Span lsp = make_span(comp + d.c_off, d.c_size);
-    const uint32_t ob0 = (uint32_t)(uintptr_t)ob;
+    const uint32_t ob0 = (uint32_t)(uintptr_t)ob, cs0 = (uint32_t)(uintptr_t)cs;
+#ifdef ZSK_TUNING
+    uint64_t tmark_ = __builtin_readcyclecounter();
+    if (t == 0)
+        atomicAdd(&g_ftime[7], 1ull);
+#endif
+    // the compressed frame into LDS (four 16-byte loads per thread issued
+    // together), so a literal run is copied LDS to LDS instead of waiting on an
+    // L2 / HBM load per 16 bytes; a frame too big for the stage reads HBM
+    const bool staged = d.c_size <= kFCStage;
+    if (staged) {
+        const uint32_t np = (d.c_size + 15) / 16;
+        u32x4 v[kFCStage / 16 / kFT];
+#pragma unroll
+        for (uint32_t q = 0; q < kFCStage / 16 / kFT; q++) {
+            const uint32_t i = t + q * kFT;
+            v[q] = load16u(lsp.r, i < np ? lsp.s0 + 16 * i : kBad);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kFCStage / 16 / kFT; q++) {
+            const uint32_t i = t + q * kFT;
+            if (i < np)
+                *lp<u32x4>(cs0 + 16 * i) = v[q];
+        }
+    }
     for (uint32_t i = t; i < kFMax / 32 + 2; i += kFT)
         done[i] = 0;
     if (t == 0)
         hi_end = 0;
     __syncthreads();
+    ZSK_FT(0)
 
     auto scan = [&](uint32_t v, uint32_t &total) -> uint32_t {   // exclusive, in thread order
         const uint32_t inc = wave_incl_add(v);
@@ -1020,23 +1068,46 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
         total = tot;
         return before + inc - v;
     };
+    // one release fence, then relaxed bit sets; readiness: relaxed reads of
+    // every word (no early exit, so they are in flight together), one acquire
+    // fence once all are set
     auto mark = [&](uint32_t a, uint32_t len) {   // output bytes [a, a + len) written
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         for (const uint32_t e = a + len; a < e;) {
             const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
-            __hip_atomic_fetch_or(&done[a >> 5], nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0, __ATOMIC_RELEASE,
+            __hip_atomic_fetch_or(&done[a >> 5], nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_WORKGROUP);
             a += nb;
         }
     };
     auto ready = [&](uint32_t a, uint32_t len) -> bool {
+        bool all = true;
         for (const uint32_t e = a + len; a < e;) {
             const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
             const uint32_t m = nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0;
-            if ((__hip_atomic_load(&done[a >> 5], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) & m) != m)
-                return false;
+            all &= (__hip_atomic_load(&done[a >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & m) == m;
             a += nb;
         }
-        return true;
+        if (all)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        return all;
+    };
+    // n bytes from LDS src to LDS dst, dst - src >= step or the ranges apart:
+    // up to four 16-byte pieces read before they are written (a piece's
+    // source was written at least `step` bytes earlier)
+    auto lcopy = [&](uint32_t dst, uint32_t src, uint32_t n, uint32_t step) {
+        for (uint32_t k = 0; k < n; k += step) {
+            u32x4 v[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++)
+                if (16 * q < step)
+                    v[q] = lds16(src + k + 16 * q);
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++)
+                if (16 * q < step && k + 16 * q < n)
+                    lds_put(dst + k + 16 * q, v[q], min(16u, n - k - 16 * q));
+            wave_lds_sync();
+        }
     };
 
     uint32_t base_op = 0;
@@ -1067,21 +1138,59 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
         }
         const uint32_t x0 = scan(lit[0] + ml[0], tot[0]);
         const uint32_t x1 = scan(lit[1] + ml[1], tot[1]);
+        ZSK_FT(1)
         op[0] = base_op + x0;
         op[1] = base_op + tot[0] + x1;
         bool pend[2];
         for (int j = 0; j < 2; j++) {
             const bool on = op[j] < stop && lit[j] + ml[j] != 0;
-            if (on && lit[j]) {
-                for (uint32_t k = 0; k < lit[j]; k += 16)
-                    lds_put(ob0 + op[j] + k, load16u(lsp.r, lsp.s0 + src[j] + k), min(16u, lit[j] - k));
-                mark(op[j], lit[j]);
+            const uint32_t L = on ? lit[j] : 0;
+            // a run longer than kFLong (staged frames) is copied and marked
+            // by the whole wave, 1 KiB per step: one lane's serial copy of a
+            // ~1 KiB run was the literal phase's critical path
+            const bool coop = staged && L > kFLong;
+            if (staged && !ZSK_FD(1)) {
+                for (uint64_t lm = __ballot(coop); lm; lm &= lm - 1) {
+                    const int q = (int)__builtin_ctzll(lm);
+                    const uint32_t d0 = ob0 + lane_val(op[j], q), s0 = cs0 + lane_val(src[j], q), n = lane_val(L, q);
+                    for (uint32_t k = 16 * lane; k < n; k += 1024)
+                        lds_put(d0 + k, lds16(s0 + k), min(16u, n - k));
+                }
             }
-            pend[j] = on && ml[j] != 0;
-            if (on)
-                atomicMax(&hi_end, op[j] + lit[j] + ml[j]);
+            if (!coop && L && !ZSK_FD(1)) {
+                if (staged)
+                    lcopy(ob0 + op[j], cs0 + src[j], L, 64);
+                else
+                    for (uint32_t k = 0; k < L; k += 16)
+                        lds_put(ob0 + op[j] + k, load16u(lsp.r, lsp.s0 + src[j] + k), min(16u, L - k));
+            }
+            if (!ZSK_FD(2)) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                for (uint64_t lm = __ballot(coop); lm; lm &= lm - 1) {
+                    const int q = (int)__builtin_ctzll(lm);
+                    const uint32_t a = lane_val(op[j], q), e = a + lane_val(L, q) - 1;
+                    for (uint32_t g = (a >> 5) + lane; g <= e >> 5; g += 64) {
+                        const uint32_t lo = g == a >> 5 ? a & 31 : 0, hi = g == e >> 5 ? e & 31 : 31;
+                        const uint32_t m = hi - lo == 31 ? 0xFFFFFFFFu : ((1u << (hi - lo + 1)) - 1) << lo;
+                        __hip_atomic_fetch_or(&done[g], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                if (!coop && L)
+                    mark(op[j], L);
+            }
+            pend[j] = on && ml[j] != 0 && !ZSK_FD(4);
+        }
+        {
+            // the decoded end: a wave max, one LDS atomic per wave (2,048
+            // atomics on one word cost ~20K cycles per frame)
+            const bool on0 = op[0] < stop && lit[0] + ml[0] != 0, on1 = op[1] < stop && lit[1] + ml[1] != 0;
+            const uint32_t e = max(on0 ? op[0] + lit[0] + ml[0] : 0u, on1 ? op[1] + lit[1] + ml[1] : 0u);
+            const uint32_t we = wave_incl_max(e);
+            if (lane == 63 && we)
+                atomicMax(&hi_end, we);
         }
         __syncthreads();
+        ZSK_FT(2)
         // each wave loops on its own until its matches are copied (no
         // workgroup barrier per round: a wave whose sources are ready runs
         // ahead; one that made no progress sleeps a little)
@@ -1093,9 +1202,8 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
                 const uint32_t mb = op[j] + lit[j], o = off[j], m = ml[j];
                 if (!ready(mb - o, o >= m ? m : o))
                     continue;
-                if (o >= m) {   // source and destination apart: pieces in any order
-                    for (uint32_t k = 0; k < m; k += 16)
-                        lds_put(ob0 + mb + k, lds16(ob0 + mb - o + k), min(16u, m - k));
+                if (o >= m || o >= 16) {   // apart, or trailing by >= 16: pieces ahead of their sources
+                    lcopy(ob0 + mb, ob0 + mb - o, m, o >= m ? 64u : min(64u, o & ~15u));
                 } else {
                     // overlapping: the first e = o * ceil(16 / o) bytes one at a
                     // time, then 16-byte pieces trailing by e (each reads bytes
@@ -1117,12 +1225,22 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
             }
             // (validated items always drain; the bound only guards the GPU
             // against a malformed list)
-            if (!__any(pend[0] || pend[1]) || pass > (1u << 22))
+            if (!__any(pend[0] || pend[1]) || pass > (1u << 22)) {
+#ifdef ZSK_TUNING
+                if (lane == 0)
+                    atomicAdd(&g_ftime[6], (unsigned long long)(pass + 1));
+#endif
                 break;
+            }
             if (!__any(moved))
                 __builtin_amdgcn_s_sleep(1);
         }
         __syncthreads();
+        ZSK_FT(3)
+#ifdef ZSK_TUNING
+        if (t == 0)
+            atomicAdd(&g_ftime[5], 1ull);
+#endif
         base_op += tot[0] + tot[1];
     }
     __syncthreads();
@@ -1139,7 +1257,12 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const uint32_t tail0 = head + 16 * nchunks;
     if (tail0 + t < E)
         o[tail0 + t] = ob[tail0 + t];
+#ifdef ZSK_TUNING
+    __syncthreads();
+    ZSK_FT(4)
+#endif
 }
+#undef ZSK_FT
 #endif
 
 }   // namespace
@@ -1238,8 +1361,31 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
 {
     if (nframes == 0)
         return 0;
+#ifdef ZSK_TUNING
+    // ZSEEK_FRAME_TIMERS: accumulate the phase cycles, print every 100 launches
+    static const bool timers = getenv("ZSEEK_FRAME_TIMERS") != nullptr;
+    static int calls = 0;
+    if (timers && calls == 0) {
+        unsigned long long z[8] = {0};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ftime), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+        const uint32_t fd = getenv("ZSEEK_FRAME_DIAG") ? (uint32_t)atoi(getenv("ZSEEK_FRAME_DIAG")) : 0u;
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fdiag), &fd, sizeof(fd), 0, hipMemcpyHostToDevice, stream);
+    }
+#endif
     hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
                        rec_base, items, nitems, d_status, stop_last);
+#ifdef ZSK_TUNING
+    if (timers && ++calls % 100 == 0) {
+        unsigned long long z[8] = {0};
+        (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_ftime), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        const double fr = z[7] ? (double)z[7] : 1.0;
+        fprintf(stderr,
+                "frame execute cycles per frame: stage+init %.0f items+scan %.0f literals %.0f matches %.0f "
+                "output %.0f | windows %.2f wave passes %.1f (%llu frames)\n",
+                z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr, z[6] / fr / 16.0, z[7]);
+    }
+#endif
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
