@@ -1092,6 +1092,33 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         return all;
     };
+    // 1..64 bytes between disjoint LDS ranges with whole-width writes only:
+    // 16-byte pieces from the start plus one ending at n (overlapping pieces
+    // rewrite equal bytes), two 8- or 4-byte ones below 16 bytes -- no
+    // per-piece partial-store branches (reads may run past the source: the
+    // arrays have slack)
+    auto scopy = [&](uint32_t dst, uint32_t src, uint32_t n) {
+        if (n >= 16) {
+            const u32x4 a = lds16(src), b = lds16(src + 16), c = lds16(src + 32), e = lds16(src + n - 16);
+            *lp<u32x4_l>(dst) = a;
+            if (n > 32)
+                *lp<u32x4_l>(dst + 16) = b;
+            if (n > 48)
+                *lp<u32x4_l>(dst + 32) = c;
+            *lp<u32x4_l>(dst + n - 16) = e;
+        } else if (n >= 8) {
+            const uint64_t a = *lp<u64_l>(src), e = *lp<u64_l>(src + n - 8);
+            *lp<u64_l>(dst) = a;
+            *lp<u64_l>(dst + n - 8) = e;
+        } else if (n >= 4) {
+            const uint32_t a = *lp<u32_l>(src), e = *lp<u32_l>(src + n - 4);
+            *lp<u32_l>(dst) = a;
+            *lp<u32_l>(dst + n - 4) = e;
+        } else {
+            for (uint32_t k = 0; k < n; k++)
+                *lp<uint8_t>(dst + k) = *lp<uint8_t>(src + k);
+        }
+    };
     // n bytes from LDS src to LDS dst, dst - src >= step or the ranges apart:
     // up to four 16-byte pieces read before they are written (a piece's
     // source was written at least `step` bytes earlier)
@@ -1158,7 +1185,9 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
                 }
             }
             if (!coop && L && !ZSK_FD(1)) {
-                if (staged)
+                if (staged && L <= 64)
+                    scopy(ob0 + op[j], cs0 + src[j], L);
+                else if (staged)
                     lcopy(ob0 + op[j], cs0 + src[j], L, 64);
                 else
                     for (uint32_t k = 0; k < L; k += 16)
@@ -1202,7 +1231,9 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
                 const uint32_t mb = op[j] + lit[j], o = off[j], m = ml[j];
                 if (!ready(mb - o, o >= m ? m : o))
                     continue;
-                if (o >= m || o >= 16) {   // apart, or trailing by >= 16: pieces ahead of their sources
+                if (o >= m && m <= 64) {
+                    scopy(ob0 + mb, ob0 + mb - o, m);
+                } else if (o >= m || o >= 16) {   // apart, or trailing by >= 16: pieces ahead of their sources
                     lcopy(ob0 + mb, ob0 + mb - o, m, o >= m ? 64u : min(64u, o & ~15u));
                 } else {
                     // overlapping: the first e = o * ceil(16 / o) bytes one at a
