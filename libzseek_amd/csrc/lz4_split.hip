@@ -555,6 +555,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                              solo ? total_dev : nullptr);
     }
     stage_mark(2, stream);
+    bool frame_handoff = false;
     if (stages & 4) {
         // the one-frame route executes a frame of <= 64 KiB per workgroup
         // (env ZSEEK_ONE_EXEC=wave: the wave kernel, as round 3)
@@ -563,8 +564,12 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
             return v && !strcmp(v, "wave");
         }();
         if (one && !wave_exec && ((tune >> 8) & 0xFFF) == 0) {
+            // hand-offs of <= 64 KiB frames decoded inside (when the batch has
+            // no bigger frame and the hand-off stage is asked for: no
+            // hand-off launch below)
+            frame_handoff = (stages & 8) && max_dsize <= 65536;
             launch_seq_exec_frames(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                                   stream, stop_last);
+                                   d_fail_at, stream, stop_last, frame_handoff);
             if (max_dsize > 65536)
                 launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status, stream,
                                 0, blk, stop_last, 65537);
@@ -579,7 +584,7 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         return -1;
     }
     int rc = 0;
-    if (stages & 8)
+    if ((stages & 8) && !frame_handoff)
         rc = launch_lz4_wave_deferred(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
     stage_mark(4, stream);
     return rc;

@@ -23,6 +23,9 @@
 #include <stdio.h>
 
 #include "lz4_dev.h"
+#ifndef ZSK_EXEC_SEG_TU
+#include "lz4_wave_dev.h"   // the one-frame execute decodes its batch's hand-offs
+#endif
 #include "zsk_internal.h"
 
 namespace zsk {
@@ -1002,7 +1005,7 @@ __device__ uint32_t g_fdiag;   // ZSEEK_FRAME_DIAG: 1 no literal copies, 2 no li
 __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
-    const int32_t *__restrict__ status, uint32_t stop_last)
+    int32_t *__restrict__ status, uint32_t *__restrict__ fail_at, uint32_t stop_last, uint32_t handoff)
 {
     __shared__ __attribute__((aligned(16))) uint8_t ob[kFMax + 80];
     __shared__ __attribute__((aligned(16))) uint8_t cs[kFCStage + 80];
@@ -1012,11 +1015,17 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const uint32_t f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (f >= n)
         return;
-    if (status[f] == ST_NOT_RUN)
-        return;   // the hand-off decodes it
     const FrameDesc d = desc[f];
     if (d.d_size > kFMax)
-        return;   // seq_exec_kernel's frame
+        return;   // seq_exec_kernel's frame (its hand-off: the wave kernel)
+    if (__builtin_amdgcn_readfirstlane(status[f]) == ST_NOT_RUN) {
+        // the hand-off (handoff != 0): the wave decoder of lz4_wave_kernel on
+        // wave 0, its ring in the stage -- the batch then launches no
+        // hand-off kernel (5 us + a launch gap per one-frame miss)
+        if (handoff && wv == 0)
+            lz4w::wave_frame<4096>(desc, f, comp, out, status, fail_at, ob);
+        return;
+    }
     const uint32_t nit = nitems[f];
     const uint32_t stop = f + 1 == n ? min(stop_last, d.d_size) : d.d_size;
     const uint64_t *it = items + rec_base[f];
@@ -1388,7 +1397,8 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 
 int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                            const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
-                           const int32_t *d_status, hipStream_t stream, uint32_t stop_last)
+                           int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
+                           bool handoff)
 {
     if (nframes == 0)
         return 0;
@@ -1404,7 +1414,7 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
     }
 #endif
     hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
-                       rec_base, items, nitems, d_status, stop_last);
+                       rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff ? 1u : 0u);
 #ifdef ZSK_TUNING
     if (timers && ++calls % 100 == 0) {
         unsigned long long z[8] = {0};

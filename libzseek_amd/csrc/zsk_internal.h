@@ -201,10 +201,13 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
                     uint32_t min_dsize = 0);
 // The one-frame route's execute (seq_exec.hip): one frame of <= 64 KiB
 // decoded per 1,024-thread workgroup, output staged whole in LDS; bigger
-// frames are left to launch_seq_exec(..., min_dsize = 65537).
+// frames are left to launch_seq_exec(..., min_dsize = 65537).  handoff: the
+// kernel also decodes its frames the parse left ST_NOT_RUN (the wave
+// decoder), so no hand-off pass is needed for them.
 int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                            const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
-                           const int32_t *d_status, hipStream_t stream, uint32_t stop_last);
+                           int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
+                           bool handoff);
 int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         const int32_t *d_status, hipStream_t stream, const SplitScratch *blk);
