@@ -182,92 +182,99 @@ __device__ __forceinline__ int32_t block_fail(const Blk &B, uint32_t bsid, uint3
 __device__ __forceinline__ void put_item(uint64_t *it, uint32_t &k, uint32_t lsrc, uint32_t lit,
                                          uint32_t off, uint32_t ml)
 {
-    if (lit > 255 || ml > 258) {
-        it[k] = ((uint64_t)off << 32) | (lsrc | kItemExt);
+    // one store always, the extended pair's second only when needed (no
+    // two-way branch in the emit loop)
+    const bool ext = lit > 255 || ml > 258;
+    it[k] = ext ? (((uint64_t)off << 32) | (lsrc | kItemExt))
+                : (((uint64_t)(off | (lit << 16) | ((ml ? ml - 3 : 0) << 24)) << 32) | lsrc);
+    if (ext)
         it[k + 1] = ((uint64_t)ml << 32) | lit;
-        k += 2;
-    } else {
-        it[k] = ((uint64_t)(off | (lit << 16) | ((ml ? ml - 3 : 0) << 24)) << 32) | lsrc;
-        k += 1;
-    }
+    k += ext ? 2 : 1;
 }
 
 // Pass 3: the validated parse of a true range [p, y) from output position op,
 // items from slot k.  Returns -1, or the status of the first failing rule
-// (ST_BLOCK_ERR for a block failure, ST_DST_OVERFLOW).
+// (ST_BLOCK_ERR for a block failure, ST_DST_OVERFLOW), in liblz4's order.
+// A sequence's rules fold into one status and one exit from the loop (fewer
+// divergent exits for the wave to track).
 __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B, uint32_t p,
                                               uint32_t y, uint32_t op, uint64_t *it, uint32_t k)
 {
     const uint32_t iend = B.iend;
+    int32_t st = -1;
     while (p < y) {
-        uint32_t lit;
-        uint32_t tok;
-        {
-            const uint32_t t4 = rd4(S, W, p);
-            tok = t4 & 0xFF;
+        const uint32_t t4 = rd4(S, W, p);
+        const uint32_t tok = t4 & 0xFF;
+        p++;
+        uint32_t lit = tok >> 4;
+        if (lit == 15) {
+            if (iend - p <= 15) {
+                st = ST_BLOCK_ERR;
+                break;
+            }
+            uint32_t e = (t4 >> 8) & 0xFF;
             p++;
-            lit = tok >> 4;
-            if (lit == 15) {
-                if (iend - p <= 15)
-                    return ST_BLOCK_ERR;
-                uint32_t s = (t4 >> 8) & 0xFF;
+            lit += e;
+            while (e == 255 && p < iend) {
+                e = rd1(S, W, p);
                 p++;
-                lit += s;
-                while (s == 255) {
-                    if (p >= iend)
-                        return ST_BLOCK_ERR;
-                    s = rd1(S, W, p);
-                    p++;
-                    lit += s;
-                }
+                lit += e;
+            }
+            if (e == 255) {   // the length bytes run past the block
+                st = ST_BLOCK_ERR;
+                break;
             }
         }
         if (op + lit > B.oend - kMfLimit || iend - p < lit + 2 + 1 + kLastLiterals) {
             // the block's last sequence: literals only, ending the block
-            if (iend - p != lit || op + lit > B.oend)
-                return ST_BLOCK_ERR;
-            if (op + lit > B.dlen)
-                return ST_DST_OVERFLOW;
-            put_item(it, k, p, lit, 0, 0);
-            return -1;
+            st = (iend - p != lit || op + lit > B.oend) ? ST_BLOCK_ERR : op + lit > B.dlen ? ST_DST_OVERFLOW : -1;
+            if (st < 0)
+                put_item(it, k, p, lit, 0, 0);
+            break;
         }
-        if (op + lit > B.dlen)
-            return ST_DST_OVERFLOW;
         const uint32_t lsrc = p;
-        op += lit;
+        const uint32_t mb = op + lit;
         p += lit;
         const uint32_t o4 = rd4(S, W, p);
         const uint32_t off = o4 & 0xFFFF;
         p += 2;
         uint32_t ml = tok & 15;
+        bool bad = false;
         if (ml == 15) {
-            uint32_t s = (o4 >> 16) & 0xFF;
-            bool first = true;
-            do {
-                if (p >= iend)
-                    return ST_BLOCK_ERR;
+            uint32_t e = (o4 >> 16) & 0xFF;
+            for (bool first = true;; first = false) {
+                if (p >= iend) {
+                    bad = true;
+                    break;
+                }
                 if (!first)
-                    s = rd1(S, W, p);
-                first = false;
+                    e = rd1(S, W, p);
                 p++;
-                ml += s;
-                if (p >= iend - (kLastLiterals - 1))
-                    return ST_BLOCK_ERR;
-            } while (s == 255);
+                ml += e;
+                if (p >= iend - (kLastLiterals - 1)) {
+                    bad = true;
+                    break;
+                }
+                if (e != 255)
+                    break;
+            }
         }
         ml += kMinMatch;
-        if (off > op - B.floor_)
-            return ST_BLOCK_ERR;
-        if (off == 0)   // liblz4 writes zeros: the wave kernel decodes the frame
-            return ST_NOT_RUN;
-        if (op + ml > B.oend - kLastLiterals)
-            return ST_BLOCK_ERR;
-        if (op + ml > B.dlen)
-            return ST_DST_OVERFLOW;
+        // the literals' output room first (checked before the offset is
+        // read), then the match length bytes, the offset, the match's room
+        st = mb > B.dlen                        ? ST_DST_OVERFLOW
+             : bad                              ? ST_BLOCK_ERR
+             : off > mb - B.floor_              ? ST_BLOCK_ERR
+             : off == 0                         ? ST_NOT_RUN   // liblz4 writes zeros: the wave kernel decodes the frame
+             : mb + ml > B.oend - kLastLiterals ? ST_BLOCK_ERR
+             : mb + ml > B.dlen                 ? ST_DST_OVERFLOW
+                                                : -1;
+        if (st >= 0)
+            break;
         put_item(it, k, lsrc, lit, off, ml);
-        op += ml;
+        op = mb + ml;
     }
-    return -1;
+    return st;
 }
 
 // One-frame route: pass 1 records, for each of a lane's first kRec visited
