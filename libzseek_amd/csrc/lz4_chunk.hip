@@ -137,16 +137,12 @@ __device__ __forceinline__ void skel(const Src &S, Win &W, uint32_t &p, uint32_t
             lit += e;
         }
     }
-    // liblz4's input-side end rule (ip + lit > iend - (2 + 1 + LASTLITERALS))
-    if (pp >= iend || iend - pp < lit + 8) {
-        out += lit;
-        nitem += lit > 255 ? 2 : 1;
-        p = iend;
-        return;
-    }
+    // liblz4's input-side end rule (ip + lit > iend - (2 + 1 + LASTLITERALS)):
+    // a literals-only last sequence (no early exit: one join for the wave)
+    const bool endr = pp >= iend || iend - pp < lit + 8;
     uint32_t q = pp + lit;
     uint32_t ml = tok & 15;
-    if (ml == 15) {
+    if (!endr && ml == 15) {
         uint32_t e = (rd4(S, W, q) >> 16) & 0xFF;
         q += 3;
         ml += e;
@@ -158,10 +154,10 @@ __device__ __forceinline__ void skel(const Src &S, Win &W, uint32_t &p, uint32_t
     } else {
         q += 2;
     }
-    ml += kMinMatch;
+    ml = endr ? 0 : ml + kMinMatch;
     out += lit + ml;
     nitem += (lit > 255 || ml > 258) ? 2 : 1;
-    p = q < iend ? q : iend;
+    p = endr || q >= iend ? iend : q;
 }
 
 struct Blk {
