@@ -1194,9 +1194,11 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
                 }
             }
             if (!coop && L && !ZSK_FD(1)) {
-                if (staged && L <= 64)
-                    scopy(ob0 + op[j], cs0 + src[j], L);
-                else if (staged)
+                if (staged && L <= 2 * 64) {   // (coop takes longer runs)
+                    scopy(ob0 + op[j], cs0 + src[j], min(L, 64u));
+                    if (L > 64)
+                        scopy(ob0 + op[j] + 64, cs0 + src[j] + 64, L - 64);
+                } else if (staged)
                     lcopy(ob0 + op[j], cs0 + src[j], L, 64);
                 else
                     for (uint32_t k = 0; k < L; k += 16)
@@ -1240,8 +1242,10 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
                 const uint32_t mb = op[j] + lit[j], o = off[j], m = ml[j];
                 if (!ready(mb - o, o >= m ? m : o))
                     continue;
-                if (o >= m && m <= 64) {
-                    scopy(ob0 + mb, ob0 + mb - o, m);
+                if (o >= m && m <= 128) {
+                    scopy(ob0 + mb, ob0 + mb - o, min(m, 64u));
+                    if (m > 64)
+                        scopy(ob0 + mb + 64, ob0 + mb - o + 64, m - 64);
                 } else if (o >= m || o >= 16) {   // apart, or trailing by >= 16: pieces ahead of their sources
                     lcopy(ob0 + mb, ob0 + mb - o, m, o >= m ? 64u : min(64u, o & ~15u));
                 } else {
