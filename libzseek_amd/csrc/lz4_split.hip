@@ -580,6 +580,10 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     }
     stage_mark(3, stream);
     if (hipGetLastError() != hipSuccess) {
+        // a plan cut short may leave its finish counter or out-of-order flag
+        // set: the next plan on this scratch must start from zero
+        (void)hipMemsetAsync(s->redo, 0, 2 * sizeof(uint32_t), stream);
+        (void)hipGetLastError();
         stage_mark(4, stream);
         return -1;
     }
@@ -595,9 +599,11 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 // the plan runs: from the compressed bytes d_comp's allocation can hold past
 // d_comp (hipMemGetAddressRange) -- the plan lays frames out at
 // (c_off - c_off[0]) / 8 + 40 f, so span / 8 + 44 n + 64 slots always fit
-// frames stored in file order in that span, whatever their size -- else for
-// 64 KiB frames; and never below the item total the previous plan on that
-// set reported.  Frames that still do not fit go to the wave kernel and the
+// frames stored in file order in that span, whatever their size -- capped at
+// what n frames of up to 4 MiB compressed can use (a caller's span may sit in
+// a multi-GiB arena: a few frames must not reserve GiBs), else for 64 KiB
+// frames; and never below the item total the previous plan on that set
+// reported.  Frames that still do not fit go to the wave kernel and the
 // next call grows.  (Round 3 sized a first call for 64 KiB frames only, so
 // a first call over 1 MiB frames handed every frame to the wave kernel.)
 // `route` (ROUTE_*) forces one production decoder for every frame (tests).
@@ -621,7 +627,10 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
     if (hipMemGetAddressRange(&base, &bytes, (hipDeviceptr_t)d_comp) == hipSuccess && bytes &&
         (uintptr_t)d_comp >= (uintptr_t)base && (uintptr_t)d_comp < (uintptr_t)base + bytes) {
         const uint64_t span = (uintptr_t)base + bytes - (uintptr_t)d_comp;
-        const uint64_t by_span = span / 8 + 44ull * nframes + 64;
+        uint64_t by_span = span / 8 + 44ull * nframes + 64;
+        const uint64_t by_frames = (uint64_t)nframes * slots_of((4u << 20) + 64) + 64;
+        if (by_span > by_frames)
+            by_span = by_frames;
         if (by_span <= (1ull << 30))   // up to 8 GiB of items
             want = by_span;
     }
@@ -629,8 +638,10 @@ int launch_lz4_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *
     if (s->total && *s->total > want)
         want = *s->total;
     int rc;
-    if (split_scratch_reserve(s, nframes, want, stream) != 0)
+    if (split_scratch_reserve(s, nframes, want, stream) != 0) {
+        (void)hipGetLastError();   // the failed allocation is not the wave launch's error
         rc = launch_lz4_wave(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream);
+    }
     else
         rc = launch_lz4_split(d_desc, nframes, d_comp, d_out, d_status, d_fail_at, stream, s, route, 15, tune);
     pool.release(s, stream);

@@ -52,6 +52,7 @@
 
 #include "../../include/zseek_hip.h"
 #include "host.h"
+#include "lane_plan.h"
 #include "pool.h"
 
 using namespace zsk;
@@ -392,22 +393,12 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     const size_t n = f1 - f0;
     const uint64_t c0 = st.c_off[f0], csz = st.c_off[f1] - c0;
     const uint64_t d0 = st.d_off[f0], dsz = st.d_off[f1] - d0;
-    // the decoded bytes the host needs: the request's part of the batch
-    // (host destination), and the frames the cache may keep (its last
-    // cache_cap frames)
-    const uint64_t lo = std::max<uint64_t>(J.offset, d0), hi = std::min<uint64_t>(J.end, st.d_off[f1]);
-    uint64_t h_lo = UINT64_MAX, h_hi = 0;
-    if (!J.device_dst && hi > lo) {
-        h_lo = lo;
-        h_hi = hi;
-    }
-    if (J.cache_cap) {
-        const size_t cf = f1 - std::min(n, J.cache_cap);
-        h_lo = std::min<uint64_t>(h_lo, st.d_off[cf]);
-        h_hi = std::max<uint64_t>(h_hi, st.d_off[f1]);
-    }
-    if (h_hi <= h_lo)
-        h_lo = h_hi = d0;
+    // where the batch's bytes go (lane_plan.h): the request's part (host
+    // bounce, same-device or peer copy), and the bytes the host downloads --
+    // the request's part for a host destination plus the frames the cache
+    // may keep (its last cache_cap frames)
+    const BatchRoute br = route_batch(J.device_dst, J.dst_dev, g.device, J.offset, J.end, st.d_off.data(), f0, f1,
+                                      J.cache_cap);
     const bool ck = r->verify && st.checksum_flag;
     // no cache and no checksum pass: the batch's last frame is executed only
     // as far as the request reaches into it (the reference's no-cache read
@@ -421,12 +412,12 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // always serialized each batch's host copy with the next batch's read
     // and upload: end to end 50.6 -> 33 GB/s); the download into h_out below
     // waits for them anyway
-    if (h_hi - h_lo > s.h_out_cap)
+    if (br.h_len > s.h_out_cap)
         pool_wait(&s.copies);
     // the descriptors ride behind the compressed span (past its 256-byte
     // read slack) in the same pinned buffer and the same upload
     const uint64_t doff = (csz + 256 + 255) & ~255ull;
-    if (!s.reserve(doff + n * sizeof(FrameDesc), dsz, h_hi - h_lo, n, ck, J.err)) {
+    if (!s.reserve(doff + n * sizeof(FrameDesc), dsz, br.h_len, n, ck, J.err)) {
         J.io_failed = true;
         return false;
     }
@@ -449,8 +440,8 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     s.f1 = f1;
     // per-frame status then fail_at, back to back (one download for both)
     uint32_t *d_fail = reinterpret_cast<uint32_t *>(s.d_status + n);
-    s.h_from = h_lo - d0;
-    s.h_len = h_hi - h_lo;
+    s.h_from = br.h_from;
+    s.h_len = br.h_len;
     hipError_t e = hipSuccess;
     e = hipMemcpyAsync(s.d_comp, s.h_comp, doff + n * sizeof(FrameDesc), hipMemcpyHostToDevice, s.stream);
     // (the LZ4 two-phase decoder's plan kernel initializes both itself)
@@ -489,14 +480,10 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // decoded bytes out: straight into a device destination (a peer copy from
     // another lane's device), or into the slot's pinned bounce once the host
     // copies of its previous batch are done
-    if (e == hipSuccess && J.device_dst && hi > lo) {
-        if (J.dst_dev == g.device)
-            e = hipMemcpyAsync(J.buf + (lo - J.offset), s.d_out + (lo - d0), hi - lo,
-                               hipMemcpyDeviceToDevice, s.stream);
-        else
-            e = hipMemcpyPeerAsync(J.buf + (lo - J.offset), J.dst_dev, s.d_out + (lo - d0), g.device,
-                                   hi - lo, s.stream);
-    }
+    if (e == hipSuccess && br.route == COPY_DEVICE)
+        e = hipMemcpyAsync(J.buf + br.dst_off, s.d_out + br.src_off, br.len, hipMemcpyDeviceToDevice, s.stream);
+    else if (e == hipSuccess && br.route == COPY_PEER)
+        e = hipMemcpyPeerAsync(J.buf + br.dst_off, J.dst_dev, s.d_out + br.src_off, g.device, br.len, s.stream);
     if (e == hipSuccess && s.h_len) {
         pool_wait(&s.copies);
         e = hipMemcpyAsync(s.h_out, s.d_out + s.h_from, s.h_len, hipMemcpyDeviceToHost, s.stream);
@@ -750,31 +737,24 @@ ssize_t pread_frames(zseek_reader *r, void *buf, size_t count, size_t offset, vo
     // multi-frame (or no-cache) request: lanes of whole frames, split by
     // decoded bytes over the reader's devices
     const size_t f_last = (size_t)st.frame_of(end - 1);
-    const size_t nfr = f_last + 1 - f_first;
     size_t L = r->lanes.size();
     // a lane gets at least one full batch (and 1 MiB)
     const size_t per_lane = std::max<size_t>(r->batch_bytes, kLaneMin);
-    L = std::min<size_t>(L, std::max<size_t>(1, (end - offset) / per_lane));
-    L = std::min(L, nfr);
     int dst_dev = -1;
     if (device_dst) {
         hipPointerAttribute_t pa;
         dst_dev = hipPointerGetAttributes(&pa, buf) == hipSuccess ? pa.device : r->lanes[0]->device;
     }
+    const std::vector<LaneShare> share =
+        plan_lanes(L, offset, end, f_first, f_last, per_lane, [&](uint64_t x) { return st.frame_of(x); });
+    L = share.size();
     std::vector<LaneJob> jobs(L);
-    size_t f = f_first;
     for (size_t i = 0; i < L; i++) {
         LaneJob &J = jobs[i];
         J.r = r;
         J.g = r->lanes[i].get();
-        J.fa = f;
-        if (i + 1 == L) {
-            J.fb = f_last + 1;
-        } else {
-            const uint64_t cut = offset + (end - offset) * (i + 1) / L;
-            J.fb = std::max((size_t)st.frame_of(cut), f + 1);
-        }
-        f = J.fb;
+        J.fa = share[i].fa;
+        J.fb = share[i].fb;
         J.offset = offset;
         J.end = end;
         J.buf = (uint8_t *)buf;

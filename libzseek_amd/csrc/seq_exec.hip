@@ -979,7 +979,9 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
 // Frames of more than 64 KiB decoded go to seq_exec_kernel (min_dsize).
 constexpr uint32_t kFT = 1024;
 constexpr uint32_t kFMax = 65536;
-constexpr uint32_t kFCStage = 65536;   // compressed bytes staged in LDS (literal source)
+// compressed bytes staged in LDS (literal source): a 64 KiB frame stored raw
+// (65,551 bytes with its headers, more with checksums) still fits
+constexpr uint32_t kFCStage = 65536 + 256;
 constexpr uint32_t kFLong = 128;       // literal runs longer than this: copied by the whole wave
 
 #ifdef ZSK_TUNING
@@ -1042,14 +1044,15 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const bool staged = d.c_size <= kFCStage;
     if (staged) {
         const uint32_t np = (d.c_size + 15) / 16;
-        u32x4 v[kFCStage / 16 / kFT];
+        constexpr uint32_t kQ = (kFCStage / 16 + kFT - 1) / kFT;
+        u32x4 v[kQ];
 #pragma unroll
-        for (uint32_t q = 0; q < kFCStage / 16 / kFT; q++) {
+        for (uint32_t q = 0; q < kQ; q++) {
             const uint32_t i = t + q * kFT;
             v[q] = load16u(lsp.r, i < np ? lsp.s0 + 16 * i : kBad);
         }
 #pragma unroll
-        for (uint32_t q = 0; q < kFCStage / 16 / kFT; q++) {
+        for (uint32_t q = 0; q < kQ; q++) {
             const uint32_t i = t + q * kFT;
             if (i < np)
                 *lp<u32x4>(cs0 + 16 * i) = v[q];
@@ -1181,16 +1184,21 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
         for (int j = 0; j < 2; j++) {
             const bool on = op[j] < stop && lit[j] + ml[j] != 0;
             const uint32_t L = on ? lit[j] : 0;
-            // a run longer than kFLong (staged frames) is copied and marked
-            // by the whole wave, 1 KiB per step: one lane's serial copy of a
-            // ~1 KiB run was the literal phase's critical path
-            const bool coop = staged && L > kFLong;
-            if (staged && !ZSK_FD(1)) {
+            // a run longer than kFLong is copied and marked by the whole wave,
+            // 1 KiB per step: one lane's serial copy of a ~1 KiB run was the
+            // literal phase's critical path (and of a stored 64 KiB block, too
+            // big for the stage, 4,096 dependent 16-byte loads)
+            const bool coop = L > kFLong;
+            if (!ZSK_FD(1)) {
                 for (uint64_t lm = __ballot(coop); lm; lm &= lm - 1) {
                     const int q = (int)__builtin_ctzll(lm);
-                    const uint32_t d0 = ob0 + lane_val(op[j], q), s0 = cs0 + lane_val(src[j], q), n = lane_val(L, q);
-                    for (uint32_t k = 16 * lane; k < n; k += 1024)
-                        lds_put(d0 + k, lds16(s0 + k), min(16u, n - k));
+                    const uint32_t d0 = ob0 + lane_val(op[j], q), s = lane_val(src[j], q), n = lane_val(L, q);
+                    if (staged)
+                        for (uint32_t k = 16 * lane; k < n; k += 1024)
+                            lds_put(d0 + k, lds16(cs0 + s + k), min(16u, n - k));
+                    else
+                        for (uint32_t k = 16 * lane; k < n; k += 1024)
+                            lds_put(d0 + k, load16u(lsp.r, lsp.s0 + s + k), min(16u, n - k));
                 }
             }
             if (!coop && L && !ZSK_FD(1)) {

@@ -91,7 +91,9 @@ struct GpuLz4 {
     // first: nothing is queued)
     bool reserve(size_t in_need)
     {
-        if (in_need <= in_cap)
+        // (the first staging is allocated even for an empty frame: its output
+        // slot needs room although it has no input bytes)
+        if (in_need <= in_cap && out_cap)
             return true;
         size_t cap = in_cap ? in_cap : kGpuFirstStaging;
         while (cap < in_need)

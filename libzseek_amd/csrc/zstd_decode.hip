@@ -2163,8 +2163,6 @@ __global__ __launch_bounds__(256) void zstd_check_kernel(const FrameDesc *__rest
     }
 }
 
-}   // namespace
-
 // blk_base at the decode's chunk boundaries (zstd_chunks) -> out[0..k]
 __global__ void zstd_bounds_kernel(const uint64_t *__restrict__ blk_base, uint32_t n, uint32_t k,
                                    uint64_t *__restrict__ out)
@@ -2173,6 +2171,8 @@ __global__ void zstd_bounds_kernel(const uint64_t *__restrict__ blk_base, uint32
     if (c <= k)
         out[c] = blk_base[(uint64_t)n * c / k];
 }
+
+}   // namespace
 
 // ---- host side -----------------------------------------------------------------------------------
 

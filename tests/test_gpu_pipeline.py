@@ -240,3 +240,18 @@ def test_concurrent_cache_hits_and_stats_during_read(gpu, zs, synth_img):
         t.join()
         assert out["got"] == data.tobytes()
         assert during > 0   # stats calls returned while the read was in flight
+
+
+def test_two_lanes_one_gib_into_host_buffer(gpu, zs):
+    """zsk_reader_set_devices([0, 0]): a 1 GiB zseek_pread into a host buffer
+    over two lanes (each its own host thread, slots and streams) is bit-exact,
+    and both lanes decoded half the frames (lane_plan.h's split)."""
+    data = zs.synth_buffer(1 << 30)
+    img = zs.lz4_seekable(data, FRAME)
+    out = np.empty(data.size, np.uint8)
+    with zs.Reader(img, 0) as r:
+        r.set_devices([0, 0])
+        assert r.pread_raw(out.ctypes.data, data.size, 0) == data.size
+        st = r.gpu_stats()
+    assert np.array_equal(out, data)
+    assert st["frames_decoded"] == data.size // FRAME

@@ -136,3 +136,14 @@ def test_gpu_writer_failure_latches(gpu, zs):
     with pytest.raises(zs.ZseekError):
         w.close()
     assert w.callbacks == 3                # frames 1, 2 (refused), then close's seek table
+
+
+def test_gpu_writer_empty_first_write(gpu, zs):
+    """An empty zseek_write first (min_frame_size 0: a frame per write) needs
+    an output slot although it has no input bytes: the GPU mode allocates its
+    first staging for it and the file equals the host writer's."""
+    data = bytes(zs.synth_buffer(1 << 20))
+    chunks = [b"", b"abc" * 100, b"", data[:70000], b""]
+    host, _ = _file(zs, chunks, 0)
+    dev, _ = _file(zs, chunks, 0, gpu_batch=0)
+    assert dev == host
