@@ -567,8 +567,27 @@ struct HufJob {
     uint32_t len;   // stream bytes
     uint32_t cnt;   // symbols to decode
     uint32_t lim;   // symbols that may be stored (the frame's capacity)
-    uint32_t tab;   // slot holding the Huffman cells | table log << 28
+    uint32_t tab;   // slot holding the Huffman cells | X2 decoder << 27 | table log << 28
 };
+constexpr uint32_t kHufSlotMask = (1u << 27) - 1;
+
+// HUF_selectDecoder (libzstd 1.4.9): the double-symbol decoder (X2) when its
+// modelled time (+1/8 for its larger table) beats X1's, per compression-ratio
+// bucket q and 256-byte output units.  dst >= 1.
+__device__ __forceinline__ uint32_t huf_select_x2(uint32_t dst, uint32_t csrc)
+{
+    constexpr uint16_t kT[16][4] = {
+        {0, 0, 1, 1},          {0, 0, 1, 1},          {38, 130, 1313, 74},   {448, 128, 1353, 74},
+        {556, 128, 1353, 74},  {714, 128, 1418, 74},  {883, 128, 1437, 74},  {897, 128, 1515, 75},
+        {926, 128, 1613, 75},  {947, 128, 1729, 77},  {1107, 128, 2083, 81}, {1177, 128, 2379, 87},
+        {1242, 128, 2415, 93}, {1349, 128, 2644, 106}, {1455, 128, 2422, 124}, {722, 128, 1891, 145},
+    };
+    const uint32_t q = csrc >= dst ? 15u : csrc * 16u / dst, d256 = dst >> 8;
+    const uint32_t t0 = kT[q][0] + kT[q][1] * d256;
+    uint32_t t1 = kT[q][2] + kT[q][3] * d256;
+    t1 += t1 >> 3;
+    return t1 < t0 ? 1u : 0u;
+}
 static_assert(sizeof(HufJob) == 32, "HufJob");
 
 // Per-frame op list, in decode order.  The frame kernel stops at its first
@@ -708,13 +727,20 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint
         return ZE_CORRUPT;
     uint32_t q = p + lh, qn = csize;
     if (type == 2) {
+        // libzstd's decoder choice (ZSTD_decodeLiteralsBlock): one stream ->
+        // X1; four -> HUF_decompress4X_hufOnly: no literals is an error, then
+        // X1 or X2 by HUF_selectDecoder.  A treeless section reuses the
+        // table's decoder (the X2 flag rides in huf_slot).
+        if (ns == 4 && size == 0)
+            return ZE_CORRUPT;
+        const uint32_t x2 = ns == 4 ? huf_select_x2(size, csize) : 0u;
         uint32_t lg = 0;
         const uint32_t hs =
             huf_read(L, F.I, wx, q, qn, &lg, reinterpret_cast<uint16_t *>(F.slots + g * kZSlot));
         if (!hs)
             return ZE_CORRUPT;
         F.huf_log = lg;
-        F.huf_slot = (uint32_t)g;
+        F.huf_slot = (uint32_t)g | x2 << 27;
         q += hs;
         qn -= hs;
     } else if (!F.huf_log) {
@@ -1509,6 +1535,87 @@ __device__ __forceinline__ void huf_stream(BRd &b, Tab T, uint32_t lg, uint8_t *
     }
 }
 
+// ---- libzstd's X2 decoder on a stream X1 rejects --------------------------------------
+// On a valid stream X1 and X2 decode the same bytes; they differ only on
+// streams X1 rejects (HUF_decodeLastSymbolX2: at a stream's last output byte a
+// two-symbol cell consumes both codes' bits, clamped at the stream's start,
+// and a read with no bits left looks at the bit container's top bits).  So a
+// lane keeps the fast X1 walk and, for an X2 stream it rejected, re-walks it
+// here in X2 cells (tests/test_zstd_oracle.py pins the rule the oracle and
+// this walk share against libzstd 1.4.9).  The re-walk reads one cell at a
+// time; only streams that failed X1 -- corrupt ones -- pay for it.
+
+// the stream at byte x of resource r, read backward through a 64-bit window
+// (two dwords, reloaded when a read leaves it: one load per ~4 cells)
+struct X2Bits {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t x;
+    uint32_t wlo;   // absolute bit of the window's bit 0 (a multiple of 32)
+    uint64_t w;
+    // bits [q - n, q) (bit q - 1 most significant), bits below the stream's
+    // first byte 0; n <= 12
+    __device__ uint32_t get(int32_t q, uint32_t n)
+    {
+        if (q <= 0)
+            return 0;
+        const int32_t lo = q - (int32_t)n, l0 = lo > 0 ? lo : 0;
+        const uint32_t a = 8 * x + (uint32_t)l0, e = 8 * x + (uint32_t)q;
+        if (a < wlo || e > wlo + 64) {
+            const uint32_t d = a >> 5;
+            w = (uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, 4 * d, 0, 0) |
+                (uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, 4 * d + 4, 0, 0) << 32;
+            wlo = 32 * d;
+        }
+        const uint32_t bits = (uint32_t)(w >> (a - wlo)) & ((1u << (uint32_t)(q - l0)) - 1);
+        return lo < 0 ? bits << (uint32_t)(-lo) : bits;
+    }
+};
+
+// X2 result of the stream (len bytes at x, cnt symbols, cells tab of table
+// log lg): bit 0 ok; bit 16: the last byte is bits 8..15 (a read with no
+// bits left), else the X1 walk's bytes stand.
+__device__ __attribute__((noinline)) uint32_t x2_rescue(__amdgpu_buffer_rsrc_t r, uint32_t x, uint32_t len,
+                                                        uint32_t cnt, const uint16_t *tab, uint32_t lg)
+{
+    const uint32_t last = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, x + len - 1, 0, 0);
+    if (!last || !cnt)
+        return 0;
+    int32_t rr = 8 * (int32_t)(len - 1) + (31 - __builtin_clz(last));   // bits below the end mark
+    X2Bits B{r, x, 0xFFFFFFC0u, 0};
+    auto Z = [&](int32_t q) -> uint32_t { return tab[B.get(q, lg)]; };
+    uint32_t p = 0;
+    while (p + 2 <= cnt) {   // HUF_decodeStreamX2's cells before the last byte
+        if (rr <= 0)
+            return 0;
+        const uint32_t nb1 = Z(rr) & 0xFF, nb2 = Z(rr - (int32_t)nb1) & 0xFF;
+        const bool two = nb1 + nb2 <= 12;
+        p += two ? 2 : 1;
+        rr -= (int32_t)(two ? nb1 + nb2 : nb1);
+    }
+    if (p == cnt)
+        return rr == 0 ? 1u : 0u;
+    if (rr > 0) {   // HUF_decodeLastSymbolX2
+        const uint32_t nb1 = Z(rr) & 0xFF, nb2 = Z(rr - (int32_t)nb1) & 0xFF;
+        if (nb1 + nb2 <= 12)
+            return rr <= (int32_t)(nb1 + nb2) ? 1u : 0u;
+        return rr == (int32_t)nb1 ? 1u : 0u;
+    }
+    if (rr < 0)
+        return 0;
+    // no bits left: the cell at the container's top 12 bits (the stream's
+    // first 8 bytes, zero past its end); only a two-symbol cell leaves it
+    // consumed exactly
+    uint64_t c = 0;
+    for (uint32_t i = 0; i < 8 && i < len; i++)
+        c |= (uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, x + i, 0, 0) << (8 * i);
+    const uint32_t v = (uint32_t)(c >> 52);
+    const uint32_t g1 = tab[v >> (12 - lg)], nb1 = g1 & 0xFF;
+    const uint32_t nb2 = tab[((v << nb1) & 0xFFF) >> (12 - lg)] & 0xFF;
+    if (nb1 + nb2 > 12)
+        return 0;
+    return 1u | 0x10000u | (g1 >> 8) << 8;
+}
+
 __device__ unsigned int g_hdiag[32];   // diagnostic builds: waves per lgmax, LDS / global path
 
 // B: steps per store burst (4 = 64 bytes)
@@ -1526,7 +1633,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zs
     if (j < nj)
         J = reinterpret_cast<const HufJob *>(jobs)[j];
     const bool act = J.len != 0;
-    const uint32_t jlg = J.tab >> 28, jslot = J.tab & 0x0FFFFFFFu;
+    const uint32_t jlg = J.tab >> 28, jslot = J.tab & kHufSlotMask, jx2 = (J.tab >> 27) & 1;
     const uint32_t lgmax = lane_val(wave_incl_max(act ? jlg : 0u), 63);
     // cells of each block's table (stream 0's lane), packed in block order
     const uint32_t cells = (lane & 3) == 0 && act ? ((1u << jlg) < 8 ? 8u : 1u << jlg) : 0u;
@@ -1589,6 +1696,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zs
             if ((int)lane == l)
                 run(span_rsrc(comp, s0, s1 - s0), s0);
         }
+    }
+    if (bad && jx2) {   // libzstd's X2 decoder may still accept the stream
+        const uint16_t *tp =
+            in_lds ? &tabs[first] : reinterpret_cast<const uint16_t *>(slots + (uint64_t)jslot * kZSlot);
+        const uint64_t s0 = J.src & ~15ull;
+        const uint32_t x = x2_rescue(span_rsrc(comp, s0, J.src + J.len - s0), (uint32_t)(J.src - s0), J.len, J.cnt,
+                                     tp, jlg);
+        bad = !(x & 1);
+        if ((x & 0x10000) && J.cnt - 1 < J.lim)
+            lit[J.dst + J.cnt - 1] = (uint8_t)(x >> 8);
     }
     hbad[j] = bad ? 1 : 0;
 }

@@ -123,6 +123,12 @@ class Oracle:
         L.orc_zstd_decode_at.restype = C.c_longlong
         L.orc_zstd_decode_at.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                          C.POINTER(C.c_size_t)]
+        L.orc_huf_select_x2.restype = C.c_int
+        L.orc_huf_select_x2.argtypes = [C.c_size_t, C.c_size_t]
+        L.orc_huf_decompress.restype = C.c_long
+        L.orc_huf_decompress.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.orc_zstd_x1_only.restype = None
+        L.orc_zstd_x1_only.argtypes = [C.c_int]
         L.orc_lz4f_compress_frame.restype = C.c_longlong
         L.orc_lz4f_compress_frame.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                               C.c_int, C.c_int]
@@ -185,6 +191,17 @@ class Oracle:
         if r < 0:
             return b"", -r
         return d[:r].tobytes(), 0
+
+    def huf_select_x2(self, dst_size: int, csrc_size: int) -> bool:
+        """HUF_selectDecoder restated: True = the double-symbol decoder (X2)."""
+        return bool(self.lib.orc_huf_select_x2(dst_size, csrc_size))
+
+    def huf_decompress(self, x2: bool, four: bool, src: bytes, cnt: int):
+        """HUF_decompress{1,4}X{1,2}_DCtx restated -> (ok, cnt bytes written)."""
+        s = np.frombuffer(src, np.uint8)
+        d = np.zeros(cnt + 64, np.uint8)
+        r = self.lib.orc_huf_decompress(int(x2), int(four), s.ctypes.data, s.size, d.ctypes.data, cnt)
+        return r >= 0, d[:cnt].tobytes()
 
     def zstd_decode_at(self, src: bytes, dst_cap: int):
         """-> (decoded bytes, 0, None) or (bytes before the failing block, zstd

@@ -86,11 +86,6 @@ static uint64_t bitr_read(BitR *b, int nb)
     return bits_at(b->p, b->n, b->pos, nb);
 }
 
-static uint64_t bitr_peek(const BitR *b, int nb)
-{
-    return bits_at(b->p, b->n, b->pos - nb, nb);
-}
-
 /* ---- FSE ------------------------------------------------------------------- */
 typedef struct {
     uint8_t sym, nb;
@@ -198,18 +193,124 @@ static int fse_build(Cell *t, const int16_t *norm, int nsym, int tl)
     return 0;
 }
 
-/* ---- Huffman literals (RFC 8878 §4.2) ------------------------------------------ */
+/* ---- Huffman literals (RFC 8878 §4.2; libzstd 1.4.9 huf_decompress.c) ------------
+ * libzstd has two Huffman decoders.  X1 looks up one symbol per read in a
+ * table of 2^tableLog cells; X2 looks up one or two symbols per read in a
+ * table of 2^12 cells (a second symbol when both codes fit in 12 bits).  A
+ * 4-stream literals section picks one by HUF_selectDecoder's timing model
+ * (litSize, litCSize), a 1-stream section always uses X1, and a treeless
+ * section reuses the previous table with the decoder that built it.  On valid
+ * streams both give the same bytes; on corrupt ones they differ, so both are
+ * restated here down to libzstd's 64-bit bit container (BIT_DStream_t):
+ *   - the look-ahead shifts by (bitsConsumed & 63): past 64 consumed bits it
+ *     reads the container's top bits again;
+ *   - X2 writes two bytes per read, and at a stream's last output byte a
+ *     two-symbol cell consumes both symbols' bits, clamped to the stream end
+ *     (HUF_decodeLastSymbolX2) -- so some over- and under-long streams pass;
+ *   - X2's 4-stream loop runs every stream until one of them nears its start
+ *     or the 4th output nears its end: an earlier stream may run past its
+ *     segment (an error), or end exactly on it after a one-symbol cell whose
+ *     second byte (0) lands on the next segment's first byte.
+ * Pinned against libzstd 1.4.9's own HUF_* entry points in
+ * tests/test_zstd_oracle.py (random and corrupted streams, every table log). */
 typedef struct {
-    uint8_t sym[1 << 12];
-    uint8_t nb[1 << 12];
-    int log;
+    const uint8_t *start, *ptr, *limit;
+    uint64_t c;          /* bitContainer */
+    uint32_t consumed;   /* bitsConsumed */
+} BitD;
+
+enum { BD_UNFINISHED = 0, BD_END_OF_BUFFER = 1, BD_COMPLETED = 2, BD_OVERFLOW = 3 };
+
+static uint64_t rd64(const uint8_t *p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+
+/* BIT_initDStream */
+static int bitd_init(BitD *b, const uint8_t *p, size_t n)
+{
+    memset(b, 0, sizeof *b);
+    if (n < 1)
+        return -1;
+    b->start = p;
+    b->limit = p + 8;
+    const uint8_t last = p[n - 1];
+    if (n >= 8) {
+        b->ptr = p + n - 8;
+        b->c = rd64(b->ptr);
+        b->consumed = last ? 8 - (uint32_t)highbit(last) : 0;
+        if (!last)
+            return -1;
+    } else {
+        b->ptr = p;
+        b->c = 0;
+        for (size_t i = 0; i < n; i++)
+            b->c |= (uint64_t)p[i] << (8 * i);
+        b->consumed = last ? 8 - (uint32_t)highbit(last) : 0;
+        if (!last)
+            return -1;
+        b->consumed += (uint32_t)(8 - n) * 8;
+    }
+    return 0;
+}
+
+/* BIT_lookBitsFast (nb >= 1) */
+static uint32_t bitd_look(const BitD *b, uint32_t nb)
+{
+    return (uint32_t)((b->c << (b->consumed & 63)) >> ((64 - nb) & 63));
+}
+
+/* BIT_reloadDStream */
+static int bitd_reload(BitD *b)
+{
+    if (b->consumed > 64)
+        return BD_OVERFLOW;
+    if (b->ptr >= b->limit) {
+        b->ptr -= b->consumed >> 3;
+        b->consumed &= 7;
+        b->c = rd64(b->ptr);
+        return BD_UNFINISHED;
+    }
+    if (b->ptr == b->start)
+        return b->consumed < 64 ? BD_END_OF_BUFFER : BD_COMPLETED;
+    uint32_t nbytes = b->consumed >> 3;
+    int res = BD_UNFINISHED;
+    if ((size_t)(b->ptr - b->start) < nbytes) {
+        nbytes = (uint32_t)(b->ptr - b->start);
+        res = BD_END_OF_BUFFER;
+    }
+    b->ptr -= nbytes;
+    b->consumed -= nbytes * 8;
+    b->c = rd64(b->ptr);
+    return res;
+}
+
+/* BIT_reloadDStreamFast */
+static int bitd_reload_fast(BitD *b)
+{
+    if (b->ptr < b->limit)
+        return BD_OVERFLOW;
+    b->ptr -= b->consumed >> 3;
+    b->consumed &= 7;
+    b->c = rd64(b->ptr);
+    return BD_UNFINISHED;
+}
+
+/* BIT_endOfDStream */
+static int bitd_end(const BitD *b) { return b->ptr == b->start && b->consumed == 64; }
+
+typedef struct {
     int valid;
+    int x2;                 /* table type: 0 X1, 1 X2 */
+    int log;                /* lookup bits: X1 the tree's table log, X2 12 */
+    int tlog;               /* the tree's table log */
+    uint8_t x1s[1 << 12], x1n[1 << 12];                  /* X1 cell: byte, nbBits */
+    uint16_t x2q[1 << 12];                               /* X2 cell: sequence (LE16) */
+    uint8_t x2n[1 << 12], x2l[1 << 12];                  /*          nbBits, length */
+    uint8_t w[256];         /* weights of the last tree read */
+    int nsym;
 } Huf;
 
-/* Huffman tree description at p[0..n); returns bytes used or -error */
-static long huf_read(Huf *h, const uint8_t *p, size_t n)
+/* Tree description at p[0..n) -> weights (HUF_readStats); bytes used or -error */
+static long huf_weights(const uint8_t *p, size_t n, uint8_t *w, int *nsym_out, int *log_out)
 {
-    uint8_t w[256];
     int nw = 0;
     if (n == 0)
         return -ZE_SRC_WRONG;
@@ -260,7 +361,7 @@ static long huf_read(Huf *h, const uint8_t *p, size_t n)
             w[i] = (i & 1) ? (p[1 + i / 2] & 15) : (p[1 + i / 2] >> 4);
         used = (long)(1 + bytes);
     }
-    /* weights -> code lengths; the last weight is implied */
+    /* weights -> table log; the last weight is implied */
     uint32_t total = 0, rank[16] = {0};
     for (int i = 0; i < nw; i++) {
         if (w[i] >= 12)
@@ -281,41 +382,319 @@ static long huf_read(Huf *h, const uint8_t *p, size_t n)
     rank[lastw]++;
     if (rank[1] < 2 || (rank[1] & 1))
         return -ZE_CORRUPTION;
-    /* table: weight 1 symbols first, then weight 2, ... (symbol order within) */
-    uint32_t start[16], acc = 0;
+    *nsym_out = nw;
+    *log_out = log;
+    return used;
+}
+
+/* HUF_readDTableX1: weight-1 symbols first, then weight 2, ... (symbol order within) */
+static void huf_build_x1(Huf *h, const uint8_t *w, int nsym, int log)
+{
+    uint32_t start[16] = {0}, acc = 0, rank[16] = {0};
+    for (int s = 0; s < nsym; s++)
+        rank[w[s]]++;
     for (int k = 1; k <= log; k++) {
         start[k] = acc;
         acc += rank[k] << (k - 1);
     }
-    for (int s = 0; s < nw; s++) {
+    for (int s = 0; s < nsym; s++) {
         if (!w[s])
             continue;
         const uint32_t len = (1u << w[s]) >> 1;
         for (uint32_t i = 0; i < len; i++) {
-            h->sym[start[w[s]] + i] = (uint8_t)s;
-            h->nb[start[w[s]] + i] = (uint8_t)(log + 1 - w[s]);
+            h->x1s[start[w[s]] + i] = (uint8_t)s;
+            h->x1n[start[w[s]] + i] = (uint8_t)(log + 1 - w[s]);
         }
         start[w[s]] += len;
     }
-    h->log = log;
+    h->x2 = 0;
+    h->log = h->tlog = log;
     h->valid = 1;
+}
+
+/* HUF_readDTableX2 (HUF_fillDTableX2 / HUF_fillDTableX2Level2): a 12-bit
+ * table; a first symbol whose code leaves room for the shortest code gets a
+ * level-2 sub-table over the next bits: two-symbol cells for the symbols
+ * whose codes fit, one-symbol cells (the first symbol alone) below them */
+static void huf_set2(Huf *h, uint32_t u, uint32_t seq, uint32_t nb, uint32_t len)
+{
+    h->x2q[u] = (uint16_t)seq;
+    h->x2n[u] = (uint8_t)nb;
+    h->x2l[u] = (uint8_t)len;
+}
+
+static void huf_build_x2(Huf *h, const uint8_t *w, int nsym, int tlog)
+{
+    enum { TL = 12 };
+    uint32_t stats[13] = {0};
+    for (int s = 0; s < nsym; s++)
+        stats[w[s]]++;
+    int maxw = tlog;
+    while (stats[maxw] == 0)
+        maxw--;
+    /* sorted symbols by weight (weight 0 dropped); rs0[k]: first of weight k */
+    uint32_t rs0[14] = {0}, *rs = rs0 + 1, next = 0;
+    for (int k = 1; k <= maxw; k++) {
+        rs[k] = next;
+        next += stats[k];
+    }
+    rs[0] = next;
+    const uint32_t nsort = next;
+    uint8_t ssym[256], swt[256];
+    for (int s = 0; s < nsym; s++) {
+        const uint32_t r = rs[w[s]]++;
+        ssym[r] = (uint8_t)s;
+        swt[r] = w[s];
+    }
+    rs[0] = 0;
+    /* rank values: rv[c][k] = first cell of weight k, scaled down by c bits */
+    uint32_t rv[TL][13];
+    memset(rv, 0, sizeof rv);
+    const int rescale = (TL - tlog) - 1;
+    uint32_t nrv = 0;
+    for (int k = 1; k <= maxw; k++) {
+        rv[0][k] = nrv;
+        nrv += stats[k] << (k + rescale);
+    }
+    const uint32_t minbits = (uint32_t)(tlog + 1 - maxw);
+    for (uint32_t c = minbits; c < TL - minbits + 1; c++)
+        for (int k = 1; k <= maxw; k++)
+            rv[c][k] = rv[0][k] >> c;
+    /* level 1 */
+    const uint32_t base = (uint32_t)tlog + 1;
+    const int scale = (int)base - TL;
+    uint32_t r1[13];
+    memcpy(r1, rv[0], sizeof r1);
+    for (uint32_t s = 0; s < nsort; s++) {
+        const uint32_t sym = ssym[s], wt = swt[s], nb = base - wt;
+        const uint32_t st = r1[wt], len = 1u << (TL - nb);
+        if (TL - nb >= minbits) {
+            int minw = (int)nb + scale;
+            if (minw < 1)
+                minw = 1;
+            const uint32_t srank = rs0[minw];
+            /* level 2 over cells [st, st + len): sub-table of TL - nb bits */
+            const uint32_t slog = TL - nb;
+            uint32_t r2[13];
+            memcpy(r2, rv[nb], sizeof r2);
+            if (minw > 1)
+                for (uint32_t i = 0; i < r2[minw]; i++)
+                    huf_set2(h, st + i, sym, nb, 1);
+            for (uint32_t q = srank; q < nsort; q++) {
+                const uint32_t sym2 = ssym[q], wt2 = swt[q], nb2 = base - wt2;
+                const uint32_t l2 = 1u << (slog - nb2), s2 = r2[wt2];
+                for (uint32_t i = s2; i < s2 + l2; i++)
+                    huf_set2(h, st + i, sym + (sym2 << 8), nb2 + nb, 2);
+                r2[wt2] += l2;
+            }
+        } else {
+            for (uint32_t u = st; u < st + len; u++)
+                huf_set2(h, u, sym, nb, 1);
+        }
+        r1[wt] += len;
+    }
+    h->x2 = 1;
+    h->log = TL;
+    h->tlog = tlog;
+    h->valid = 1;
+}
+
+/* read a tree into h as X1 or X2 cells; bytes used or -error */
+static long huf_read(Huf *h, const uint8_t *p, size_t n, int x2)
+{
+    int nsym = 0, log = 0;
+    const long used = huf_weights(p, n, h->w, &nsym, &log);
+    if (used < 0)
+        return used;
+    h->nsym = nsym;
+    if (x2)
+        huf_build_x2(h, h->w, nsym, log);
+    else
+        huf_build_x1(h, h->w, nsym, log);
     return used;
 }
 
-/* one Huffman stream p[0..n) -> out[0..cnt) */
-static int huf_stream(const Huf *h, const uint8_t *p, size_t n, uint8_t *out, size_t cnt)
+/* HUF_selectDecoder: X2 when its modelled time (+1/8, for its bigger table)
+ * beats X1's, per compression ratio bucket Q and 256-byte output units */
+static const uint16_t HUF_ALGO[16][2][2] = {
+    {{0, 0}, {1, 1}},           {{0, 0}, {1, 1}},           {{38, 130}, {1313, 74}},
+    {{448, 128}, {1353, 74}},   {{556, 128}, {1353, 74}},   {{714, 128}, {1418, 74}},
+    {{883, 128}, {1437, 74}},   {{897, 128}, {1515, 75}},   {{926, 128}, {1613, 75}},
+    {{947, 128}, {1729, 77}},   {{1107, 128}, {2083, 81}},  {{1177, 128}, {2379, 87}},
+    {{1242, 128}, {2415, 93}},  {{1349, 128}, {2644, 106}}, {{1455, 128}, {2422, 124}},
+    {{722, 128}, {1891, 145}},
+};
+
+int orc_huf_select_x2(size_t dst, size_t csrc)
 {
-    BitR b;
-    if (bitr_init(&b, p, n) != 0)
-        return -ZE_CORRUPTION;
-    for (size_t i = 0; i < cnt; i++) {
-        const uint32_t v = (uint32_t)bitr_peek(&b, h->log);
-        out[i] = h->sym[v];
-        b.pos -= h->nb[v];
+    const uint32_t q = csrc >= dst ? 15 : (uint32_t)(csrc * 16 / dst);
+    const uint32_t d256 = (uint32_t)(dst >> 8);
+    const uint32_t t0 = HUF_ALGO[q][0][0] + HUF_ALGO[q][0][1] * d256;
+    uint32_t t1 = HUF_ALGO[q][1][0] + HUF_ALGO[q][1][1] * d256;
+    t1 += t1 >> 3;
+    return t1 < t0;
+}
+
+/* X1: one symbol per read */
+static void x1_sym(const Huf *h, BitD *b, uint8_t *p)
+{
+    const uint32_t v = bitd_look(b, (uint32_t)h->log);
+    *p = h->x1s[v];
+    b->consumed += h->x1n[v];
+}
+
+/* HUF_decodeStreamX1 over [p, pe) (offsets into o) */
+static void x1_stream(const Huf *h, BitD *b, uint8_t *o, long p, long pe)
+{
+    while ((bitd_reload(b) == BD_UNFINISHED) & (p < pe - 3)) {
+        for (int k = 0; k < 4; k++)
+            x1_sym(h, b, o + p++);
     }
-    if (b.pos != 0)
+    while (p < pe)
+        x1_sym(h, b, o + p++);
+}
+
+/* X2: two bytes written, 1 or 2 of them kept */
+static uint32_t x2_sym(const Huf *h, BitD *b, uint8_t *p)
+{
+    const uint32_t v = bitd_look(b, 12);
+    p[0] = (uint8_t)h->x2q[v];
+    p[1] = (uint8_t)(h->x2q[v] >> 8);
+    b->consumed += h->x2n[v];
+    return h->x2l[v];
+}
+
+/* HUF_decodeLastSymbolX2 */
+static void x2_last(const Huf *h, BitD *b, uint8_t *p)
+{
+    const uint32_t v = bitd_look(b, 12);
+    p[0] = (uint8_t)h->x2q[v];
+    if (h->x2l[v] == 1) {
+        b->consumed += h->x2n[v];
+    } else if (b->consumed < 64) {
+        b->consumed += h->x2n[v];
+        if (b->consumed > 64)
+            b->consumed = 64;
+    }
+}
+
+/* HUF_decodeStreamX2 over [p, pe) */
+static void x2_stream(const Huf *h, BitD *b, uint8_t *o, long p, long pe)
+{
+    while ((bitd_reload(b) == BD_UNFINISHED) & (p < pe - 7)) {
+        for (int k = 0; k < 4; k++)
+            p += x2_sym(h, b, o + p);
+    }
+    while ((bitd_reload(b) == BD_UNFINISHED) & (p <= pe - 2))
+        p += x2_sym(h, b, o + p);
+    while (p <= pe - 2)
+        p += x2_sym(h, b, o + p);
+    if (p < pe)
+        x2_last(h, b, o + p);
+}
+
+/* HUF_decompress1X{1,2}_usingDTable: one stream p[0..n) -> out[0..cnt) */
+static int huf_1x(const Huf *h, const uint8_t *p, size_t n, uint8_t *out, size_t cnt)
+{
+    BitD b;
+    if (bitd_init(&b, p, n) != 0)
         return -ZE_CORRUPTION;
+    if (h->x2)
+        x2_stream(h, &b, out, 0, (long)cnt);
+    else
+        x1_stream(h, &b, out, 0, (long)cnt);
+    return bitd_end(&b) ? 0 : -ZE_CORRUPTION;
+}
+
+/* HUF_decompress4X{1,2}_usingDTable: jump table + four streams p[0..n) ->
+ * out[0..cnt) (out has 32 bytes of slack past cnt, as libzstd's literal
+ * buffer) */
+static int huf_4x(const Huf *h, const uint8_t *p, size_t n, uint8_t *out, size_t cnt)
+{
+    if (n < 10)
+        return -ZE_CORRUPTION;
+    const size_t l1 = rd16(p), l2 = rd16(p + 2), l3 = rd16(p + 4);
+    const size_t l4 = n - (l1 + l2 + l3 + 6);
+    if (l4 > n)   /* (wrapped) */
+        return -ZE_CORRUPTION;
+    const uint8_t *q[4] = {p + 6, p + 6 + l1, p + 6 + l1 + l2, p + 6 + l1 + l2 + l3};
+    const size_t ln[4] = {l1, l2, l3, l4};
+    const long seg = (long)((cnt + 3) / 4), oend = (long)cnt;
+    if (3 * seg > oend)
+        return -ZE_CORRUPTION;
+    long op[4] = {0, seg, 2 * seg, 3 * seg};
+    const long ostart[5] = {0, seg, 2 * seg, 3 * seg, oend};
+    BitD b[4];
+    for (int k = 0; k < 4; k++)
+        if (bitd_init(&b[k], q[k], ln[k]) != 0)
+            return -ZE_CORRUPTION;
+    if (!h->x2) {
+        /* 4 symbols per stream per round, in lock step */
+        for (uint32_t go = 1; go & (op[3] < oend - 3);) {
+            for (int r = 0; r < 4; r++)
+                for (int k = 0; k < 4; k++)
+                    x1_sym(h, &b[k], out + op[k]++);
+            for (int k = 0; k < 4; k++)
+                go &= bitd_reload_fast(&b[k]) == BD_UNFINISHED;
+        }
+    } else {
+        /* 4 cells per stream per round; the streams are not in lock step */
+        for (uint32_t go = 1; go & (op[3] < oend - 7);) {
+            for (int r = 0; r < 4; r++)
+                for (int k = 0; k < 4; k++)
+                    op[k] += x2_sym(h, &b[k], out + op[k]);
+            uint32_t g = 1;
+            for (int k = 0; k < 4; k++)
+                g &= bitd_reload_fast(&b[k]) == BD_UNFINISHED;
+            go = g;
+        }
+    }
+    for (int k = 0; k < 3; k++)
+        if (op[k] > ostart[k + 1])
+            return -ZE_CORRUPTION;
+    for (int k = 0; k < 4; k++) {
+        if (h->x2)
+            x2_stream(h, &b[k], out, op[k], ostart[k + 1]);
+        else
+            x1_stream(h, &b[k], out, op[k], ostart[k + 1]);
+    }
+    for (int k = 0; k < 4; k++)
+        if (!bitd_end(&b[k]))
+            return -ZE_CORRUPTION;
     return 0;
+}
+
+/* test hook (tests/golden/make_zstd_x2.py): 1 = decode every Huffman
+ * literals section with X1, as this restatement did before round 5 -- to find
+ * the inputs on which X2's rules change libzstd's result */
+static int g_x1_only;
+void orc_zstd_x1_only(int on) { g_x1_only = on; }
+
+/* test hooks: libzstd's exported HUF entry points restated (tree + streams) */
+static long huf_entry(int x2, int four, const uint8_t *src, size_t n, uint8_t *dst, size_t cnt, Huf **keep)
+{
+    Huf *h = (Huf *)calloc(1, sizeof(Huf));
+    if (!h)
+        return -ZE_GENERIC;
+    long rc;
+    const long hs = huf_read(h, src, n, x2);
+    if (hs < 0)
+        rc = hs;
+    else if ((size_t)hs >= n)
+        rc = -ZE_SRC_WRONG;
+    else
+        rc = four ? huf_4x(h, src + hs, n - (size_t)hs, dst, cnt) : huf_1x(h, src + hs, n - (size_t)hs, dst, cnt);
+    if (keep)
+        *keep = h;
+    else
+        free(h);
+    return rc ? rc : (long)cnt;
+}
+
+/* HUF_decompress{1,4}X{1,2}_DCtx (x2: 0/1; four: 0/1); dst needs cnt + 32 bytes */
+long orc_huf_decompress(int x2, int four, const uint8_t *src, size_t n, uint8_t *dst, size_t cnt)
+{
+    return huf_entry(x2, four, src, n, dst, cnt, NULL);
 }
 
 /* ---- sequences (RFC 8878 §3.1.1.3.2) ------------------------------------------- */
@@ -449,34 +828,26 @@ static long literals(Dec *D, const uint8_t *p, size_t n, size_t *litn)
     const uint8_t *s = p + lh;
     size_t sn = csize;
     if (type == 2) {
-        const long hs = huf_read(&D->huf, s, sn);
-        if (hs < 0)
+        /* ZSTD_decodeLiteralsBlock: 1 stream -> HUF_decompress1X1_DCtx_wksp;
+         * 4 streams -> HUF_decompress4X_hufOnly_wksp (X1 or X2 by
+         * HUF_selectDecoder on litSize, litCSize) */
+        int x2 = 0;
+        if (!single) {
+            if (size == 0 || csize == 0)
+                return -ZE_CORRUPTION;
+            x2 = g_x1_only ? 0 : orc_huf_select_x2(size, csize);
+        }
+        const long hs = huf_read(&D->huf, s, sn, x2);
+        if (hs < 0 || (size_t)hs >= sn)
             return -ZE_CORRUPTION;
         s += hs;
         sn -= (size_t)hs;
     } else if (!D->huf.valid) {
         return -ZE_DICT_CORRUPTED;
     }
-    if (single) {
-        if (huf_stream(&D->huf, s, sn, D->lit, size))
-            return -ZE_CORRUPTION;
-    } else {
-        if (sn < 10)
-            return -ZE_CORRUPTION;
-        const size_t l1 = rd16(s), l2 = rd16(s + 2), l3 = rd16(s + 4);
-        if (l1 + l2 + l3 + 6 > sn)
-            return -ZE_CORRUPTION;
-        const size_t l4 = sn - 6 - l1 - l2 - l3;
-        const size_t seg = (size + 3) / 4;
-        if (3 * seg > size)
-            return -ZE_CORRUPTION;
-        const uint8_t *q = s + 6;
-        if (huf_stream(&D->huf, q, l1, D->lit, seg) ||
-            huf_stream(&D->huf, q + l1, l2, D->lit + seg, seg) ||
-            huf_stream(&D->huf, q + l1 + l2, l3, D->lit + 2 * seg, seg) ||
-            huf_stream(&D->huf, q + l1 + l2 + l3, l4, D->lit + 3 * seg, size - 3 * seg))
-            return -ZE_CORRUPTION;
-    }
+    /* (treeless: HUF_decompress{1,4}X_usingDTable, the table's own decoder) */
+    if (single ? huf_1x(&D->huf, s, sn, D->lit, size) : huf_4x(&D->huf, s, sn, D->lit, size))
+        return -ZE_CORRUPTION;
     *litn = size;
     return (long)(lh + csize);
 }

@@ -353,3 +353,73 @@ def test_zstd_many_small_frames(gpu, zs, nframes):
     img = bytes(zs.zstd_seekable(data, 1024).tobytes())
     with zs.Reader(img, 0) as r:
         assert r.read_all(data.size, 0) == data.tobytes()
+
+
+# ---------------------------------------------------------------------------
+# libzstd's double-symbol Huffman decoder (X2) on corrupted literal streams
+# ---------------------------------------------------------------------------
+def _x2_fixtures():
+    import json
+    import os
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    meta = json.load(open(os.path.join(g, "zstd_x2.json")))
+    blob = open(os.path.join(g, "zstd_x2.bin"), "rb").read()
+    frames = [blob[c["off"]: c["off"] + c["len"]] for c in meta["cases"]]
+    return meta, frames
+
+
+def _x2_seekable(meta, frame, dsize):
+    """the case between its two intact neighbours, with a seek table (as
+    tests/golden/make_zstd_x2.py built it for the reference)"""
+    fa, fb = (bytes.fromhex(h) for h in meta["neighbour_frames_hex"])
+    sa, sb = meta["neighbours"]["a"]["dsize"], meta["neighbours"]["b"]["dsize"]
+    sizes = [sa, dsize, sb]
+    table = bytearray((0x184D2A5E).to_bytes(4, "little") + (8 * 3 + 9).to_bytes(4, "little"))
+    for f, s in zip((fa, frame, fb), sizes):
+        table += len(f).to_bytes(4, "little") + s.to_bytes(4, "little")
+    table += (3).to_bytes(4, "little") + bytes([0]) + (0x8F92EAB1).to_bytes(4, "little")
+    return fa + frame + fb + bytes(table), sum(sizes)
+
+
+@pytest.mark.parametrize("repeat", [1, 700])
+def test_device_zstd_x2_fixtures(gpu, zs, repeat):
+    """tests/golden/zstd_x2.* (corrupted frames whose literal streams
+    libzstd's X2 decoder accepts and an X1 decode rejects) through
+    zsk_zstd_decode_frames: libzstd's status and bytes for every frame; at
+    700 copies (22,400 frames) the launch runs as the 3-chunk pipeline"""
+    import hashlib
+    meta, frames = _x2_fixtures()
+    cases = meta["cases"]
+    out, st = device_decode(zs, gpu, frames * repeat, [c["dsize"] for c in cases] * repeat)
+    for i, (o, s) in enumerate(zip(out, st)):
+        c = cases[i % len(cases)]
+        code = c["libzstd"]["code"]
+        if code:
+            assert s == ZSK_STATUS_ZSTD | code, (i, hex(int(s)))
+        else:
+            assert s == 0, (i, hex(int(s)))
+            assert hashlib.sha256(o).hexdigest() == c["libzstd"]["sha"], i
+
+
+@pytest.mark.parametrize("cache", [0, 1])
+def test_zstd_x2_fixtures_pread(gpu, zs, cache):
+    """the same frames inside seekable files through zseek_pread under a
+    caller's loop: the compiled reference's recorded answers (bytes
+    delivered, their hash, the last return value and its error string)"""
+    import hashlib
+    meta, frames = _x2_fixtures()
+    for c, frame in zip(meta["cases"], frames):
+        img, total = _x2_seekable(meta, frame, c["dsize"])
+        want = c["reference"][f"cache{cache}"]
+        with zs.Reader(img, cache) as r:
+            out = np.empty(total + 1, np.uint8)
+            pos = 0
+            while True:
+                n = r.pread_raw(out.ctypes.data + pos, max(total - pos, 1), pos)
+                if n <= 0:
+                    break
+                pos += n
+            assert (pos, n) == (want["bytes"], want["last"]), c["pos"]
+            assert hashlib.sha256(out[:pos].tobytes()).hexdigest() == want["sha"]
+            if n < 0:
+                assert r.error == want["error"]

@@ -100,3 +100,42 @@ def decode(z, src: bytes, cap: int):
         return out.raw[:r], 0
     finally:
         z.ZSTD_freeDCtx(d)
+
+
+# -- libzstd 1.4.9's Huffman entry points (exported by the shared library):
+#    the oracle's X1 / X2 restatement is pinned against these directly
+def load_huf(z):
+    z.HUF_selectDecoder.argtypes = [C.c_size_t, C.c_size_t]
+    z.HUF_selectDecoder.restype = C.c_uint32
+    for n in ("HUF_compress2", "HUF_compress1X"):
+        f = getattr(z, n)
+        f.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_uint, C.c_uint]
+        f.restype = C.c_size_t
+    for n in ("HUF_decompress1X1_DCtx", "HUF_decompress1X2_DCtx", "HUF_decompress4X1_DCtx",
+              "HUF_decompress4X2_DCtx", "HUF_decompress4X_hufOnly"):
+        f = getattr(z, n)
+        f.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        f.restype = C.c_size_t
+    return z
+
+
+def huf_compress(z, data: bytes, four: bool, max_log: int = 11) -> bytes | None:
+    """HUF_compress2 (4 streams) / HUF_compress1X: tree description + streams,
+    None when libzstd declines (incompressible or a single symbol)."""
+    out = C.create_string_buffer(len(data) + 1024)
+    f = z.HUF_compress2 if four else z.HUF_compress1X
+    n = f(out, len(out), data, len(data), 255, max_log)
+    if z.ZSTD_isError(n) or n <= 1:
+        return None
+    return out.raw[:n]
+
+
+def huf_decompress(z, x2: bool, four: bool, src: bytes, cnt: int):
+    """HUF_decompress{1,4}X{1,2}_DCtx on a fresh 12-bit DTable ->
+    (ok, the cnt output bytes)."""
+    dt = (C.c_uint32 * (1 + 4096))()
+    dt[0] = 12 * 0x01000001
+    out = C.create_string_buffer(cnt + 64)
+    f = getattr(z, "HUF_decompress%dX%d_DCtx" % (4 if four else 1, 2 if x2 else 1))
+    r = f(dt, out, cnt, src, len(src))
+    return (not z.ZSTD_isError(r)), out.raw[:cnt]
