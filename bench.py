@@ -392,7 +392,7 @@ def main():
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
-        n_timed, stage_ms = z.kernel_times()
+        n_timed, stage_ms = z.kernel_times(spans=zstd)
         z.kernel_timing(False)
 
     # ---- correctness: decoded == generator (size-independent check) --------
@@ -437,26 +437,30 @@ def main():
     stages, kname = None, None
     if stage_ms is not None and n_timed:
         avg_c = comp_bytes / max(nfr, 1)
-        parse_k = ("zstd_frame_kernel (every chunk; each chunk's sequence and Huffman kernels start "
-                   "beside the later chunks' frame kernels)" if zstd
-                   else z.parse_kernel_name(min(nfr, chunk_frames(args.frame)), int(avg_c)))
-        # zstd: the decode runs in frame chunks over three streams, so after the
-        # frame kernels the caller's stream measures the rest together
-        names = ({"plan": "zstd_plan_kernel + zstd_scan_kernel + zstd_bounds_kernel", "parse": parse_k,
-                  "execute": "rest of the chunks: zstd_seq_kernel | zstd_huf_kernel, zstd_lit_fix_kernel, "
-                             "seq_exec_kernel, zstd_check_kernel", "hand-off": "-"} if zstd else
-                 {"plan": "lz4_plan_direct_kernel", "parse": parse_k,
-                  "execute": "seq_exec_kernel", "hand-off": "lz4_wave_kernel<4096, 4, true>"})
-        launches = 1 if zstd else (nfr + chunk_frames(args.frame) - 1) // chunk_frames(args.frame)
-        # kernel_times averages per launch; a step is `launches` launches
-        stages = {k: {"kernel": names[k], "avg_ms": round(v * launches, 4)} for k, v in stage_ms.items()}
-        kname = names[max(("parse", "execute"), key=lambda k: stage_ms[k])]
+        if zstd:
+            # the decode runs in frame chunks over three streams: per-kernel
+            # spans on the stream each kernel runs on, summed over the chunks
+            # (they overlap one another; `stages` below are not additive)
+            names = {"plan": "zstd_plan_kernel + zstd_scan_kernel + zstd_bounds_kernel",
+                     "zstd_frame_kernel": "zstd_frame_kernel", "zstd_seq_kernel": "zstd_seq_kernel",
+                     "zstd_huf_kernel": "zstd_huf_kernel", "seq_exec_kernel": "seq_exec_kernel"}
+            launches = 1
+            kernels = ("zstd_frame_kernel", "zstd_seq_kernel", "zstd_huf_kernel", "seq_exec_kernel")
+        else:
+            parse_k = z.parse_kernel_name(min(nfr, chunk_frames(args.frame)), int(avg_c))
+            names = {"plan": "lz4_plan_direct_kernel", "parse": parse_k,
+                     "execute": "seq_exec_kernel", "hand-off": "lz4_wave_kernel<4096, 4, true>"}
+            launches = (nfr + chunk_frames(args.frame) - 1) // chunk_frames(args.frame)
+            kernels = ("parse", "execute")
+        # kernel_times gives per-launch medians; a step is `launches` launches
+        stages = {k: {"kernel": names[k], "median_ms": round(stage_ms[k] * launches, 4)} for k in names}
+        kname = names[max(kernels, key=lambda k: stage_ms[k])]
     dom = None
     if stages and kname:
         dk = [k for k, v in stages.items() if v["kernel"] == kname]
         if dk:
-            dms = stages[dk[0]]["avg_ms"] / 1e3
-            dom = {"kernel": kname, "avg_ms": round(dms * 1e3, 4),
+            dms = stages[dk[0]]["median_ms"] / 1e3
+            dom = {"kernel": kname, "median_ms": round(dms * 1e3, 4),
                    "achieved": round(alg_bytes / dms / 1e9, 1),
                    "frac": round(alg_bytes / dms / 1e9 / HBM_PEAK_GBS, 4)}
     if strong and world > 1:
@@ -791,6 +795,7 @@ def end_to_end(z, img, size):
     import ctypes as C
     res = {"api": "zseek_pread (host buffer, one call, C in-memory pread callback)", "bytes": size}
     buf = np.empty(size, np.uint8)
+    gs = z.zseek.GpuStatsC()
     for io in (1, 8):
         err = C.create_string_buffer(80)
         r = T.zsk_tool_open_mem(C.cast(L.zseek_reader_open_full, C.c_void_p), img.ctypes.data,
@@ -808,8 +813,12 @@ def end_to_end(z, img, size):
             if got.value != size:
                 return {"error": f"short read {got.value}"}
             best = max(best, got.value / secs / 1e9)
+        L.zsk_reader_gpu_stats(r, C.byref(gs))
         T.zsk_tool_close_mem(C.cast(L.zseek_reader_close, C.c_void_p), r)
         res["GBps" if io == 1 else f"GBps_io{io}"] = round(best, 2)
+        # host threads the read ran on: the copy / pread pool (usable CPUs - 2)
+        # and the concurrent pread callbacks per batch (io, capped at half the pool)
+        res["threads" if io == 1 else f"threads_io{io}"] = {"copy_pool": gs.copy_threads, "pread_parts": gs.io_parts}
     return res
 
 

@@ -124,11 +124,15 @@ ZSEEK_EXPORT const char *zsk_lz4_kernel_name(uint32_t nframes);
 ZSEEK_EXPORT const char *zsk_lz4_parse_kernel_name(uint32_t nframes, uint32_t c_size);
 
 /* Measurement hook: while on, every two-phase decode launch records HIP
- * events between its stages (plan, parse, execute, hand-off) on its stream.
- * zsk_kernel_timing(on) switches it and clears the totals;
- * zsk_kernel_times(ms, cap) waits for the recorded launches and writes the
- * average milliseconds per stage into ms[0..min(cap,4)), returning the
- * number of launches averaged.  Not on any decode path's critical path. */
+ * events between its stages (plan, parse, execute, hand-off) on its stream,
+ * and a zstd launch also around each chunk's kernels on the streams they run
+ * on.  zsk_kernel_timing(on) switches it and clears the records;
+ * zsk_kernel_times(ms, cap) waits for the recorded launches and writes, per
+ * slot, the MEDIAN milliseconds over them into ms[0..min(cap,8)): [0..3] the
+ * stages; [4..7] (zstd launches, summed over the launch's chunks)
+ * zstd_frame_kernel, zstd_seq_kernel, zstd_huf_kernel and seq_exec_kernel
+ * (the zstd literal-source execute).  Returns the
+ * number of launches recorded.  Not on any decode path's critical path. */
 ZSEEK_EXPORT int zsk_kernel_timing(int on);
 ZSEEK_EXPORT int zsk_kernel_times(double *ms, int cap);
 
@@ -157,6 +161,8 @@ typedef struct {
     uint64_t bytes_uploaded;   /* compressed bytes copied host->device  */
     uint64_t device_memory;    /* device bytes held by the reader       */
     int device;                /* HIP device ordinal, -1 before first use */
+    int copy_threads;          /* host copy / pread pool threads (usable CPUs - 2, 2..16) */
+    int io_parts;              /* concurrent pread callbacks a batch uses: min(io_threads, copy_threads / 2) */
 } zsk_gpu_stats_t;
 
 ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader,
@@ -200,6 +206,8 @@ ZSEEK_EXPORT bool zsk_reader_set_verify_checksums(zseek_reader_t *reader,
  * the reference's contract: it calls pread under the reader's lock, one call
  * at a time, and its default FILE* callback is not safe to call concurrently.
  * Only for callbacks that are (an in-memory image, pread(2) on a descriptor).
+ * The calls run on the library's host pool, at most half of it at once (the
+ * rest keeps copying decoded batches out): zsk_gpu_stats_t.io_parts.
  * Env ZSEEK_IO_THREADS at open.  false for a NULL reader or n outside 1..64.
  */
 ZSEEK_EXPORT bool zsk_reader_set_io_threads(zseek_reader_t *reader, int n);

@@ -97,6 +97,8 @@ struct DeviceGuard {
 struct CopyTicket {
     std::atomic<int> left{0};
 };
+int usable_cpus();          // affinity, capped by the cgroup CPU quota
+int copy_pool_threads();    // the pool below: max(2, min(16, usable_cpus() - 2)), env ZSEEK_COPY_THREADS
 void pool_copy(void *dst, const void *src, size_t n, CopyTicket *t);
 void pool_run(std::function<void()> fn, CopyTicket *t);   // any task, same ticket rules
 void pool_wait(CopyTicket *t);

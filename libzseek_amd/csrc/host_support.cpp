@@ -1,6 +1,7 @@
 // host_support.cpp — error buffers, seek table, decoded-frame LRU, GPU
 // context.  Host C++ behind the C ABI of include/zseek.h.
 #include <errno.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -192,6 +193,45 @@ size_t FrameCache::memory_usage() const
 }
 
 // ---------------------------------------------------------------------------
+// CPUs this process may use: its affinity mask, capped by a cgroup CPU quota
+// (v2 cpu.max, else v1 cfs_quota_us / cfs_period_us), rounded down, >= 1
+int usable_cpus()
+{
+    static const int n = [] {
+        cpu_set_t set;
+        int aff = 0;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0)
+            aff = CPU_COUNT(&set);
+        if (aff <= 0)
+            aff = (int)std::thread::hardware_concurrency();
+        double quota = 0;
+        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            long long per = 0;
+            if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+                quota = atof(q) / (double)per;
+            fclose(f);
+        } else if (FILE *f1 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+            long long q = -1, per = 0;
+            if (fscanf(f1, "%lld", &q) != 1)
+                q = -1;
+            fclose(f1);
+            if (FILE *f2 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+                if (fscanf(f2, "%lld", &per) != 1)
+                    per = 0;
+                fclose(f2);
+            }
+            if (q > 0 && per > 0)
+                quota = (double)q / (double)per;
+        }
+        int u = aff;
+        if (quota > 0 && (int)quota < u)
+            u = (int)quota;
+        return u < 1 ? 1 : u;
+    }();
+    return n;
+}
+
 // copy pool: host memcpy on worker threads (process lifetime, never joined)
 // ---------------------------------------------------------------------------
 namespace {
@@ -208,16 +248,24 @@ struct CopyTask {
 
 class CopyPool {
   public:
+    // one thread per usable CPU past two (the caller's thread and the HIP
+    // runtime's), 2..16: the pool runs both the host copies out of the pinned
+    // bounces and the concurrent pread callbacks (io_threads), so on a
+    // 16-CPU cgroup quota it must not oversubscribe (round 4 sized it from
+    // the 256 visible CPUs: 8 copy + 8 pread threads, and io8 ran slower than
+    // io1 on a loaded box)
     CopyPool()
     {
-        unsigned hw = std::thread::hardware_concurrency();
-        int n = hw >= 32 ? 8 : hw >= 8 ? 4 : 2;
+        int n = usable_cpus() - 2;
+        n = n < 2 ? 2 : n > 16 ? 16 : n;
         const char *env = getenv("ZSEEK_COPY_THREADS");
         if (env && *env && atoi(env) > 0)
             n = atoi(env);
+        threads_ = n;
         for (int i = 0; i < n; i++)
             std::thread([this] { work(); }).detach();
     }
+    int threads() const { return threads_; }
     void put(const CopyTask &t)
     {
         {
@@ -256,6 +304,7 @@ class CopyPool {
     std::mutex mu_;
     std::condition_variable cv_, done_;
     std::deque<CopyTask> q_;
+    int threads_ = 0;
 };
 
 CopyPool &copy_pool()
@@ -264,6 +313,8 @@ CopyPool &copy_pool()
     return *p;
 }
 }   // namespace
+
+int copy_pool_threads() { return copy_pool().threads(); }
 
 void pool_copy(void *dst, const void *src, size_t n, CopyTicket *t)
 {

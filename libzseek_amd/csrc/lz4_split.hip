@@ -30,6 +30,7 @@
 #include <mutex>
 #include <utility>
 #include <vector>
+#include <vector>
 
 #include "lz4_dev.h"
 #include "pool.h"
@@ -387,21 +388,31 @@ int split_scratch_reserve(SplitScratch *s, uint32_t frames, uint64_t items, hipS
 
 // ---- per-stage launch timing (zsk_kernel_timing / zsk_kernel_times) ----------
 // Events around the stages of each launch on its stream: [plan, parse,
-// execute, hand-off]; read back (and averaged) on request.
+// execute, hand-off]; zstd launches add spans around their per-chunk kernels
+// on the streams those run on (kernel_span_begin / _end; summed per launch in
+// slots kTimedStages..).  Read back on request as the MEDIAN over the launches
+// recorded (a warm-up or a straggler does not move it).
 namespace {
+struct Span3 {
+    int slot;
+    hipEvent_t a, b;
+};
+struct Pend {
+    std::array<hipEvent_t, kTimedStages + 1> ev;
+    std::vector<Span3> spans;
+};
 struct StageTimer {
     std::mutex mu;
     bool on = false;
     std::vector<hipEvent_t> pool;
-    std::vector<std::array<hipEvent_t, kTimedStages + 1>> pend;
-    double sum[kTimedStages] = {};
-    uint64_t n = 0;
+    std::vector<Pend> pend;
+    std::vector<std::array<double, kTimedSlots>> rec;   // per launch
 };
 StageTimer g_timer;
-thread_local std::array<hipEvent_t, kTimedStages + 1> t_ev;
+thread_local Pend t_pend;
 thread_local bool t_active = false;
 
-hipEvent_t timer_event()
+hipEvent_t timer_event()   // (g_timer.mu held)
 {
     if (!g_timer.pool.empty()) {
         hipEvent_t e = g_timer.pool.back();
@@ -412,6 +423,38 @@ hipEvent_t timer_event()
     (void)hipEventCreate(&e);
     return e;
 }
+
+void timer_release(Pend &p)   // (g_timer.mu held)
+{
+    for (auto e : p.ev)
+        g_timer.pool.push_back(e);
+    for (auto &x : p.spans) {
+        g_timer.pool.push_back(x.a);
+        g_timer.pool.push_back(x.b);
+    }
+}
+
+void timer_collect()   // (g_timer.mu held) pending launches -> records
+{
+    for (auto &p : g_timer.pend) {
+        (void)hipEventSynchronize(p.ev[kTimedStages]);
+        std::array<double, kTimedSlots> r{};
+        for (int i = 0; i < kTimedStages; i++) {
+            float t = 0;
+            if (hipEventElapsedTime(&t, p.ev[i], p.ev[i + 1]) == hipSuccess)
+                r[i] = t;
+        }
+        for (auto &x : p.spans) {
+            float t = 0;
+            (void)hipEventSynchronize(x.b);
+            if (hipEventElapsedTime(&t, x.a, x.b) == hipSuccess)
+                r[x.slot] += t;
+        }
+        g_timer.rec.push_back(r);
+        timer_release(p);
+    }
+    g_timer.pend.clear();
+}
 }   // namespace
 
 void stage_mark(int boundary, hipStream_t stream)
@@ -421,53 +464,75 @@ void stage_mark(int boundary, hipStream_t stream)
         t_active = g_timer.on;
         if (!t_active)
             return;
-        for (auto &e : t_ev)
+        for (auto &e : t_pend.ev)
             e = timer_event();
+        t_pend.spans.clear();
     }
     if (!t_active)
         return;
-    (void)hipEventRecord(t_ev[boundary], stream);
+    (void)hipEventRecord(t_pend.ev[boundary], stream);
     if (boundary == kTimedStages) {
         std::lock_guard<std::mutex> g(g_timer.mu);
-        g_timer.pend.push_back(t_ev);
+        g_timer.pend.push_back(t_pend);
+        t_pend.spans.clear();
         t_active = false;
     }
+}
+
+hipEvent_t kernel_span_begin(hipStream_t stream)
+{
+    if (!t_active)
+        return nullptr;
+    hipEvent_t e;
+    {
+        std::lock_guard<std::mutex> g(g_timer.mu);
+        e = timer_event();
+    }
+    (void)hipEventRecord(e, stream);
+    return e;
+}
+
+void kernel_span_end(int slot, hipEvent_t begin, hipStream_t stream)
+{
+    if (!t_active || !begin || slot < kTimedStages || slot >= kTimedSlots)
+        return;
+    hipEvent_t e;
+    {
+        std::lock_guard<std::mutex> g(g_timer.mu);
+        e = timer_event();
+    }
+    (void)hipEventRecord(e, stream);
+    t_pend.spans.push_back({slot, begin, e});
 }
 
 int kernel_timing(int on)
 {
     std::lock_guard<std::mutex> g(g_timer.mu);
-    for (auto &a : g_timer.pend) {
-        (void)hipEventSynchronize(a[kTimedStages]);
-        for (auto e : a)
-            g_timer.pool.push_back(e);
+    for (auto &p : g_timer.pend) {
+        (void)hipEventSynchronize(p.ev[kTimedStages]);
+        for (auto &x : p.spans)
+            (void)hipEventSynchronize(x.b);
+        timer_release(p);
     }
     g_timer.pend.clear();
+    g_timer.rec.clear();
     g_timer.on = on != 0;
-    for (double &x : g_timer.sum)
-        x = 0;
-    g_timer.n = 0;
     return 0;
 }
 
 int kernel_times(double *ms, int cap)
 {
     std::lock_guard<std::mutex> g(g_timer.mu);
-    for (auto &a : g_timer.pend) {
-        (void)hipEventSynchronize(a[kTimedStages]);
-        for (int i = 0; i < kTimedStages; i++) {
-            float t = 0;
-            if (hipEventElapsedTime(&t, a[i], a[i + 1]) == hipSuccess)
-                g_timer.sum[i] += t;
-        }
-        g_timer.n++;
-        for (auto e : a)
-            g_timer.pool.push_back(e);
+    timer_collect();
+    const size_t n = g_timer.rec.size();
+    for (int i = 0; i < cap && i < kTimedSlots; i++) {
+        std::vector<double> v;
+        for (auto &r : g_timer.rec)
+            v.push_back(r[i]);
+        std::sort(v.begin(), v.end());
+        ms[i] = n == 0 ? 0.0 : (n & 1) ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]);
     }
-    g_timer.pend.clear();
-    for (int i = 0; i < cap && i < kTimedStages; i++)
-        ms[i] = g_timer.n ? g_timer.sum[i] / g_timer.n : 0.0;
-    return (int)g_timer.n;
+    return (int)n;
 }
 
 ParseRoute parse_route(uint32_t nframes, int route)

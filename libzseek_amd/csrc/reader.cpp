@@ -342,6 +342,15 @@ size_t batch_end(const SeekTable &st, size_t f, size_t fb, size_t limit)
     return g;
 }
 
+// Concurrent pread callbacks a batch may use: the reader's io_threads, at most
+// half the copy pool (the other half keeps the previous batch's host copies
+// moving: both run on the pool)
+int io_parts(const zseek_reader *r)
+{
+    const int half = copy_pool_threads() / 2;
+    return std::max(1, std::min(r->io_threads, half));
+}
+
 // The batch's compressed span through the user's pread callback: one call
 // at a time (the reference's contract: it calls pread under the reader's
 // lock), or, where the caller allowed it (zsk_reader_set_io_threads), up to
@@ -350,7 +359,7 @@ bool read_span(LaneJob &J, uint8_t *dst, uint64_t len, uint64_t off)
 {
     zseek_reader *r = J.r;
     const uint64_t kPiece = 4u << 20;
-    const int parts = (int)std::min<uint64_t>((uint64_t)r->io_threads, len / kPiece);
+    const int parts = (int)std::min<uint64_t>((uint64_t)io_parts(r), len / kPiece);
     if (parts <= 1) {
         std::lock_guard<std::mutex> io(r->io_lock);
         ssize_t got = r->user_file.pread(dst, len, off, r->user_file.user_data, J.call_data);
@@ -987,6 +996,8 @@ extern "C" ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader, zsk_gp
     std::unique_lock<std::shared_mutex> guard(reader->lock);
     memset(s, 0, sizeof(*s));
     s->device = reader->lanes.empty() ? -1 : reader->lanes[0]->device;
+    s->copy_threads = copy_pool_threads();
+    s->io_parts = io_parts(reader);
     for (auto &l : reader->lanes) {
         s->batches += l->batches;
         s->frames_decoded += l->frames_decoded;

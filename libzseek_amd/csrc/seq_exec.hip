@@ -405,6 +405,108 @@ __device__ __forceinline__ void copy_desc4(const Stage &S, const uint8_t *lbase,
     }
 }
 
+// The first w bytes of a at LDS address d and of b at d + n - w: a run of n
+// bytes (1..32) written whole-width with at most two stores (w = 16, 8, 4, 2
+// or 1 by n; the two overlap below 2w bytes and rewrite equal bytes), never a
+// byte outside [d, d + n).
+__device__ __forceinline__ void put_ends(uint32_t d, uint32_t n, const u32x4 &a, const u32x4 &b)
+{
+    if (n >= 16) {
+        *lp<u32x4_l>(d) = a;
+        *lp<u32x4_l>(d + n - 16) = b;
+    } else if (n >= 8) {
+        *lp<u64_l>(d) = ((uint64_t)a.y << 32) | a.x;
+        *lp<u64_l>(d + n - 8) = ((uint64_t)b.y << 32) | b.x;
+    } else if (n >= 4) {
+        *lp<u32_l>(d) = a.x;
+        *lp<u32_l>(d + n - 4) = b.x;
+    } else if (n >= 2) {
+        *lp<u16_l>(d) = (uint16_t)a.x;
+        *lp<u16_l>(d + n - 2) = (uint16_t)b.x;
+    } else if (n) {
+        *lp<uint8_t>(d) = (uint8_t)a.x;
+    }
+}
+
+// Round 0, direct (round 5): every lane copies its own literal run and its
+// early match (source before the batch) itself -- the run's first bytes and
+// its last bytes (put_ends: all of a run of up to 32 bytes, at most two
+// stores) -- and only the middle 16-byte pieces of runs longer than 32 bytes
+// go through descriptors and the deal.  copy_desc4 sent every piece of every
+// run through the descriptor table (one descriptor loop step per piece of the
+// batch's longest run, ~3 deal slots per batch): the round cost ~300 VALU per
+// 64-sequence batch, 48 % of the execute's.  Literal loads go through the
+// frame's resource (the bytes a run needs lie 4+ bytes before its end: the
+// end mark), match loads through the output's (below `flushed`) or the stage.
+template <int DIAG>
+__device__ __forceinline__ void copy_direct(const Stage &S, const uint8_t *lbase, const Span &lsp,
+                                            const Out &O, uint32_t descs, uint32_t flushed, uint32_t lane,
+                                            uint32_t src, uint32_t op, uint32_t lit, uint32_t msrc, uint32_t mb,
+                                            uint32_t mn)
+{
+    const uint32_t wl = lit >= 16 ? 16 : lit >= 8 ? 8 : lit >= 4 ? 4 : lit >= 2 ? 2 : lit;
+    const uint32_t wm = mn >= 16 ? 16 : mn >= 8 ? 8 : mn >= 4 ? 4 : mn;   // (matches: >= 4 bytes)
+    // loads: the run's first 16 bytes and the 16 from its last w bytes' start
+    const uint32_t lt = src + lit - wl;
+    const u32x4 la = bload16(lsp.r, lit ? lsp.s0 + src : kBad);
+    const u32x4 lb = bload16(lsp.r, lit ? lsp.s0 + lt : kBad);
+    const uint32_t mt = msrc + mn - wm;
+    const bool ha = mn && msrc + 16 <= flushed, hb = mn && mt + 16 <= flushed;
+    const u32x4 ma_h = bload16(O.sp.r, ha ? O.sp.s0 + msrc : kBad);
+    const u32x4 mb_h = bload16(O.sp.r, hb ? O.sp.s0 + mt : kBad);
+    const u32x4 ma_s = lds16(mn && !ha ? saddr(S, msrc) : S.base);
+    const u32x4 mb_s = lds16(mn && !hb ? saddr(S, mt) : S.base);
+    // middle pieces of runs over 32 bytes: [16, n - 16) in 16-byte pieces
+    const uint32_t lpn = lit > 32 ? (lit - 17) >> 4 : 0, mpn = mn > 32 ? (mn - 17) >> 4 : 0;
+    const uint32_t nf = lpn + mpn;
+    const uint32_t inc = wave_incl_add(nf);
+    const uint32_t T = lane_val(inc, 63);
+    put_ends(saddr(S, op), lit, la, lb);
+    put_ends(saddr(S, mb), mn, ha ? ma_h : ma_s, hb ? mb_h : mb_s);
+    if (T == 0)
+        return;
+    const uint64_t dl = ((uint64_t)((saddr(S, op) - S.base) | 16u << 16 | K_LIT << 24) << 32) | src;
+    const uint64_t dm = ((uint64_t)((saddr(S, mb) - S.base) | 16u << 16 | K_HBM << 24) << 32) | msrc;
+    const uint64_t kst = (uint64_t)(K_STAGE - K_HBM) << 56;
+    const uint32_t al = descs + 8 * (inc - nf);
+    for (uint32_t i = 0; __ballot(i < lpn || i < mpn); i++) {
+        const uint32_t o = 16 * i + 16;
+        if (i < lpn)
+            *lp<uint64_t>(al + 8 * i) = dl + (uint64_t)o * 0x100000001ull;
+        if (i < mpn)
+            *lp<uint64_t>(al + 8 * (lpn + i)) = dm + (uint64_t)o * 0x100000001ull + (msrc + o + 16 > flushed ? kst : 0);
+    }
+    wave_lds_sync();
+    for (uint32_t t0 = 0; t0 < T; t0 += 256) {
+        u32x4 v[4];
+        uint32_t dw[4], sx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t t = t0 + 64 * j + lane;
+            const bool on = t < T;
+            const uint64_t D = *lp<uint64_t>(descs + 8 * (on ? t : 0));
+            sx[j] = on ? (uint32_t)D : 0;
+            dw[j] = on ? (uint32_t)(D >> 32) : 0;
+            const uint32_t kind = dw[j] >> 24;
+            const uint8_t *p = kind == K_HBM ? O.o + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);
+            v[j] = *reinterpret_cast<const u32x4_l *>(p);
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (dw[j]) {
+                u32x4 w = v[j];
+                if ((dw[j] >> 24) == K_STAGE)
+                    w = lds16(saddr(S, sx[j]));
+                *lp<u32x4_l>(S.base + (dw[j] & 0xFFFF)) = w;
+            }
+            if (t0 + 64 * j + 64 >= T)
+                break;
+        }
+    }
+}
+
 // A ready match (mn bytes, msrc -> mb, no overlap) whose source lies in this
 // batch: lane-owned pieces, two per step, from the stage (the HBM path only
 // runs when some lane's piece lies below `flushed`).
@@ -857,7 +959,9 @@ __global__ __launch_bounds__(64 * kXW) __attribute__((amdgpu_waves_per_eu(SEG ? 
         produced += lane_val(inc, (int)nb - 1);
         ZSK_T(0)
         // round 0: literal runs + matches whose source precedes the batch
-        if ((DIAG & 8) == 0 && (DIAG & 128) == 0)
+        if ((DIAG & 8) == 0 && (DIAG & 65536))
+            copy_direct<DIAG>(S, lbase, lsp, O, descs, flushed, lane, src, op, lit_n, msrc, mb, early ? ml : 0);
+        else if ((DIAG & 8) == 0 && (DIAG & 128) == 0)
             copy_desc4<DIAG>(S, lbase, lsp, llen, O.o, descs, flushed, lane, src, op, lit_n, msrc, mb,
                              early ? ml : 0);
         else if ((DIAG & 8) == 0)
@@ -1383,6 +1487,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
     case 0x340: ZSK_X(16384); break;  // rounds: readiness by broadcast instead of the LDS search
     case 0x360: ZSK_X(24576); break;  // both
     case 0x380: ZSK_X(32768); break;  // round 0: long runs' descriptors by the whole wave (-0.8 % at 6 waves, +0.5 % at 7)
+    case 0x400: ZSK_X(65536); break;  // round 0 direct (copy_direct)
     case 0x110: {
         unsigned long long z[12] = {0};
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xstats), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);

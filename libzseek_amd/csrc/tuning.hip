@@ -44,6 +44,9 @@ int staged(int stages, int route, int tune, const FrameDesc *d_desc, uint32_t nf
 //              the dependency rounds removed)
 //   0x2xx      plan + lean parse with diagnostic bits xx (lz4_lean.hip;
 //              0x204 prints sub-step counters)
+//   0x400      execute alone with round 0 direct (copy_direct); 0x401 the
+//              whole decode with it; 0x402 the whole decode, production
+//              execute, same scratch (control)
 int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nframes,
                               const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
                               hipStream_t stream)
@@ -65,6 +68,12 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
         return staged(4, ROUTE_AUTO, (variant & 0x3FF) << 8, d_desc, nframes, d_comp, d_out, d_status, stream);
     if ((variant & 0xF00) == 0x200)
         return staged(3, ROUTE_LEAN, variant & 0xFF, d_desc, nframes, d_comp, d_out, d_status, stream);
+    if (variant == 0x400)   // execute alone, round 0 direct (seq_exec.hip copy_direct)
+        return staged(4, ROUTE_AUTO, 0x400 << 8, d_desc, nframes, d_comp, d_out, d_status, stream);
+    if (variant == 0x401)   // the whole decode with it
+        return staged(15, ROUTE_AUTO, 0x400 << 8, d_desc, nframes, d_comp, d_out, d_status, stream);
+    if (variant == 0x402)   // the whole decode through the same scratch, production execute (control)
+        return staged(15, ROUTE_AUTO, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     return -1;
 }
 

@@ -172,9 +172,16 @@ enum : int { ENGINE_AUTO = 0, ENGINE_SPLIT, ENGINE_WAVE };
 
 // Per-stage launch timing: stages [plan, parse, execute, hand-off]; marks
 // 0..4 are the boundaries, recorded as HIP events on the launch's stream
-// while enabled.
+// while enabled.  Slots kTimedStages.. are per-kernel spans a launch sums
+// over its chunks (zstd: frame, sequence, Huffman and execute kernels, each
+// on the stream it runs on): kernel_span_begin returns the begin event
+// (null when timing is off), kernel_span_end closes it.
 constexpr int kTimedStages = 4;
+constexpr int kTimedSlots = 8;
+enum : int { SPAN_ZFRAME = 4, SPAN_ZSEQ = 5, SPAN_ZHUF = 6, SPAN_ZEXEC = 7 };
 void stage_mark(int boundary, hipStream_t stream);
+hipEvent_t kernel_span_begin(hipStream_t stream);
+void kernel_span_end(int slot, hipEvent_t begin, hipStream_t stream);
 
 // HIP streams and events of reader slots and writers: created on the current
 // device (low = the lowest stream priority), destroyed drained at release;

@@ -2508,9 +2508,11 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         if (m == 0)
             continue;
         const uint64_t b0 = s->total[4 + c], b1 = s->total[5 + c];
+        hipEvent_t tf = kernel_span_begin(stream);   // (per-kernel spans: timing on only)
         hipLaunchKernelGGL(zstd_frame_kernel, dim3((m + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc, f1,
                            d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops, s->slots,
                            s->hjobs, f0);
+        kernel_span_end(SPAN_ZFRAME, tf, stream);
         if (hipEventRecord(s->ev_f[c], stream) != hipSuccess || hipStreamWaitEvent(qs, s->ev_f[c], 0) != hipSuccess)
             return drain();
         // the Huffman streams decode beside the sequence replay (neither reads
@@ -2522,6 +2524,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             const uint8_t *jb = s->hjobs + 4 * b0 * sizeof(HufJob);
             uint8_t *hb = s->hbad + 4 * b0;
             const dim3 g((nj + 63) / 64), b(64);
+            hipEvent_t th = kernel_span_begin(hs);
 #ifdef ZSK_TUNING
             // diagnostics (tuning builds, ZSEEK_ZSTD_HUF_DIAG): 1 / 3 / 7 / 8
             // counters and elisions (printed)
@@ -2552,9 +2555,11 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                 fprintf(stderr, "  global %u lds %u\n", z[16], z[17]);
             }
 #endif
+            kernel_span_end(SPAN_ZHUF, th, hs);
             if (hipEventRecord(s->ev_h[c], hs) != hipSuccess)
                 return drain();
         }
+        hipEvent_t tq = kernel_span_begin(qs);
 #ifdef ZSK_TUNING
         // A/B (tuning builds): ZSEEK_ZSTD_SEQ=1 tables from the slot (no LDS),
         // 64 frames per wave; 2: the same, 32 frames per wave; 3: all three
@@ -2577,6 +2582,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells, kSeqGm>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
                            qs, d_desc, f1, d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items,
                            s->nitems, d_status, s->ck, d_fail_at, f0);
+        kernel_span_end(SPAN_ZSEQ, tq, qs);
         if (hipEventRecord(s->ev_s[c], qs) != hipSuccess)
             return drain();
     }
@@ -2593,9 +2599,11 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         if (b1 > b0)
             hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, f1, s->ops,
                                s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at, f0);
+        hipEvent_t tx = kernel_span_begin(stream);
         if (launch_seq_exec_lit(d_desc + f0, m, s->lit, d_out, s->rec_base + f0, s->items, s->nitems + f0,
                                 d_status + f0, stream) != 0)
             rc = -1;
+        kernel_span_end(SPAN_ZEXEC, tx, stream);
         hipLaunchKernelGGL(zstd_check_kernel, dim3((m + 3) / 4), dim3(256), 0, stream, d_desc + f0, m, d_out,
                            s->ck + f0, d_status + f0, d_fail_at ? d_fail_at + f0 : nullptr);
     }

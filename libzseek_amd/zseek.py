@@ -78,7 +78,8 @@ class WriterStatsC(C.Structure):
 class GpuStatsC(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("frames_decoded", C.c_uint64),
                 ("bytes_decoded", C.c_uint64), ("bytes_uploaded", C.c_uint64),
-                ("device_memory", C.c_uint64), ("device", C.c_int)]
+                ("device_memory", C.c_uint64), ("device", C.c_int), ("copy_threads", C.c_int),
+                ("io_parts", C.c_int)]
 
 
 # zsk_frame_desc_t
@@ -692,8 +693,16 @@ def kernel_timing(on: bool) -> None:
     lib().zsk_kernel_timing(1 if on else 0)
 
 
-def kernel_times() -> tuple[int, dict]:
-    """(launches averaged, {stage: average ms}) since kernel_timing(True)."""
-    ms = (C.c_double * 4)()
-    n = lib().zsk_kernel_times(ms, 4)
-    return n, {k: float(ms[i]) for i, k in enumerate(STAGES)}
+ZSTD_KERNEL_SPANS = ("zstd_frame_kernel", "zstd_seq_kernel", "zstd_huf_kernel", "seq_exec_kernel")
+
+
+def kernel_times(spans: bool = False) -> tuple[int, dict]:
+    """(launches recorded, {stage: median ms}) since kernel_timing(True);
+    spans=True adds the zstd per-kernel spans (summed over a launch's
+    chunks, each on its own stream)."""
+    ms = (C.c_double * 8)()
+    n = lib().zsk_kernel_times(ms, 8)
+    out = {k: float(ms[i]) for i, k in enumerate(STAGES)}
+    if spans:
+        out.update({k: float(ms[4 + i]) for i, k in enumerate(ZSTD_KERNEL_SPANS)})
+    return n, out
