@@ -1,0 +1,19 @@
+# Memory-side traffic by request size and by destination (DRAM share) from the
+# L2's EA counters -- exact bytes instead of FETCH_SIZE's derived figure --
+# for the calibration workload and config 2.  One pass per counter group.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-traffic}
+mkdir -p $O
+P1="TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+P2="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum"
+P3="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_WRREQ_DRAM_sum"
+timeout -k 10 300 python scripts/fetch_calib.py --meta $O/meta.json > $O/calib_run.log 2>&1 || { tail -5 $O/calib_run.log; exit 1; }
+i=0
+for P in "$P1" "$P2" "$P3"; do
+  i=$((i+1))
+  timeout -s KILL 200 rocprofv3 --pmc $P --output-format csv -d $O/calib_p$i -- python scripts/fetch_calib.py > $O/calib_p$i.log 2>&1 || { tail -5 $O/calib_p$i.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d $O/c2_p$i -- python bench.py --profile --steps 2 --warmup 1 > $O/c2_p$i.log 2>&1 || { tail -5 $O/c2_p$i.log; exit 1; }
+done
+python3 scripts/traffic_summary.py $O > $O/traffic.txt && cat $O/traffic.txt
