@@ -1111,7 +1111,8 @@ __device__ uint32_t g_fdiag;   // ZSEEK_FRAME_DIAG: 1 no literal copies, 2 no li
 __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
-    int32_t *__restrict__ status, uint32_t *__restrict__ fail_at, uint32_t stop_last, uint32_t handoff)
+    int32_t *__restrict__ status, uint32_t *__restrict__ fail_at, uint32_t stop_last, uint32_t handoff,
+    const uint8_t *__restrict__ lit)
 {
     __shared__ __attribute__((aligned(16))) uint8_t ob[kFMax + 80];
     __shared__ __attribute__((aligned(16))) uint8_t cs[kFCStage + 80];
@@ -1135,19 +1136,22 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const uint32_t nit = nitems[f];
     const uint32_t stop = f + 1 == n ? min(stop_last, d.d_size) : d.d_size;
     const uint64_t *it = items + rec_base[f];
-    const Span lsp = make_span(comp + d.c_off, d.c_size);
+    // literal source: the compressed frame (LZ4), or the frame's decoded
+    // literals (zstd scratch laid out like the output, 16 bytes of slack)
+    const uint32_t llen = lit ? d.d_size + 16 : d.c_size;
+    const Span lsp = make_span(lit ? lit + d.d_off : comp + d.c_off, llen);
     const uint32_t ob0 = (uint32_t)(uintptr_t)ob, cs0 = (uint32_t)(uintptr_t)cs;
 #ifdef ZSK_TUNING
     uint64_t tmark_ = __builtin_readcyclecounter();
     if (t == 0)
         atomicAdd(&g_ftime[7], 1ull);
 #endif
-    // the compressed frame into LDS (four 16-byte loads per thread issued
+    // the literal source into LDS (its 16-byte loads per thread issued
     // together), so a literal run is copied LDS to LDS instead of waiting on an
-    // L2 / HBM load per 16 bytes; a frame too big for the stage reads HBM
-    const bool staged = d.c_size <= kFCStage;
+    // L2 / HBM load per 16 bytes; a source too big for the stage reads HBM
+    const bool staged = llen <= kFCStage;
     if (staged) {
-        const uint32_t np = (d.c_size + 15) / 16;
+        const uint32_t np = (llen + 15) / 16;
         constexpr uint32_t kQ = (kFCStage / 16 + kFT - 1) / kFT;
         u32x4 v[kQ];
 #pragma unroll
@@ -1515,7 +1519,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                            const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                            int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                           bool handoff)
+                           bool handoff, const uint8_t *lit)
 {
     if (nframes == 0)
         return 0;
@@ -1531,7 +1535,7 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
     }
 #endif
     hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
-                       rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff ? 1u : 0u);
+                       rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff && !lit ? 1u : 0u, lit);
 #ifdef ZSK_TUNING
     if (timers && ++calls % 100 == 0) {
         unsigned long long z[8] = {0};
@@ -1549,13 +1553,20 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
 
 int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *lit,
                         uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
-                        const uint32_t *nitems, const int32_t *d_status, hipStream_t stream)
+                        const uint32_t *nitems, int32_t *d_status, hipStream_t stream, bool one,
+                        uint32_t max_dsize)
 {
     if (nframes == 0)
         return 0;
+    if (one) {   // frames of <= 64 KiB a workgroup each, bigger ones a wave
+        hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, nullptr,
+                           d_out, rec_base, items, nitems, d_status, nullptr, 0xFFFFFFFFu, 0u, lit);
+        if (max_dsize <= kFMax)
+            return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit, nullptr,
-                       nullptr, nullptr, nullptr, 0xFFFFFFFFu, 0u);
+                       nullptr, nullptr, nullptr, 0xFFFFFFFFu, one ? kFMax + 1 : 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

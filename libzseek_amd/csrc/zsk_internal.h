@@ -214,16 +214,20 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                            const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                            int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                           bool handoff);
+                           bool handoff, const uint8_t *lit = nullptr);
 int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         const int32_t *d_status, hipStream_t stream, const SplitScratch *blk);
 
 // Execute phase over items whose literal runs come from a literal scratch
 // laid out like the output (zstd): frame f's literals at lit + d_off[f].
+// one: the one-frame route's execute (a workgroup per frame of <= 64 KiB;
+// max_dsize, the batch's largest frame, says whether a wave kernel for bigger
+// ones is needed too).
 int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *lit,
                         uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
-                        const uint32_t *nitems, const int32_t *d_status, hipStream_t stream);
+                        const uint32_t *nitems, int32_t *d_status, hipStream_t stream, bool one = false,
+                        uint32_t max_dsize = 0xFFFFFFFFu);
 
 // zstd decoder (zstd_decode.hip): plan (item bounds -> rec_base[0..n]) and
 // decode (frame kernel -> items + literal scratch, execute, checksums).
@@ -241,7 +245,7 @@ struct ZstdScratch {
     uint8_t *hjobs = nullptr;      // Huffman stream jobs, 4 per block, 32 B each
     uint8_t *slots = nullptr;      // per-block decoding tables (kZSlot bytes each)
     uint8_t *hbad = nullptr;       // per Huffman stream: 1 = corrupt
-    // [0] item total, [1] output extent, [2] blocks, [3] -, [4 + k] blk_base
+    // [0] item total, [1] output extent, [2] blocks, [3] largest frame (d_size), [4 + k] blk_base
     // at chunk boundary k (zstd_decode.hip: the decode runs in chunks)
     uint64_t *d_total = nullptr;
     uint64_t *total = nullptr;     // pinned host copy of d_total

@@ -29,7 +29,9 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -1067,9 +1069,14 @@ __global__ __launch_bounds__(256) void zstd_plan_kernel(const FrameDesc *__restr
         d = desc[f];
     // the output extent max(d_off + d_size), a wave at a time (the scan then
     // reads no descriptors)
+    // (and the largest frame, extent[2]: whether the one-frame route's
+    // execute needs a wave kernel beside its workgroups)
     const uint64_t wx = wave_max64(f < n ? d.d_off + d.d_size : 0ull);
+    const uint64_t wd = wave_max64(f < n ? d.d_size : 0ull);
     if ((threadIdx.x & 63) == 0 && wx)
         atomicMax(extent, (unsigned long long)wx);
+    if ((threadIdx.x & 63) == 0 && wd)
+        atomicMax(extent + 2, (unsigned long long)wd);
     if (f >= n)
         return;
     const Span sp = make_span(comp + d.c_off, d.c_size);
@@ -1738,6 +1745,8 @@ __device__ __forceinline__ void lput3(const LSink &S, uint32_t n, uint64_t v0, u
 // the 8-byte item format of lz4_split.hip (Sink), with the full offset in
 // extended items (an extended pair never starts in slot 63 of a 64-slot
 // group: a zero item pads it)
+// (ONE: every lane runs the emit in step; lane 0's stores land)
+template <bool ONE = false>
 __device__ __forceinline__ bool lemit(LSink &S, uint32_t src, uint32_t lit, uint32_t off, uint32_t ml)
 {
     const bool ext = lit > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF;
@@ -1746,7 +1755,7 @@ __device__ __forceinline__ bool lemit(LSink &S, uint32_t src, uint32_t lit, uint
     const bool ok = S.k + n <= S.cap;
     const uint64_t e0 = ((uint64_t)off << 32) | src | kItemExt, e1 = ((uint64_t)ml << 32) | lit;
     const uint64_t sh = ((uint64_t)(off | lit << 16 | (ml ? ml - 3 : 0) << 24) << 32) | src;
-    lput3(S, ok ? n : 0, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
+    lput3(S, ok && (!ONE || lane_id() == 0) ? n : 0, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
     S.k += ok ? n : 0;
     return ok;
 }
@@ -1768,7 +1777,11 @@ struct SRd {
     uint32_t r1, r0;    // the two dwords below C
     u32x4 L;            // the window in flight (sr_issue -> sr_use)
     int32_t D;
+    uint32_t sl;        // the one-frame route: the stream's dwords staged at this LDS address (0: not)
+    uint32_t zv;        // (ONE) an opaque per-lane zero added to LDS addresses (below)
 };
+
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
 
 // len >= 1.  False when the stream's last byte (its end mark) is 0.
 __device__ __forceinline__ bool sr_init(SRd &b, __amdgpu_buffer_rsrc_t r, uint32_t x, uint32_t len)
@@ -1777,7 +1790,8 @@ __device__ __forceinline__ bool sr_init(SRd &b, __amdgpu_buffer_rsrc_t r, uint32
     b.x0 = x & ~3u;
     b.xs = 8 * (int32_t)(x & 3u);
     const uint32_t rel = (x & 3u) + len;
-    const uint32_t last = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, b.x0 + rel - 1, 0, 0);
+    const uint32_t last = b.sl ? (uint32_t)*la<uint8_t>(b.sl + rel - 1)
+                               : (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, b.x0 + rel - 1, 0, 0);
     b.cur = 8 * (int32_t)(rel - 1) + (last ? 31 - __builtin_clz(last) : 0);
     return last != 0;
 }
@@ -1788,11 +1802,15 @@ __device__ __forceinline__ bool sr_init(SRd &b, __amdgpu_buffer_rsrc_t r, uint32
 // dwords below the base reading as 0), sr_use unpacks it where it is first
 // needed -- a sequence's window is issued at the end of the one before,
 // ahead of that one's item stores
+template <bool ONE>
 __device__ __forceinline__ void sr_issue(SRd &b)
 {
     const int32_t D = (b.cur + 31) >> 5, k0 = D - 4;   // dwords [k0, D) hold bits [32 k0, 32 D)
-    b.L = __builtin_bit_cast(
-        u32x4, __builtin_amdgcn_raw_buffer_load_b128(b.r, b.x0 + 4u * (uint32_t)(k0 > 0 ? k0 : 0), 0, 0));
+    if (ONE && b.sl)
+        b.L = *la<u32x4_a4>(b.sl + 4u * (uint32_t)(k0 > 0 ? k0 : 0) + b.zv);
+    else
+        b.L = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(b.r, b.x0 + 4u * (uint32_t)(k0 > 0 ? k0 : 0), 0, 0));
     b.D = D;
 }
 
@@ -1822,9 +1840,10 @@ __device__ __forceinline__ void sr_use(SRd &b)
     b.r0 = w.x;
 }
 
+template <bool ONE>
 __device__ __forceinline__ void sr_load(SRd &b)
 {
-    sr_issue(b);
+    sr_issue<ONE>(b);
     sr_use(b);
 }
 
@@ -1897,8 +1916,23 @@ __device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
 constexpr uint32_t kSeqLanes = 32;
 constexpr uint32_t kSeqCells = 544;   // u16 cells per frame (LL + ML 512 + copy slack)
 constexpr uint32_t kSeqGm = 2;        // OF from the slot
+// ONE (the one-frame route, a request's few frames): a wave per frame, every
+// lane replaying the same frame in step (one lane's item stores land), with
+// all three tables (up to 512 + 256 + 512 cells) and each block's sequence
+// bitstream (up to kSeqStage bytes) staged in LDS by the whole wave.  A lone
+// frame's replay is one dependent chain: with the window and the OF cell read
+// from L2 / HBM per sequence it ran at ~0.8 us per sequence (853 us for a
+// 64 KiB frame); from LDS the chain waits on LDS latency only.
+constexpr uint32_t kSeqOneCells = 1312;
+constexpr uint32_t kSeqStage = 32768;
+#ifdef ZSK_TUNING
+// tuning builds, ONE: [0] kernel cycles, [1] sequence-loop cycles, [2]
+// sequences, [3] kernel real-time ticks (100 MHz), [4] frames; printed under
+// ZSEEK_SEQ_TIMERS
+__device__ unsigned long long g_sdiag[8];
+#endif
 
-template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0>
+template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false>
 __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
@@ -1907,13 +1941,20 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at, uint32_t f0)
 {
     __shared__ uint32_t codes[89];
-    __shared__ __attribute__((aligned(16))) uint16_t ftab[CELLS ? LANES * CELLS : 8];
+    __shared__ __attribute__((aligned(16))) uint16_t ftab[CELLS && !ONE ? LANES * CELLS : 8];
+    __shared__ __attribute__((aligned(16))) uint8_t sstage[ONE ? kSeqStage + 32 : 16];
+    __shared__ uint64_t xtab[ONE ? kSeqOneCells : 1];   // ONE: the expanded cells (below)
+    __shared__ __attribute__((aligned(16))) uint32_t srec[ONE ? 64 * 4 : 4];   // ONE: a batch's records
+#ifdef ZSK_TUNING
+    const uint64_t tk0 = __builtin_readcyclecounter(), rt0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t tloop = 0, nseqs = 0;
+#endif
     for (uint32_t i = threadIdx.x; i < 89; i += 64)
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
     __syncthreads();
     const uint32_t lane = threadIdx.x;
-    const uint32_t f = f0 + blockIdx.x * LANES + lane;   // frames [f0, n)
-    const bool act = lane < LANES && f < n;
+    const uint32_t f = ONE ? f0 + blockIdx.x : f0 + blockIdx.x * LANES + lane;   // frames [f0, n)
+    const bool act = (ONE || lane < LANES) && f < n;
     FrameDesc d = {0, 0, 0, 0};
     if (act)
         d = desc[f];
@@ -1938,7 +1979,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     LSink S;
     S.k = 0;
     S.cap = icap;
-    uint16_t *const mytab = &ftab[CELLS ? lane * CELLS : 0];
+    uint16_t *const mytab = &ftab[CELLS && !ONE ? lane * CELLS : 0];
     const uint32_t cap = d.d_size;
     uint32_t o = 0, o0 = 0, rep0 = 1, rep1 = 4, rep2 = 8;
     uint64_t c = 0;
@@ -1970,7 +2011,20 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                 const uint32_t le = P.d + P.e;
                 if (nseq) {
                     SRd b;
-                    if (P.c == 0 || !sr_init(b, r, (uint32_t)(d.c_off - base) + P.b, P.c)) {
+                    b.sl = 0;
+                    b.zv = 0;
+                    const uint32_t sx = (uint32_t)(d.c_off - base) + P.b;
+                    if (ONE && P.c != 0 && (sx & 3u) + P.c + 16 <= kSeqStage) {
+                        // the stream's dwords into LDS, 16 bytes per lane per step
+                        const uint32_t x0 = sx & ~3u, nb = (sx & 3u) + P.c, sl = ldsaddr(sstage);
+                        wave_lds_sync();
+                        for (uint32_t q = 16 * lane; q < nb; q += 1024)
+                            *la<u32x4_a4>(sl + q) =
+                                __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, x0 + q, 0, 0));
+                        wave_lds_sync();
+                        b.sl = sl;
+                    }
+                    if (P.c == 0 || !sr_init(b, r, sx, P.c)) {
                         err = ZE_CORRUPT;
                     } else {
                         const uint32_t tll = P.g & 15, tof = (P.g >> 4) & 15, tml = (P.g >> 8) & 15;
@@ -1979,27 +2033,175 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)P.f * kZSlot + kSlotFse);
                         const uint32_t nll = 1u << tll, nof = 1u << tof, nml = 1u << tml;
                         const uint16_t *TL = gt + kFseOff[0], *TO = gt + kFseOff[1], *TM = gt + kFseOff[2];
+                      if constexpr (ONE) {
+                        // the one-frame replay: every cell expanded once by the
+                        // wave into 8 bytes -- next-state base (16 bits), its bit
+                        // count (7), a bad-symbol flag (bit 23), the value's extra
+                        // bits (8) | the value's baseline (32) -- so a sequence's
+                        // chain is one LDS read per table (no code-table read,
+                        // no next-state arithmetic); each sequence's next cells
+                        // are read as soon as its states are known, ahead of its
+                        // checks and item stores.  Same bit order, values and
+                        // checks as the loop below.
+                        const uint32_t xb = ldsaddr(xtab), ncell = nll + nof + nml;
+                        wave_lds_sync();
+                        for (uint32_t cix = lane; cix < ncell; cix += 64) {
+                            const uint32_t t = cix < nll ? 0u : cix < nll + nof ? 1u : 2u;
+                            const uint32_t x = cix - (t == 0 ? 0u : t == 1 ? nll : nll + nof);
+                            const uint32_t e = t == 0 ? TL[x] : t == 1 ? TO[x] : TM[x];
+                            const uint32_t tl = t == 0 ? tll : t == 1 ? tof : tml;
+                            const uint32_t sym = e & 63, ns = e >> 6;
+                            const uint32_t nbits = tl + (uint32_t)__builtin_clz(ns) - 31;
+                            const uint32_t nbase = (ns << nbits) - (1u << tl);
+                            const bool bad = sym > (t == 0 ? 35u : t == 1 ? 31u : 52u);
+                            // OF: value 2^code + code extra bits; LL / ML: the code table
+                            const uint32_t code = bad || t == 1 ? 0u : codes[t == 0 ? sym : 36 + sym];
+                            const uint32_t base = bad ? 0u : t == 1 ? 1u << sym : code & 0xFFFFFF;
+                            const uint32_t add = bad ? 0u : t == 1 ? sym : code >> 24;
+                            const uint32_t lo32 = (nbase & 0xFFFF) | (nbits & 0x7F) << 16 | (bad ? 1u : 0u) << 23 | add << 24;
+                            *la<uint64_t>(xb + 8 * cix) = (uint64_t)base << 32 | lo32;
+                        }
+                        wave_lds_sync();
+                        // (an opaque per-lane zero in the addresses keeps the chain
+                        // in VGPRs: scalarized, each LDS result waited for and
+                        // copied to SGPRs at once -- the window's and the cells'
+                        // reads no longer in flight together)
+                        uint32_t zv;
+                        asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
+                        b.zv = zv;
+                        auto XL = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * x + zv); };
+                        auto XO = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * (nll + x) + zv); };
+                        auto XM = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * (nll + nof + x) + zv); };
+                        auto nxt = [&](uint64_t cell) {
+                            return ((uint32_t)cell & 0xFFFF) + sr_take(b, ((uint32_t)cell >> 16) & 0x7F);
+                        };
+                        sr_load<ONE>(b);
+                        uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
+                        sr_done(b);
+                        sr_issue<ONE>(b);
+                        uint64_t cl = XL(sll), co = XO(sof), cm = XM(sml);
+#ifdef ZSK_TUNING
+                        const uint64_t tl0 = __builtin_readcyclecounter();
+                        nseqs += nseq;
+#endif
+                        // batches of up to 64 sequences: (1) the chain, wave-
+                        // uniform -- cells, bits, next states, repeat offsets and
+                        // item slots -> one 16-byte record per sequence in LDS,
+                        // stopping at a bad cell; (2) lane q takes record q: the
+                        // output / literal prefix sums, the replay's four checks
+                        // in its order, the first failing sequence by ballot, and
+                        // the items of the sequences before it (a lane's own
+                        // stores).  Everything the serial loop below leaves --
+                        // items, o, lp_, S.k, err -- is the same.
+                        const uint32_t rec = ldsaddr(srec);
+                        uint32_t kk = S.k;   // item slot of the chain's next sequence
+                        for (uint32_t i = 0; i < nseq && !err;) {
+                            const uint32_t nb = min(64u, nseq - i);
+                            uint32_t nd = 0;
+                            bool afail = false;
+                            wave_lds_sync();   // the last batch's records read
+                            for (; nd < nb; nd++) {
+                                sr_use(b);
+                                if ((((uint32_t)cl | (uint32_t)co | (uint32_t)cm) >> 23) & 1) {
+                                    afail = true;
+                                    break;
+                                }
+                                const uint32_t ofv = (uint32_t)(co >> 32) + sr_take(b, (uint32_t)co >> 24);
+                                sr_fill(b);
+                                const uint32_t ml = (uint32_t)(cm >> 32) + sr_take(b, (uint32_t)cm >> 24);
+                                const uint32_t ll = (uint32_t)(cl >> 32) + sr_take(b, (uint32_t)cl >> 24);
+                                sr_fill(b);
+                                sll = nxt(cl);
+                                sml = nxt(cm);
+                                sof = nxt(co);
+                                sr_done(b);
+                                sr_issue<ONE>(b);
+                                cl = XL(sll);
+                                co = XO(sof);
+                                cm = XM(sml);
+                                const bool fresh = ofv > 3;
+                                const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
+                                const uint32_t off = fresh ? ofv - 3
+                                                     : idx == 0 ? rep0
+                                                     : idx == 1 ? rep1
+                                                     : idx == 2 ? rep2
+                                                                : max(rep0 - 1, 1u);
+                                const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
+                                rep2 = sh2 ? rep1 : rep2;
+                                rep1 = sh1 ? rep0 : rep1;
+                                rep0 = sh1 ? off : rep0;
+                                // lemit's slot rule: an extended pair never starts in slot 63 of a group
+                                const bool ext = ll > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF;
+                                const uint32_t pad = ext && (kk & 63) == 63 ? 1u : 0u;
+                                *la<u32x4>(rec + 16 * nd) = (u32x4){off, ml, ll, kk | (ext ? 1u : 0u) << 30 | pad << 31};
+                                kk += ext ? 2 + pad : 1;
+                            }
+                            wave_lds_sync();
+                            const bool on = lane < nd;
+                            const u32x4 R = on ? *la<u32x4>(rec + 16 * lane) : (u32x4){0, 0, 0, 0};
+                            const uint32_t off = R.x, ml = R.y, ll = R.z, kq = R.w & 0x3FFFFFFF;
+                            const bool ext = (R.w >> 30) & 1;
+                            const uint32_t pad = R.w >> 31, ni = ext ? 2 + pad : 1;
+                            const uint32_t ill = wave_incl_add(ll), iol = wave_incl_add(ll + ml);
+                            const uint32_t lpq = lp_ + ill - ll, oq = o + iol - (ll + ml);
+                            const uint32_t kind = ll + ml > cap - oq ? (uint32_t)ZE_DST_SMALL
+                                                  : le - lpq < ll    ? (uint32_t)ZE_CORRUPT
+                                                  : off > oq + ll    ? (uint32_t)ZE_CORRUPT
+                                                  : kq + ni > S.cap  ? (uint32_t)ZE_GENERIC
+                                                                     : 0u;
+                            const uint64_t em = __ballot(on && kind != 0);
+                            const uint32_t e = em ? (uint32_t)__builtin_ctzll(em) : nd;
+                            if (lane < e) {
+                                const uint64_t e0 = ((uint64_t)off << 32) | lpq | kItemExt, e1 = ((uint64_t)ml << 32) | ll;
+                                const uint64_t sh = ((uint64_t)(off | ll << 16 | (ml ? ml - 3 : 0) << 24) << 32) | lpq;
+                                LSink Q = S;
+                                Q.k = kq;
+                                lput3(Q, ni, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
+                            }
+                            if (e > 0) {
+                                lp_ += lane_val(ill, (int)e - 1);
+                                o += lane_val(iol, (int)e - 1);
+                            }
+                            if (e < nd) {
+                                err = lane_val(kind, (int)e);
+                                S.k = lane_val(kq, (int)e);
+                            } else {
+                                S.k = kk;
+                                if (afail)
+                                    err = ZE_CORRUPT;
+                            }
+                            i += nd;
+                        }
+#ifdef ZSK_TUNING
+                        tloop += __builtin_readcyclecounter() - tl0;
+#endif
+                      } else {
                         // cells staged in LDS per table (0: read from the slot)
                         const uint32_t nlll = (GM & 1) ? 0u : nll, nofl = (GM & 2) ? 0u : nof,
                                        nmll = (GM & 4) ? 0u : nml;
                         const bool fit = nlll + nofl + nmll == 0 || (CELLS && nlll + nofl + nmll + 32 <= CELLS);
                         if (fit) {
+                            // (ONE: the whole wave copies, 8 cells per lane per step)
                             auto cp = [&](const uint16_t *src, uint32_t at, uint32_t cells) {
-                                for (uint32_t c = 0; c < cells; c += 8)
+                                for (uint32_t c = ONE ? 8 * lane : 0; c < cells; c += ONE ? 512 : 8)
                                     *reinterpret_cast<u32x4 *>(mytab + at + c) = *reinterpret_cast<const u32x4 *>(src + c);
                             };
+                            if (ONE)
+                                wave_lds_sync();
                             cp(TL, 0, nlll);
                             cp(TO, nlll, nofl);
                             cp(TM, nlll + nofl, nmll);
+                            if (ONE)
+                                wave_lds_sync();
                         }
                         // the sequence loop, over tables in LDS (ds_read: the
                         // lookups' waits stay off vmcnt) or in the slot
                         auto seqs = [&](auto TLf, auto TOf, auto TMf) {
-                            sr_load(b);
+                            sr_load<ONE>(b);
 
                             uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
                             sr_done(b);
-                            sr_issue(b);
+                            sr_issue<ONE>(b);
                             // three disabled stores: the loop's entry then has the
                             // VMEM pattern of its back edge (window, then three
                             // stores), so the window's wait stays vmcnt(3)
@@ -2055,7 +2257,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 if (GM & 4)
                                     eml_n = TMf(sml);
                                 sr_done(b);
-                                sr_issue(b);
+                                sr_issue<ONE>(b);
                                 // o <= cap: no 32-bit overflow in these tests
                                 if (ll + ml > cap - o)
                                     err = ZE_DST_SMALL;
@@ -2086,6 +2288,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         else
                             seqs([&](uint32_t x) -> uint32_t { return TL[x]; }, [&](uint32_t x) -> uint32_t { return TO[x]; },
                                  [&](uint32_t x) -> uint32_t { return TM[x]; });
+                      }
                         if (!err && b.cur - b.xs > 0)
                             err = ZE_CORRUPT;
                     }
@@ -2094,7 +2297,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                     const uint32_t last = le - lp_;
                     if (o + last > cap)
                         err = ZE_DST_SMALL;
-                    else if (last && !lemit(S, lp_, last, 0, 0))
+                    else if (last && !lemit<ONE>(S, lp_, last, 0, 0))
                         err = ZE_GENERIC;
                     else
                         o += last;
@@ -2102,7 +2305,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
             } else if (P.k == OP_RUN) {
                 if (P.b > cap - o)
                     err = ZE_DST_SMALL;
-                else if (P.b && !lemit(S, P.a, P.b, 0, 0))
+                else if (P.b && !lemit<ONE>(S, P.a, P.b, 0, 0))
                     err = ZE_GENERIC;
                 else
                     o += P.b;
@@ -2132,7 +2335,8 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     auto irsrc = [&](uint64_t a, uint64_t b) {
         return __builtin_amdgcn_make_buffer_rsrc((void *)(items + a), 0, (int)(uint32_t)(8 * (b - a)), kRsrcDw3);
     };
-    if (hi > lo && hi - lo < kMaxSpan && 8 * (ihi - ilo) < kMaxSpan) {
+    if (ONE || (hi > lo && hi - lo < kMaxSpan && 8 * (ihi - ilo) < kMaxSpan)) {
+        // (ONE: one frame's span, < 4 GiB compressed and items)
         replay(span_rsrc(comp, lo, hi - lo), lo, irsrc(ilo, ihi), ilo);
     } else {
         for (uint64_t m = __ballot(true); m; m &= m - 1) {
@@ -2144,6 +2348,17 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                 replay(span_rsrc(comp, s0, s1 - s0), s0, irsrc(i0, i1), i0);
         }
     }
+    if (ONE && lane != 0)
+        return;
+#ifdef ZSK_TUNING
+    if (ONE) {
+        atomicAdd(&g_sdiag[0], (unsigned long long)(__builtin_readcyclecounter() - tk0));
+        atomicAdd(&g_sdiag[1], (unsigned long long)tloop);
+        atomicAdd(&g_sdiag[2], (unsigned long long)nseqs);
+        atomicAdd(&g_sdiag[3], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rt0));
+        atomicAdd(&g_sdiag[4], 1ull);
+    }
+#endif
     status[f] = st;
     nitems[f] = S.k;
     ck[f] = c;
@@ -2490,6 +2705,13 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         return -1;
     const uint32_t K = zstd_chunks(nframes);
     static const bool serial = getenv("ZSEEK_ZSTD_SERIAL") != nullptr;   // diagnostics: one stream
+    // the one-frame route (a request's few frames): the execute a workgroup
+    // per frame (env ZSEEK_ONE_ROUTE=0: the wave kernels, as round 4)
+    static const bool one_off = [] {
+        const char *v = getenv("ZSEEK_ONE_ROUTE");
+        return v && !strcmp(v, "0");
+    }();
+    const bool one = !one_off && nframes <= kOneMaxFrames;
     hipStream_t const hs = serial ? stream : s->side, qs = serial ? stream : s->sq;
 #ifdef ZSK_TUNING
     static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
@@ -2579,6 +2801,28 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                                s->ck, d_fail_at, f0);
         else
 #endif
+        if (one) {
+            hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true>), dim3(m), dim3(64), 0, qs, d_desc, f1,
+                               d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
+                               d_status, s->ck, d_fail_at, f0);
+#ifdef ZSK_TUNING
+            static const bool timers = getenv("ZSEEK_SEQ_TIMERS") != nullptr;
+            static int calls = 0;
+            if (timers && ++calls % 100 == 0) {
+                unsigned long long z[8] = {0};
+                (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_sdiag), sizeof(z), 0, hipMemcpyDeviceToHost, qs);
+                (void)hipStreamSynchronize(qs);
+                const double fr = z[4] ? (double)z[4] : 1.0, sq = z[2] ? (double)z[2] : 1.0;
+                fprintf(stderr,
+                        "one-frame sequences: kernel %.0f cycles (%.1f us, %.0f MHz) per frame, loop %.0f cycles "
+                        "(%.0f per sequence, %.0f sequences per frame)\n",
+                        z[0] / fr, z[3] / fr / 100.0, z[3] ? z[0] * 100.0 / z[3] : 0.0, z[1] / fr, z[1] / sq, sq / fr);
+            }
+        }
+#else
+        }
+#endif
+        else
         hipLaunchKernelGGL((zstd_seq_kernel<kSeqLanes, kSeqCells, kSeqGm>), dim3((m + kSeqLanes - 1) / kSeqLanes), dim3(64), 0,
                            qs, d_desc, f1, d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items,
                            s->nitems, d_status, s->ck, d_fail_at, f0);
@@ -2601,7 +2845,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                                s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at, f0);
         hipEvent_t tx = kernel_span_begin(stream);
         if (launch_seq_exec_lit(d_desc + f0, m, s->lit, d_out, s->rec_base + f0, s->items, s->nitems + f0,
-                                d_status + f0, stream) != 0)
+                                d_status + f0, stream, one, (uint32_t)std::min<uint64_t>(s->total[3], 0xFFFFFFFFu)) != 0)
             rc = -1;
         kernel_span_end(SPAN_ZEXEC, tx, stream);
         hipLaunchKernelGGL(zstd_check_kernel, dim3((m + 3) / 4), dim3(256), 0, stream, d_desc + f0, m, d_out,

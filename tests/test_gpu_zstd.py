@@ -142,9 +142,13 @@ def test_device_zstd_three_chunk_pipeline(gpu, zs, nframes):
     assert b"".join(out) == data.tobytes()
 
 
-def test_device_zstd_corrupt_status(gpu, zs, oracle, zstd):
+@pytest.mark.parametrize("batch", [0, 40])
+def test_device_zstd_corrupt_status(gpu, zs, oracle, zstd, batch):
     """single-byte corruptions and truncations: every frame's status is the
-    libzstd error code the oracle gives, intact frames decode bit-exact"""
+    libzstd error code the oracle gives, intact frames decode bit-exact --
+    all 198 frames in one batch (a lane per frame), and in batches of 40 (the
+    one-frame route: a wave per frame's sequences, a workgroup per frame's
+    execute)"""
     rng = np.random.default_rng(3)
     data = datasets(oracle)
     frames, sizes = [], []
@@ -159,7 +163,14 @@ def test_device_zstd_corrupt_status(gpu, zs, oracle, zstd):
         for cut in (1, 5, 9, 20, len(comp) // 2, len(comp) - 1):
             frames.append(comp[:cut])
             sizes.append(len(src))
-    out, st = device_decode(zs, gpu, frames, sizes)
+    if batch:
+        out, st = [], []
+        for b in range(0, len(frames), batch):
+            o, t = device_decode(zs, gpu, frames[b: b + batch], sizes[b: b + batch])
+            out += o
+            st += list(t)
+    else:
+        out, st = device_decode(zs, gpu, frames, sizes)
     for i, (f, n) in enumerate(zip(frames, sizes)):
         want, err = oracle.zstd_decode(f, n)
         if err:
