@@ -108,6 +108,8 @@ __device__ __forceinline__ __attribute__((address_space(3))) T *lp(const void *a
     return (__attribute__((address_space(3))) T *)(uintptr_t)(uint32_t)(uintptr_t)a;
 }
 
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+
 template <typename T>
 __device__ __forceinline__ __attribute__((address_space(3))) T *la(uint32_t a)
 {
@@ -128,6 +130,20 @@ __device__ __forceinline__ int32_t hibit(uint32_t v)
 {
     return 31 - __builtin_clz(v);
 }
+
+#ifdef ZSK_TUNING
+// tuning builds: the frame kernel's cycles, lane 0 at section ends: [0]
+// kernel, [1] Huffman descriptions, [2] sequence tables (+ slot cells), [3]
+// window stagings, [4] frames; printed under ZSEEK_ZFRAME_TIMERS
+__device__ unsigned long long g_zftime[8];
+#define ZF_T0(v) const uint64_t v = __builtin_readcyclecounter();
+#define ZF_ADD(i, v)                                                                                  \
+    if (lane_id() == 0)                                                                               \
+        atomicAdd(&g_zftime[i], (unsigned long long)(__builtin_readcyclecounter() - v));
+#else
+#define ZF_T0(v)
+#define ZF_ADD(i, v)
+#endif
 
 // ---- compressed input: coordinates x relative to the frame's 4-aligned base
 struct In {
@@ -160,9 +176,11 @@ __device__ __forceinline__ void dma_wait()
 // the coordinate of win[0]
 __device__ __forceinline__ uint32_t stage_win(ZLds &L, const In &I, uint32_t p)
 {
+    ZF_T0(t0)
     const uint32_t a = (I.s0 + p) & ~3u;
     dma256(I, a, ldsaddr(L.win));
     dma_wait();
+    ZF_ADD(3, t0)
     return a;
 }
 
@@ -737,8 +755,10 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint
             return ZE_CORRUPT;
         const uint32_t x2 = ns == 4 ? huf_select_x2(size, csize) : 0u;
         uint32_t lg = 0;
+        ZF_T0(t0)
         const uint32_t hs =
             huf_read(L, F.I, wx, q, qn, &lg, reinterpret_cast<uint16_t *>(F.slots + g * kZSlot));
+        ZF_ADD(1, t0)
         if (!hs)
             return ZE_CORRUPT;
         F.huf_log = lg;
@@ -897,6 +917,7 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_
         const uint32_t modes = uni(wb(L, wx, F.I, q));
         q++;
         const uint32_t mode[3] = {modes >> 6, (modes >> 4) & 3, (modes >> 2) & 3};
+        ZF_T0(t0)
 #pragma unroll
         for (uint32_t t = 0; t < 3; t++) {
             uint32_t err = 0;
@@ -919,6 +940,7 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_
             }
         }
         tl = F.tlog[0] | F.tlog[1] << 4 | F.tlog[2] << 8;
+        ZF_ADD(2, t0)
     }
     if (!put_op(F, OP_SEQ, nseq, q, qe > q ? qe - q : 0, F.lo, litn, (uint32_t)g, tl))
         return ZE_GENERIC;
@@ -1238,6 +1260,7 @@ __global__ __launch_bounds__(64 * kZW) __attribute__((amdgpu_waves_per_eu(4))) v
     uint8_t *__restrict__ slots, uint8_t *__restrict__ jobs, uint32_t f0)
 {
     __shared__ ZLds lds[kZW];
+    ZF_T0(tk)
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t f = uni(f0 + blockIdx.x * kZW + w);   // frames [f0, n)
     if (f >= n)
@@ -1279,6 +1302,11 @@ __global__ __launch_bounds__(64 * kZW) __attribute__((amdgpu_waves_per_eu(4))) v
         put_op(F, OP_ERR, (uint32_t)zerr(e));
     else
         put_op(F, OP_DONE);
+    ZF_ADD(0, tk)
+#ifdef ZSK_TUNING
+    if (lane_id() == 0)
+        atomicAdd(&g_zftime[4], 1ull);
+#endif
 }
 
 // ---- backward bitstreams, lane per stream -------------------------------------------
@@ -1717,6 +1745,167 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void zs
     hbad[j] = bad ? 1 : 0;
 }
 
+// ---- Huffman literals, the one-frame route: a workgroup per stream ----------------------
+// A lone frame's four streams on four lanes were a 366 us serial chain (~130
+// cycles a symbol: an LDS lookup per symbol).  Here 256 threads split the
+// stream's bits into chunks and decode them at once.  A symbol boundary at a
+// chunk's top is unknown until the chunks above are decoded, but it lies in
+// the top lg bits of the chunk (no code is longer than lg): so each thread
+// decodes its chunk from every one of those lg entry bits (lockstep, ILP over
+// the entries), recording for each entry where the walk leaves the chunk and
+// how many symbols it took.  One thread then follows the true entries from
+// the stream's end mark chunk by chunk (the exit of one chunk is the next
+// one's entry), giving each chunk its entry and output base; a second pass
+// decodes each chunk from its true entry into an LDS copy of the output,
+// written out in 16-byte stores.  Identical bytes to the serial walk (the
+// same cells and bit reads, bits below the stream read as 0): a stream is
+// valid iff the followed walk makes exactly cnt symbols and ends at bit 0.
+// Anything else -- a stream the walk rejects (X2 rescue), too long for the
+// stage, an empty end mark -- is decoded by thread 0 exactly as
+// zstd_huf_kernel's lane does.
+constexpr uint32_t kHufOneT = 256;
+constexpr uint32_t kHufOneStage = 65536;    // stream bytes staged (else the serial walk)
+constexpr uint32_t kHufOneOut = 32768;      // symbols staged (else the serial walk)
+constexpr uint32_t kHufOneMaxLg = 12;
+
+__global__ __launch_bounds__(kHufOneT) void zstd_huf_one_kernel(const uint8_t *__restrict__ jobs,
+                                                                const uint8_t *__restrict__ comp,
+                                                                const uint8_t *__restrict__ slots,
+                                                                uint8_t *__restrict__ lit,
+                                                                uint8_t *__restrict__ hbad)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t sst[16 + kHufOneStage + 32];
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[kHufOneOut + 16];
+    __shared__ __attribute__((aligned(16))) uint16_t tab[1u << kHufOneMaxLg];
+    __shared__ uint32_t cand[kHufOneT * kHufOneMaxLg];   // exit offset | symbols << 8, per chunk and entry
+    __shared__ uint32_t ent[kHufOneT];                   // true entry | output base << 4
+    __shared__ uint32_t verdict;
+    __shared__ __attribute__((aligned(16))) uint8_t rings[kRS * 1024];   // the serial walk's ring
+    const uint32_t j = blockIdx.x, t = threadIdx.x;
+    const HufJob J = reinterpret_cast<const HufJob *>(jobs)[j];
+    if (J.len == 0) {
+        if (t == 0)
+            hbad[j] = 0;
+        return;
+    }
+    const uint32_t lg = J.tab >> 28, jslot = J.tab & kHufSlotMask, jx2 = (J.tab >> 27) & 1;
+    const uint16_t *gt = reinterpret_cast<const uint16_t *>(slots + (uint64_t)jslot * kZSlot);
+    const uint64_t s0 = J.src & ~15ull;
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(comp, s0, J.src + J.len - s0);
+    const uint32_t x = (uint32_t)(J.src - s0);
+    const uint32_t sl = ldsaddr(sst) + 16;
+    bool par = J.len <= kHufOneStage && J.cnt <= kHufOneOut && lg >= 1 && lg <= kHufOneMaxLg;
+    if (par) {
+        // the stream's bytes (16 zero bytes below them), the cells
+        if (t < 4)
+            *la<uint32_t>(sl - 16 + 4 * t) = 0;
+        for (uint32_t q = 16 * t; q < J.len; q += 16 * kHufOneT)
+            *la<u32x4>(sl + q) = load16u(r, x + q);
+        for (uint32_t c = t; c < (1u << lg); c += kHufOneT)
+            tab[c] = gt[c];
+        __syncthreads();
+    }
+    const uint32_t last = par ? (uint32_t)*la<uint8_t>(sl + J.len - 1) : 0u;
+    par = par && last != 0;
+    if (par) {
+        const int32_t S = 8 * (int32_t)(J.len - 1) + (31 - __builtin_clz(last));   // bits below the end mark
+        const uint32_t mask = (1u << lg) - 1;
+        // lg bits below bit p (bit p - 1 most significant); bits below 0 read 0
+        auto cell = [&](int32_t p) -> uint32_t {
+            const int32_t lo = p - (int32_t)lg;
+            const int32_t d = lo >> 5;   // >= -1: the zero bytes below
+            const uint32_t a = (uint32_t)((int32_t)sl + 4 * d);
+            const uint64_t w = (uint64_t)*la<uint32_t>(a) | (uint64_t)*la<uint32_t>(a + 4) << 32;
+            return tab[(uint32_t)(w >> (uint32_t)(lo - 32 * d)) & mask];
+        };
+        // chunks of C >= 16 bits (> lg), at most kHufOneT of them, each with
+        // bits: hi > 0
+        const int32_t C = max<int32_t>(16, (S + (int32_t)kHufOneT - 1) / (int32_t)kHufOneT);
+        const uint32_t T = (uint32_t)max<int32_t>(1, (S + C - 1) / C);
+        const int32_t hi = S - (int32_t)t * C, lo = max(hi - C, 0);
+        if (t < T) {
+            const uint32_t ne = t == 0 ? 1u : lg;
+            int32_t pc[kHufOneMaxLg];
+            uint32_t nc[kHufOneMaxLg];
+#pragma unroll
+            for (uint32_t c = 0; c < kHufOneMaxLg; c++) {
+                pc[c] = hi - (int32_t)c;
+                nc[c] = 0;
+            }
+            for (bool any = true; any;) {
+                any = false;
+#pragma unroll
+                for (uint32_t c = 0; c < kHufOneMaxLg; c++) {
+                    if (c < ne && pc[c] > lo) {
+                        const uint32_t e = cell(pc[c]);
+                        pc[c] -= (int32_t)max(e & 0xFFu, 1u);
+                        nc[c]++;
+                        any = true;
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < kHufOneMaxLg; c++)
+                if (c < ne)
+                    cand[t * kHufOneMaxLg + c] = (uint32_t)(lo - pc[c]) | nc[c] << 8;
+        }
+        __syncthreads();
+        if (t == 0) {
+            uint32_t c = 0, base = 0;
+            for (uint32_t k = 0; k < T; k++) {
+                ent[k] = c | base << 4;
+                const uint32_t v = cand[k * kHufOneMaxLg + c];
+                base += v >> 8;
+                c = v & 0xFF;
+            }
+            verdict = c == 0 && base == J.cnt ? 1u : 0u;
+        }
+        __syncthreads();
+        par = verdict != 0;
+        if (par) {
+            if (t < T) {
+                const uint32_t e0 = ent[t];
+                int32_t p = hi - (int32_t)(e0 & 15);
+                for (uint32_t i = e0 >> 4; p > lo; i++) {
+                    const uint32_t e = cell(p);
+                    obuf[i] = (uint8_t)(e >> 8);
+                    p -= (int32_t)max(e & 0xFFu, 1u);
+                }
+            }
+            __syncthreads();
+            // out: [0, lim) of the decoded symbols, 16-byte stores where aligned
+            uint8_t *out = lit + J.dst;
+            const uint32_t n = J.lim, head = min(n, (uint32_t)((16 - ((uintptr_t)out & 15)) & 15));
+            if (t < head)
+                out[t] = obuf[t];
+            const uint32_t nq = (n - head) / 16;
+            for (uint32_t q = t; q < nq; q += kHufOneT)
+                *reinterpret_cast<u32x4 *>(out + head + 16 * q) = *la<u32x4_u>(ldsaddr(obuf) + head + 16 * q);
+            const uint32_t tail = head + 16 * nq;
+            if (tail + t < n)
+                out[tail + t] = obuf[tail + t];
+            if (t == 0)
+                hbad[j] = 0;
+            return;
+        }
+    }
+    // the serial walk (zstd_huf_kernel's lane), thread 0
+    if (t != 0)
+        return;
+    BRd b;
+    bool bad = !br_init(b, r, x, J.len, ldsaddr(rings));
+    auto Tg = [&](uint32_t i) -> uint32_t { return gt[i]; };
+    huf_stream<2, 2, 0, 4>(b, Tg, lg, lit + J.dst, J.dst, J.cnt, J.lim);
+    bad = bad || br_left(b) != 0;
+    if (bad && jx2) {
+        const uint32_t xr = x2_rescue(r, x, J.len, J.cnt, gt, lg);
+        bad = !(xr & 1);
+        if ((xr & 0x10000) && J.cnt - 1 < J.lim)
+            lit[J.dst + J.cnt - 1] = (uint8_t)(xr >> 8);
+    }
+    hbad[j] = bad ? 1 : 0;
+}
+
 // ---- sequences: one lane per seek-table entry ------------------------------------------
 // Replays the frame's op list: FSE states (tables from the block slots),
 // repeat offsets, every libzstd check, items in the LZ4 item format with the
@@ -1781,8 +1970,6 @@ struct SRd {
     uint32_t zv;        // (ONE) an opaque per-lane zero added to LDS addresses (below)
 };
 
-typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
-
 // len >= 1.  False when the stream's last byte (its end mark) is 0.
 __device__ __forceinline__ bool sr_init(SRd &b, __amdgpu_buffer_rsrc_t r, uint32_t x, uint32_t len)
 {
@@ -1806,21 +1993,26 @@ template <bool ONE>
 __device__ __forceinline__ void sr_issue(SRd &b)
 {
     const int32_t D = (b.cur + 31) >> 5, k0 = D - 4;   // dwords [k0, D) hold bits [32 k0, 32 D)
-    if (ONE && b.sl)
-        b.L = *la<u32x4_a4>(b.sl + 4u * (uint32_t)(k0 > 0 ? k0 : 0) + b.zv);
+    // (ONE: the staged stream has 16 zero bytes below it, bits [-128, 0): a
+    // window wholly below the stream -- a corrupt stream read past its start,
+    // which libzstd 1.4.9 reads as zeros -- is those bytes too)
+    if (ONE)
+        b.L = *la<u32x4_a4>(b.sl + 4u * (uint32_t)(k0 > -4 ? k0 : -4) + b.zv);
     else
         b.L = __builtin_bit_cast(
             u32x4, __builtin_amdgcn_raw_buffer_load_b128(b.r, b.x0 + 4u * (uint32_t)(k0 > 0 ? k0 : 0), 0, 0));
     b.D = D;
 }
 
+template <bool ONE = false>
 __device__ __forceinline__ void sr_use(SRd &b)
 {
     const int32_t D = b.D, k0 = D - 4;
     u32x4 w = b.L;
     // the window reaches the stream's first dword only at a block's last few
-    // sequences: a branch the wave skips, not selects on every sequence
-    if (k0 <= 0) {
+    // sequences: a branch the wave skips, not selects on every sequence (ONE:
+    // the staged copy reads zeros there itself)
+    if (!ONE && k0 <= 0) {
         const u32x4 L = b.L;
         const int32_t sft = -k0;
         w.x = sft == 0 ? L.x : 0u;
@@ -1844,7 +2036,7 @@ template <bool ONE>
 __device__ __forceinline__ void sr_load(SRd &b)
 {
     sr_issue<ONE>(b);
-    sr_use(b);
+    sr_use<ONE>(b);
 }
 
 __device__ __forceinline__ void sr_fill(SRd &b)
@@ -1924,7 +2116,8 @@ constexpr uint32_t kSeqGm = 2;        // OF from the slot
 // from L2 / HBM per sequence it ran at ~0.8 us per sequence (853 us for a
 // 64 KiB frame); from LDS the chain waits on LDS latency only.
 constexpr uint32_t kSeqOneCells = 1312;
-constexpr uint32_t kSeqStage = 32768;
+constexpr uint32_t kSeqStage = 131072 + 64;   // > a block's largest sequences section
+constexpr int kSeqOneV = 0;                    // the chain's bit reads (OV, below)
 #ifdef ZSK_TUNING
 // tuning builds, ONE: [0] kernel cycles, [1] sequence-loop cycles, [2]
 // sequences, [3] kernel real-time ticks (100 MHz), [4] frames; printed under
@@ -1932,7 +2125,7 @@ constexpr uint32_t kSeqStage = 32768;
 __device__ unsigned long long g_sdiag[8];
 #endif
 
-template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false>
+template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false, int OV = 0>
 __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
@@ -2014,17 +2207,29 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                     b.sl = 0;
                     b.zv = 0;
                     const uint32_t sx = (uint32_t)(d.c_off - base) + P.b;
+                    bool staged = !ONE;
                     if (ONE && P.c != 0 && (sx & 3u) + P.c + 16 <= kSeqStage) {
-                        // the stream's dwords into LDS, 16 bytes per lane per step
-                        const uint32_t x0 = sx & ~3u, nb = (sx & 3u) + P.c, sl = ldsaddr(sstage);
+                        // the stream's dwords into LDS, 16 bytes per lane per
+                        // step, after 16 zero bytes; the bytes of its first dword
+                        // below the stream zeroed too (the window's "bits below
+                        // the stream read as 0" without a branch per sequence)
+                        const uint32_t x0 = sx & ~3u, nb = (sx & 3u) + P.c, sl = ldsaddr(sstage) + 16;
                         wave_lds_sync();
                         for (uint32_t q = 16 * lane; q < nb; q += 1024)
                             *la<u32x4_a4>(sl + q) =
                                 __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, x0 + q, 0, 0));
                         wave_lds_sync();
+                        if (lane == 0) {
+                            *la<u32x4>(sl - 16) = (u32x4){0, 0, 0, 0};
+                            *la<uint32_t>(sl) &= above(8 * (int32_t)(sx & 3u), 0);
+                        }
+                        wave_lds_sync();
                         b.sl = sl;
+                        staged = true;
                     }
-                    if (P.c == 0 || !sr_init(b, r, sx, P.c)) {
+                    if (!staged) {   // (ONE: a block's sequences always fit the stage)
+                        err = ZE_GENERIC;
+                    } else if (P.c == 0 || !sr_init(b, r, sx, P.c)) {
                         err = ZE_CORRUPT;
                     } else {
                         const uint32_t tll = P.g & 15, tof = (P.g >> 4) & 15, tml = (P.g >> 8) & 15;
@@ -2075,73 +2280,130 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         auto nxt = [&](uint64_t cell) {
                             return ((uint32_t)cell & 0xFFFF) + sr_take(b, ((uint32_t)cell >> 16) & 0x7F);
                         };
-                        sr_load<ONE>(b);
-                        uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
-                        sr_done(b);
-                        sr_issue<ONE>(b);
+                        // OV 1: every field read straight from the staged stream at
+                        // its own position (two dwords and an alignbit each), all
+                        // six positions from the cursor and the cells -- no
+                        // register window, no fills: the chain per sequence is
+                        // cells -> widths -> positions -> reads -> states
+                        int32_t cur1 = 0;
+                        auto fld = [&](int32_t a, uint32_t w) -> uint32_t {   // bits [a, a + w), w <= 31
+                            const int32_t dq = max(a >> 5, -4);   // (below -128: the zero bytes)
+                            const uint32_t ad = (uint32_t)((int32_t)b.sl + 4 * dq) + zv;
+                            const uint32_t lo = *la<uint32_t>(ad), hi = *la<uint32_t>(ad + 4);
+                            return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, (uint32_t)a & 31), 0, w);
+                        };
+                        uint32_t sll, sof, sml;
+                        if (OV == 1) {
+                            const int32_t c0 = b.cur;
+                            sll = fld(c0 - (int32_t)tll, tll);
+                            sof = fld(c0 - (int32_t)(tll + tof), tof);
+                            sml = fld(c0 - (int32_t)(tll + tof + tml), tml);
+                            cur1 = c0 - (int32_t)(tll + tof + tml);
+                        } else {
+                            sr_load<ONE>(b);
+                            sll = sr_take(b, tll);
+                            sof = sr_take(b, tof);
+                            sml = sr_take(b, tml);
+                            sr_done(b);
+                            sr_issue<ONE>(b);
+                        }
                         uint64_t cl = XL(sll), co = XO(sof), cm = XM(sml);
 #ifdef ZSK_TUNING
                         const uint64_t tl0 = __builtin_readcyclecounter();
                         nseqs += nseq;
 #endif
                         // batches of up to 64 sequences: (1) the chain, wave-
-                        // uniform -- cells, bits, next states, repeat offsets and
-                        // item slots -> one 16-byte record per sequence in LDS,
-                        // stopping at a bad cell; (2) lane q takes record q: the
+                        // uniform -- cells, bits, next states and repeat offsets
+                        // -> one 16-byte record per sequence in LDS, stopping at
+                        // a bad cell; (2) lane q takes record q: item slots, the
                         // output / literal prefix sums, the replay's four checks
                         // in its order, the first failing sequence by ballot, and
                         // the items of the sequences before it (a lane's own
                         // stores).  Everything the serial loop below leaves --
                         // items, o, lp_, S.k, err -- is the same.
                         const uint32_t rec = ldsaddr(srec);
-                        uint32_t kk = S.k;   // item slot of the chain's next sequence
                         for (uint32_t i = 0; i < nseq && !err;) {
                             const uint32_t nb = min(64u, nseq - i);
                             uint32_t nd = 0;
                             bool afail = false;
                             wave_lds_sync();   // the last batch's records read
                             for (; nd < nb; nd++) {
-                                sr_use(b);
-                                if ((((uint32_t)cl | (uint32_t)co | (uint32_t)cm) >> 23) & 1) {
+                                if (OV != 1)
+                                    sr_use<ONE>(b);
+                                // (a ballot: the exit stays a uniform branch, not
+                                // an exec-mask loop exit)
+                                if (__ballot((((uint32_t)cl | (uint32_t)co | (uint32_t)cm) >> 23) & 1)) {
                                     afail = true;
                                     break;
                                 }
-                                const uint32_t ofv = (uint32_t)(co >> 32) + sr_take(b, (uint32_t)co >> 24);
-                                sr_fill(b);
-                                const uint32_t ml = (uint32_t)(cm >> 32) + sr_take(b, (uint32_t)cm >> 24);
-                                const uint32_t ll = (uint32_t)(cl >> 32) + sr_take(b, (uint32_t)cl >> 24);
-                                sr_fill(b);
-                                sll = nxt(cl);
-                                sml = nxt(cm);
-                                sof = nxt(co);
-                                sr_done(b);
-                                sr_issue<ONE>(b);
+                                uint32_t ofv, ml, ll;
+                                if (OV == 1) {
+                                    const uint32_t ofb = (uint32_t)co >> 24, mlb = (uint32_t)cm >> 24,
+                                                   llb = (uint32_t)cl >> 24;
+                                    const int32_t t1 = cur1 - (int32_t)ofb, t2 = t1 - (int32_t)mlb,
+                                                  t3 = t2 - (int32_t)llb;
+                                    const int32_t t4 = t3 - (int32_t)(((uint32_t)cl >> 16) & 0x7F);
+                                    const int32_t t5 = t4 - (int32_t)(((uint32_t)cm >> 16) & 0x7F);
+                                    const int32_t t6 = t5 - (int32_t)(((uint32_t)co >> 16) & 0x7F);
+                                    ofv = (uint32_t)(co >> 32) + fld(t1, ofb);
+                                    ml = (uint32_t)(cm >> 32) + fld(t2, mlb);
+                                    ll = (uint32_t)(cl >> 32) + fld(t3, llb);
+                                    sll = ((uint32_t)cl & 0xFFFF) + fld(t4, (uint32_t)(t3 - t4));
+                                    sml = ((uint32_t)cm & 0xFFFF) + fld(t5, (uint32_t)(t4 - t5));
+                                    sof = ((uint32_t)co & 0xFFFF) + fld(t6, (uint32_t)(t5 - t6));
+                                    cur1 = t6;
+                                } else {
+                                    ofv = (uint32_t)(co >> 32) + sr_take(b, (uint32_t)co >> 24);
+                                    sr_fill(b);
+                                    ml = (uint32_t)(cm >> 32) + sr_take(b, (uint32_t)cm >> 24);
+                                    ll = (uint32_t)(cl >> 32) + sr_take(b, (uint32_t)cl >> 24);
+                                    sr_fill(b);
+                                    sll = nxt(cl);
+                                    sml = nxt(cm);
+                                    sof = nxt(co);
+                                    sr_done(b);
+                                    sr_issue<ONE>(b);
+                                }
                                 cl = XL(sll);
                                 co = XO(sof);
                                 cm = XM(sml);
+                                // (selects by the index bits: a nested ?: chain
+                                // compiled to divergent branches)
                                 const bool fresh = ofv > 3;
                                 const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
-                                const uint32_t off = fresh ? ofv - 3
-                                                     : idx == 0 ? rep0
-                                                     : idx == 1 ? rep1
-                                                     : idx == 2 ? rep2
-                                                                : max(rep0 - 1, 1u);
+                                const uint32_t r01 = (idx & 1) ? rep1 : rep0, r23 = (idx & 1) ? max(rep0 - 1, 1u) : rep2;
+                                const uint32_t off = fresh ? ofv - 3 : (idx & 2) ? r23 : r01;
                                 const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
                                 rep2 = sh2 ? rep1 : rep2;
                                 rep1 = sh1 ? rep0 : rep1;
                                 rep0 = sh1 ? off : rep0;
-                                // lemit's slot rule: an extended pair never starts in slot 63 of a group
-                                const bool ext = ll > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF;
-                                const uint32_t pad = ext && (kk & 63) == 63 ? 1u : 0u;
-                                *la<u32x4>(rec + 16 * nd) = (u32x4){off, ml, ll, kk | (ext ? 1u : 0u) << 30 | pad << 31};
-                                kk += ext ? 2 + pad : 1;
+                                *la<u32x4>(rec + 16 * nd) = (u32x4){off, ml, ll, 0u};
                             }
                             wave_lds_sync();
                             const bool on = lane < nd;
                             const u32x4 R = on ? *la<u32x4>(rec + 16 * lane) : (u32x4){0, 0, 0, 0};
-                            const uint32_t off = R.x, ml = R.y, ll = R.z, kq = R.w & 0x3FFFFFFF;
-                            const bool ext = (R.w >> 30) & 1;
-                            const uint32_t pad = R.w >> 31, ni = ext ? 2 + pad : 1;
+                            const uint32_t off = R.x, ml = R.y, ll = R.z;
+                            // item slots (lemit's rule: an extended pair never
+                            // starts in slot 63 of a 64-slot group, a zero item
+                            // pads it): a scan without pads, then, only if some
+                            // extended pair lands on slot 63, the slots again
+                            // sequence by sequence
+                            const bool ext = on && (ll > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF);
+                            const uint32_t n1 = on ? (ext ? 2u : 1u) : 0u;
+                            uint32_t kq = S.k + wave_incl_add(n1) - n1, pad = 0;
+                            if (__ballot(ext && (kq & 63) == 63)) {
+                                uint32_t k = S.k;
+                                for (uint32_t q = 0; q < nd; q++) {
+                                    const bool eq = lane_val(ext ? 1u : 0u, (int)q) != 0;
+                                    const uint32_t pq = eq && (k & 63) == 63 ? 1u : 0u;
+                                    if (lane == q) {
+                                        kq = k;
+                                        pad = pq;
+                                    }
+                                    k += eq ? 2 + pq : 1;
+                                }
+                            }
+                            const uint32_t ni = ext ? 2 + pad : 1;
                             const uint32_t ill = wave_incl_add(ll), iol = wave_incl_add(ll + ml);
                             const uint32_t lpq = lp_ + ill - ll, oq = o + iol - (ll + ml);
                             const uint32_t kind = ll + ml > cap - oq ? (uint32_t)ZE_DST_SMALL
@@ -2166,12 +2428,15 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 err = lane_val(kind, (int)e);
                                 S.k = lane_val(kq, (int)e);
                             } else {
-                                S.k = kk;
+                                if (nd)
+                                    S.k = lane_val(kq + ni, (int)nd - 1);
                                 if (afail)
                                     err = ZE_CORRUPT;
                             }
                             i += nd;
                         }
+                        if (OV == 1)
+                            b.cur = cur1;
 #ifdef ZSK_TUNING
                         tloop += __builtin_readcyclecounter() - tl0;
 #endif
@@ -2734,6 +2999,22 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         hipLaunchKernelGGL(zstd_frame_kernel, dim3((m + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc, f1,
                            d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops, s->slots,
                            s->hjobs, f0);
+#ifdef ZSK_TUNING
+        {
+            static const bool ztimers = getenv("ZSEEK_ZFRAME_TIMERS") != nullptr;
+            static int zcalls = 0;
+            if (ztimers && ++zcalls % 100 == 0) {
+                unsigned long long z[8] = {0};
+                (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_zftime), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+                (void)hipStreamSynchronize(stream);
+                const double fr = z[4] ? (double)z[4] : 1.0;
+                fprintf(stderr,
+                        "zstd frame kernel cycles per frame: total %.0f huffman descriptions %.0f sequence tables %.0f "
+                        "window stagings %.0f (%llu frames)\n",
+                        z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4]);
+            }
+        }
+#endif
         kernel_span_end(SPAN_ZFRAME, tf, stream);
         if (hipEventRecord(s->ev_f[c], stream) != hipSuccess || hipStreamWaitEvent(qs, s->ev_f[c], 0) != hipSuccess)
             return drain();
@@ -2755,7 +3036,10 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                 unsigned int z[32] = {};
                 (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hdiag), z, sizeof(z), 0, hipMemcpyHostToDevice, hs);
             }
-            switch (diag) {
+            switch (one ? -1 : diag) {
+            case -1:
+                hipLaunchKernelGGL(zstd_huf_one_kernel, dim3(nj), dim3(kHufOneT), 0, hs, jb, d_comp, s->slots, s->lit, hb);
+                break;
             case 0: hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             case 1: hipLaunchKernelGGL(zstd_huf_kernel<1>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             case 3: hipLaunchKernelGGL(zstd_huf_kernel<3>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
@@ -2763,7 +3047,10 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             default: hipLaunchKernelGGL(zstd_huf_kernel<8>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb); break;
             }
 #else
-            hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb);
+            if (one)
+                hipLaunchKernelGGL(zstd_huf_one_kernel, dim3(nj), dim3(kHufOneT), 0, hs, jb, d_comp, s->slots, s->lit, hb);
+            else
+                hipLaunchKernelGGL(zstd_huf_kernel<0>, g, b, 0, hs, jb, nj, d_comp, s->slots, s->lit, hb);
 #endif
 #ifdef ZSK_TUNING
             if (counters) {
@@ -2802,9 +3089,21 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         else
 #endif
         if (one) {
-            hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true>), dim3(m), dim3(64), 0, qs, d_desc, f1,
+#ifdef ZSK_TUNING
+            static const int ov = getenv("ZSEEK_ZSEQ_ONE") ? atoi(getenv("ZSEEK_ZSEQ_ONE")) : kSeqOneV;
+            if (ov == 1)
+                hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true, 1>), dim3(m), dim3(64), 0, qs, d_desc, f1,
+                                   d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
+                                   d_status, s->ck, d_fail_at, f0);
+            else
+                hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true, 0>), dim3(m), dim3(64), 0, qs, d_desc, f1,
+                                   d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
+                                   d_status, s->ck, d_fail_at, f0);
+#else
+            hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true, kSeqOneV>), dim3(m), dim3(64), 0, qs, d_desc, f1,
                                d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
                                d_status, s->ck, d_fail_at, f0);
+#endif
 #ifdef ZSK_TUNING
             static const bool timers = getenv("ZSEEK_SEQ_TIMERS") != nullptr;
             static int calls = 0;
