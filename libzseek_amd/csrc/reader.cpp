@@ -453,11 +453,13 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     s.h_len = br.h_len;
     hipError_t e = hipSuccess;
     e = hipMemcpyAsync(s.d_comp, s.h_comp, doff + n * sizeof(FrameDesc), hipMemcpyHostToDevice, s.stream);
-    // (the LZ4 two-phase decoder's plan kernel initializes both itself)
+    // (the LZ4 two-phase decoder's plan kernel initializes both itself, the
+    // zstd sequence kernel writes both for every frame)
     const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
-    if (e == hipSuccess && !lz4_split)
+    const bool preset = r->type == ZSEEK_LZ4 && !lz4_split;
+    if (e == hipSuccess && preset)
         e = hipMemsetD32Async((hipDeviceptr_t)s.d_status, ST_NOT_RUN, n, s.stream);
-    if (e == hipSuccess && !lz4_split)
+    if (e == hipSuccess && preset)
         e = hipMemsetD32Async((hipDeviceptr_t)d_fail, 0, n, s.stream);
     if (e == hipSuccess && r->type == ZSEEK_ZSTD &&
         zstd_decode_frames(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream,

@@ -1290,6 +1290,12 @@ __global__ __launch_bounds__(64 * kZW) __attribute__((amdgpu_waves_per_eu(4))) v
     F.blk_cap = (uint32_t)(blk_base[f + 1] - F.blk0);
     F.slots = slots;
     F.jobs = reinterpret_cast<HufJob *>(jobs);
+    // this frame's Huffman jobs zeroed (a block without Huffman literals, or
+    // one the frame never reaches, has no streams) -- no memset of the whole
+    // job array per launch; ordered before the jobs literals() writes
+    for (uint32_t i = lane_id(); i < 4 * F.blk_cap; i += 64)
+        F.jobs[4 * F.blk0 + i] = HufJob{0, 0, 0, 0, 0, 0};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     uint32_t e;
     // scratch sized by the plan: a frame that would not fit is refused, never
     // written out of bounds
@@ -2977,12 +2983,12 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         return v && !strcmp(v, "0");
     }();
     const bool one = !one_off && nframes <= kOneMaxFrames;
-    hipStream_t const hs = serial ? stream : s->side, qs = serial ? stream : s->sq;
+    // (the one-frame route's sequence replay on the caller's stream, right
+    // behind the frame kernel: a cross-stream hand-off cost ~30 us each way)
+    hipStream_t const hs = serial ? stream : s->side, qs = serial || one ? stream : s->sq;
 #ifdef ZSK_TUNING
     static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
 #endif
-    if (blocks && hipMemsetAsync(s->hjobs, 0, (size_t)(4 * blocks) * sizeof(HufJob), stream) != hipSuccess)
-        return -1;
     auto drain = [&] {   // an enqueue failed: nothing may still write the scratch
         (void)hipStreamSynchronize(stream);
         (void)hipStreamSynchronize(s->side);
