@@ -2373,22 +2373,73 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 cl = XL(sll);
                                 co = XO(sof);
                                 cm = XM(sml);
-                                // (selects by the index bits: a nested ?: chain
-                                // compiled to divergent branches)
-                                const bool fresh = ofv > 3;
-                                const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
-                                const uint32_t r01 = (idx & 1) ? rep1 : rep0, r23 = (idx & 1) ? max(rep0 - 1, 1u) : rep2;
-                                const uint32_t off = fresh ? ofv - 3 : (idx & 2) ? r23 : r01;
-                                const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
-                                rep2 = sh2 ? rep1 : rep2;
-                                rep1 = sh1 ? rep0 : rep1;
-                                rep0 = sh1 ? off : rep0;
-                                *la<u32x4>(rec + 16 * nd) = (u32x4){off, ml, ll, 0u};
+                                *la<u32x4>(rec + 16 * nd) = (u32x4){ofv, ml, ll, 0u};
                             }
                             wave_lds_sync();
                             const bool on = lane < nd;
                             const u32x4 R = on ? *la<u32x4>(rec + 16 * lane) : (u32x4){0, 0, 0, 0};
-                            const uint32_t off = R.x, ml = R.y, ll = R.z;
+                            const uint32_t ofv = R.x, ml = R.y, ll = R.z;
+                            // repeat offsets (RFC 8878 §3.1.2.5) by a scan: each
+                            // sequence maps the history (a, b, c) = (rep0, rep1,
+                            // rep2) to a new one -- a new offset v: (v, a, b);
+                            // index 0: (a, b, c); 1: (b, a, c); 2: (c, a, b); 3:
+                            // (a - 1 but >= 1, a, b) -- and its offset is the new
+                            // first entry.  A composed map keeps, per entry,
+                            // either a value (tag 3) or "old entry t less d"
+                            // (tag t, d decrements: max(x - d, 1), as repeated
+                            // decrements of values >= 1 compose).  Six shuffle
+                            // steps compose each lane's prefix; applied to the
+                            // batch's starting history they give every offset.
+                            uint32_t tg[3], vl[3];
+                            {
+                                const bool fresh = ofv > 3;
+                                const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
+                                tg[0] = fresh ? 3u : idx == 3 ? 0u : idx;
+                                vl[0] = fresh ? ofv - 3 : idx == 3 ? 1u : 0u;
+                                tg[1] = !fresh && idx == 0 ? 1u : 0u;
+                                tg[2] = !fresh && idx <= 1 ? 2u : 1u;
+                                vl[1] = vl[2] = 0;
+                                if (!on) {   // identity
+                                    tg[0] = 0;
+                                    tg[1] = 1;
+                                    tg[2] = 2;
+                                    vl[0] = 0;
+                                }
+                            }
+#pragma unroll
+                            for (uint32_t sft = 1; sft < 64; sft <<= 1) {
+                                uint32_t pt[3], pv[3];
+#pragma unroll
+                                for (int q = 0; q < 3; q++) {
+                                    pt[q] = (uint32_t)__shfl_up((int)tg[q], sft, 64);
+                                    pv[q] = (uint32_t)__shfl_up((int)vl[q], sft, 64);
+                                }
+                                if (lane >= sft) {
+#pragma unroll
+                                    for (int q = 0; q < 3; q++) {   // mine after the earlier prefix
+                                        const uint32_t t = tg[q], v = vl[q];
+                                        const uint32_t et = t == 0 ? pt[0] : t == 1 ? pt[1] : pt[2];
+                                        const uint32_t ev = t == 0 ? pv[0] : t == 1 ? pv[1] : pv[2];
+                                        tg[q] = t == 3 ? 3u : et;
+                                        vl[q] = t == 3 ? v : et == 3 ? (ev > v ? ev - v : 1u) : ev + v;
+                                    }
+                                }
+                            }
+                            auto apply = [&](uint32_t t, uint32_t v) -> uint32_t {
+                                if (t == 3)
+                                    return v;
+                                const uint32_t x = t == 0 ? rep0 : t == 1 ? rep1 : rep2;
+                                return x > v ? x - v : 1u;
+                            };
+                            const uint32_t off = apply(tg[0], vl[0]);
+                            if (nd) {
+                                const uint32_t n0 = lane_val(off, (int)nd - 1),
+                                               n1v = lane_val(apply(tg[1], vl[1]), (int)nd - 1),
+                                               n2v = lane_val(apply(tg[2], vl[2]), (int)nd - 1);
+                                rep0 = n0;
+                                rep1 = n1v;
+                                rep2 = n2v;
+                            }
                             // item slots (lemit's rule: an extended pair never
                             // starts in slot 63 of a 64-slot group, a zero item
                             // pads it): a scan without pads, then, only if some
