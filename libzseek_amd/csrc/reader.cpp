@@ -31,12 +31,14 @@
 // error string the reference would produce — the same observable sequence a
 // caller looping on the reference sees.
 #include <errno.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <deque>
 #include <functional>
@@ -393,9 +395,39 @@ bool read_span(LaneJob &J, uint8_t *dst, uint64_t len, uint64_t off)
     return true;
 }
 
+#ifdef ZSK_TUNING
+// tuning builds, ZSEEK_HOST_TIMERS: a batch's host steps (ns, summed):
+// [0] submit to after the read, [1] read to queued, [2] finish's wait, [3]
+// finish after the wait, [4] batches; [5] queued to the wait's start
+std::atomic<uint64_t> g_ht[6];
+uint64_t ht_now()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+void ht_report()
+{
+    static const bool on = getenv("ZSEEK_HOST_TIMERS") != nullptr;
+    const uint64_t b = g_ht[4].load();
+    if (!on || b == 0 || b % 200)
+        return;
+    fprintf(stderr, "host per batch (us): read %.1f enqueue %.1f to-wait %.1f wait %.1f after %.1f (%llu batches)\n",
+            g_ht[0] / 1e3 / b, g_ht[1] / 1e3 / b, g_ht[5] / 1e3 / b, g_ht[2] / 1e3 / b, g_ht[3] / 1e3 / b,
+            (unsigned long long)b);
+}
+thread_local uint64_t t_queued = 0;
+#define HT_T(v) const uint64_t v = ht_now();
+#define HT_ADD(i, v) g_ht[i] += ht_now() - v;
+#else
+#define HT_T(v)
+#define HT_ADD(i, v)
+#endif
+
 // Read, upload, decode and queue the download of frames [f0, f1) on slot s.
 bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
 {
+    HT_T(ht0)
     zseek_reader *r = J.r;
     DeviceCtx &g = *J.g;
     const SeekTable &st = r->st;
@@ -434,6 +466,8 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         J.io_failed = true;
         return false;
     }
+    HT_ADD(0, ht0)
+    HT_T(ht1)
     FrameDesc *const h_desc = reinterpret_cast<FrameDesc *>(s.h_comp + doff);
     const FrameDesc *const d_desc = reinterpret_cast<const FrameDesc *>(s.d_comp + doff);
     uint32_t max_dsize = 0;
@@ -511,6 +545,10 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     g.frames_decoded += n;
     g.bytes_decoded += dsz;
     g.bytes_uploaded += csz;
+    HT_ADD(1, ht1)
+#ifdef ZSK_TUNING
+    t_queued = ht_now();
+#endif
     return true;
 }
 
@@ -521,7 +559,24 @@ bool finish(LaneJob &J, Slot &s)
 {
     zseek_reader *r = J.r;
     const SeekTable &st = r->st;
+#ifdef ZSK_TUNING
+    if (t_queued)
+        g_ht[5] += ht_now() - t_queued;
+    const uint64_t ht2 = ht_now();
+#endif
     hipError_t e = hipEventSynchronize(s.done);
+#ifdef ZSK_TUNING
+    g_ht[2] += ht_now() - ht2;
+    struct HtAfter {
+        uint64_t t = ht_now();
+        ~HtAfter()
+        {
+            g_ht[3] += ht_now() - t;
+            g_ht[4]++;
+            ht_report();
+        }
+    } ht_after;
+#endif
     if (e != hipSuccess) {
         set_error(J.err, "GPU decode failed: %s", hipGetErrorString(e));
         J.io_failed = true;

@@ -2123,7 +2123,6 @@ constexpr uint32_t kSeqGm = 2;        // OF from the slot
 // 64 KiB frame); from LDS the chain waits on LDS latency only.
 constexpr uint32_t kSeqOneCells = 1312;
 constexpr uint32_t kSeqStage = 131072 + 64;   // > a block's largest sequences section
-constexpr int kSeqOneV = 0;                    // the chain's bit reads (OV, below)
 #ifdef ZSK_TUNING
 // tuning builds, ONE: [0] kernel cycles, [1] sequence-loop cycles, [2]
 // sequences, [3] kernel real-time ticks (100 MHz), [4] frames; printed under
@@ -2131,7 +2130,7 @@ constexpr int kSeqOneV = 0;                    // the chain's bit reads (OV, bel
 __device__ unsigned long long g_sdiag[8];
 #endif
 
-template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false, int OV = 0>
+template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false>
 __global__ __launch_bounds__(64) void zstd_seq_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
@@ -2283,36 +2282,10 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         auto XL = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * x + zv); };
                         auto XO = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * (nll + x) + zv); };
                         auto XM = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * (nll + nof + x) + zv); };
-                        auto nxt = [&](uint64_t cell) {
-                            return ((uint32_t)cell & 0xFFFF) + sr_take(b, ((uint32_t)cell >> 16) & 0x7F);
-                        };
-                        // OV 1: every field read straight from the staged stream at
-                        // its own position (two dwords and an alignbit each), all
-                        // six positions from the cursor and the cells -- no
-                        // register window, no fills: the chain per sequence is
-                        // cells -> widths -> positions -> reads -> states
-                        int32_t cur1 = 0;
-                        auto fld = [&](int32_t a, uint32_t w) -> uint32_t {   // bits [a, a + w), w <= 31
-                            const int32_t dq = max(a >> 5, -4);   // (below -128: the zero bytes)
-                            const uint32_t ad = (uint32_t)((int32_t)b.sl + 4 * dq) + zv;
-                            const uint32_t lo = *la<uint32_t>(ad), hi = *la<uint32_t>(ad + 4);
-                            return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, (uint32_t)a & 31), 0, w);
-                        };
-                        uint32_t sll, sof, sml;
-                        if (OV == 1) {
-                            const int32_t c0 = b.cur;
-                            sll = fld(c0 - (int32_t)tll, tll);
-                            sof = fld(c0 - (int32_t)(tll + tof), tof);
-                            sml = fld(c0 - (int32_t)(tll + tof + tml), tml);
-                            cur1 = c0 - (int32_t)(tll + tof + tml);
-                        } else {
-                            sr_load<ONE>(b);
-                            sll = sr_take(b, tll);
-                            sof = sr_take(b, tof);
-                            sml = sr_take(b, tml);
-                            sr_done(b);
-                            sr_issue<ONE>(b);
-                        }
+                        sr_load<ONE>(b);
+                        uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
+                        sr_done(b);
+                        sr_issue<ONE>(b);
                         uint64_t cl = XL(sll), co = XO(sof), cm = XM(sml);
 #ifdef ZSK_TUNING
                         const uint64_t tl0 = __builtin_readcyclecounter();
@@ -2334,8 +2307,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             bool afail = false;
                             wave_lds_sync();   // the last batch's records read
                             for (; nd < nb; nd++) {
-                                if (OV != 1)
-                                    sr_use<ONE>(b);
+                                sr_use<ONE>(b);
                                 // (a ballot: the exit stays a uniform branch, not
                                 // an exec-mask loop exit)
                                 if (__ballot((((uint32_t)cl | (uint32_t)co | (uint32_t)cm) >> 23) & 1)) {
@@ -2343,30 +2315,26 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                     break;
                                 }
                                 uint32_t ofv, ml, ll;
-                                if (OV == 1) {
-                                    const uint32_t ofb = (uint32_t)co >> 24, mlb = (uint32_t)cm >> 24,
-                                                   llb = (uint32_t)cl >> 24;
-                                    const int32_t t1 = cur1 - (int32_t)ofb, t2 = t1 - (int32_t)mlb,
-                                                  t3 = t2 - (int32_t)llb;
-                                    const int32_t t4 = t3 - (int32_t)(((uint32_t)cl >> 16) & 0x7F);
-                                    const int32_t t5 = t4 - (int32_t)(((uint32_t)cm >> 16) & 0x7F);
-                                    const int32_t t6 = t5 - (int32_t)(((uint32_t)co >> 16) & 0x7F);
-                                    ofv = (uint32_t)(co >> 32) + fld(t1, ofb);
-                                    ml = (uint32_t)(cm >> 32) + fld(t2, mlb);
-                                    ll = (uint32_t)(cl >> 32) + fld(t3, llb);
-                                    sll = ((uint32_t)cl & 0xFFFF) + fld(t4, (uint32_t)(t3 - t4));
-                                    sml = ((uint32_t)cm & 0xFFFF) + fld(t5, (uint32_t)(t4 - t5));
-                                    sof = ((uint32_t)co & 0xFFFF) + fld(t6, (uint32_t)(t5 - t6));
-                                    cur1 = t6;
-                                } else {
+                                {
                                     ofv = (uint32_t)(co >> 32) + sr_take(b, (uint32_t)co >> 24);
                                     sr_fill(b);
-                                    ml = (uint32_t)(cm >> 32) + sr_take(b, (uint32_t)cm >> 24);
-                                    ll = (uint32_t)(cl >> 32) + sr_take(b, (uint32_t)cl >> 24);
+                                    // the ML and LL extra bits (<= 32, ML above
+                                    // LL) in one extract, then the three state
+                                    // fields (<= 26: LL, ML, OF from the top)
+                                    const uint32_t mlb = (uint32_t)cm >> 24, llb = (uint32_t)cl >> 24;
+                                    const uint32_t X = (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)(mlb + llb)) & 63));
+                                    b.nb -= (int32_t)(mlb + llb);
+                                    ll = (uint32_t)(cl >> 32) + __builtin_amdgcn_ubfe(X, 0u, llb);
+                                    ml = (uint32_t)(cm >> 32) + __builtin_amdgcn_ubfe(X, llb, mlb);
                                     sr_fill(b);
-                                    sll = nxt(cl);
-                                    sml = nxt(cm);
-                                    sof = nxt(co);
+                                    const uint32_t lln = ((uint32_t)cl >> 16) & 0x7F, mln = ((uint32_t)cm >> 16) & 0x7F,
+                                                   ofn = ((uint32_t)co >> 16) & 0x7F;
+                                    const uint32_t Y =
+                                        (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)(lln + mln + ofn)) & 63));
+                                    b.nb -= (int32_t)(lln + mln + ofn);
+                                    sof = ((uint32_t)co & 0xFFFF) + __builtin_amdgcn_ubfe(Y, 0u, ofn);
+                                    sml = ((uint32_t)cm & 0xFFFF) + __builtin_amdgcn_ubfe(Y, ofn, mln);
+                                    sll = ((uint32_t)cl & 0xFFFF) + __builtin_amdgcn_ubfe(Y, ofn + mln, lln);
                                     sr_done(b);
                                     sr_issue<ONE>(b);
                                 }
@@ -2492,8 +2460,6 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             }
                             i += nd;
                         }
-                        if (OV == 1)
-                            b.cur = cur1;
 #ifdef ZSK_TUNING
                         tloop += __builtin_readcyclecounter() - tl0;
 #endif
@@ -3146,21 +3112,9 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         else
 #endif
         if (one) {
-#ifdef ZSK_TUNING
-            static const int ov = getenv("ZSEEK_ZSEQ_ONE") ? atoi(getenv("ZSEEK_ZSEQ_ONE")) : kSeqOneV;
-            if (ov == 1)
-                hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true, 1>), dim3(m), dim3(64), 0, qs, d_desc, f1,
-                                   d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
-                                   d_status, s->ck, d_fail_at, f0);
-            else
-                hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true, 0>), dim3(m), dim3(64), 0, qs, d_desc, f1,
-                                   d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
-                                   d_status, s->ck, d_fail_at, f0);
-#else
-            hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true, kSeqOneV>), dim3(m), dim3(64), 0, qs, d_desc, f1,
-                               d_comp, s->ops, s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems,
-                               d_status, s->ck, d_fail_at, f0);
-#endif
+            hipLaunchKernelGGL((zstd_seq_kernel<1, 0, 0, true>), dim3(m), dim3(64), 0, qs, d_desc, f1, d_comp, s->ops,
+                               s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems, d_status, s->ck,
+                               d_fail_at, f0);
 #ifdef ZSK_TUNING
             static const bool timers = getenv("ZSEEK_SEQ_TIMERS") != nullptr;
             static int calls = 0;
