@@ -495,9 +495,13 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         e = hipMemsetD32Async((hipDeviceptr_t)s.d_status, ST_NOT_RUN, n, s.stream);
     if (e == hipSuccess && preset)
         e = hipMemsetD32Async((hipDeviceptr_t)d_fail, 0, n, s.stream);
+    // (zstd: a request's few frames are planned on the host from the pinned
+    // span -- no plan launch, no synchronization between plan and decode)
     if (e == hipSuccess && r->type == ZSEEK_ZSTD &&
-        zstd_decode_frames(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream,
-                           d_fail) != 0)
+        (n <= kOneMaxFrames ? zstd_decode_frames_host(h_desc, s.h_comp, d_desc, (uint32_t)n, s.d_comp, s.d_out,
+                                                      s.d_status, &s.zs, s.stream, d_fail)
+                            : zstd_decode_frames(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs,
+                                                 s.stream, d_fail)) != 0)
         e = hipErrorLaunchFailure;
     if (e == hipSuccess && r->type == ZSEEK_LZ4) {
         if (lz4_pick_engine((uint32_t)n) == ENGINE_WAVE) {

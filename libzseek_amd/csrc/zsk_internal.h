@@ -249,6 +249,8 @@ struct ZstdScratch {
     // at chunk boundary k (zstd_decode.hip: the decode runs in chunks)
     uint64_t *d_total = nullptr;
     uint64_t *total = nullptr;     // pinned host copy of d_total
+    uint64_t *h_plan = nullptr;    // pinned: a host plan's rec_base then blk_base (zstd_decode_frames_host)
+    uint64_t h_plan_cap = 0;       //   (u64 entries)
     hipStream_t side = nullptr;    // the Huffman kernel's stream (beside the sequence replay)
     hipStream_t sq = nullptr;      // the sequence kernel's stream
     static constexpr int kChunks = 8;   // most chunks a decode runs in
@@ -279,6 +281,14 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
                        uint32_t *d_fail_at = nullptr);
+// The same for a request's few frames whose compressed bytes are also in host
+// memory (h_desc / h_comp: the reader's pinned upload, the same layout as
+// d_desc / d_comp): the plan -- zstd_plan_kernel's per-frame bounds, the scans,
+// the totals -- computed on the host, so the decode needs no plan launch and
+// no synchronization.  nframes <= kOneMaxFrames.
+int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, const FrameDesc *d_desc,
+                            uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at);
 
 // Parse phase, streaming lane-per-frame (lz4_scan.hip), for the frames
 // under max_csize compressed bytes (the short frames of config 3).

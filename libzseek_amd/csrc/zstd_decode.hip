@@ -2935,6 +2935,10 @@ void zstd_scratch_release_memory(ZstdScratch *s)
             (void)hipFree(p);
     if (s->total)
         (void)hipHostFree(s->total);
+    if (s->h_plan)
+        (void)hipHostFree(s->h_plan);
+    s->h_plan = nullptr;
+    s->h_plan_cap = 0;
     s->bound = s->bblk = s->nitems = s->stop = nullptr;
     s->rec_base = s->blk_base = s->ck = s->d_total = s->total = nullptr;
     s->lit = s->slots = s->hbad = nullptr;
@@ -3186,6 +3190,121 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         return -1;
     if (zstd_scratch_reserve(s, nframes, s->total[1], s->total[0], s->total[2], stream) != 0)
         return -1;
+    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+}
+
+// zstd_plan_kernel's per-frame bound on the host: item slots (8 + 4 per
+// block + 2 per sequence + the pairs' padding, rounded up to 4) and blocks,
+// from the frame headers, block headers, literals section headers and
+// sequence counts -- the same walk, the same arithmetic.
+static void zstd_plan_frame_host(const uint8_t *c, uint32_t clen, uint32_t *bound, uint32_t *bblk)
+{
+    auto B = [&](uint32_t p) -> uint32_t { return p < clen ? (uint32_t)c[p] : 0u; };
+    uint64_t items = 8;
+    uint32_t ip = 0, blocks = 0;
+    while (clen - ip >= 9 && items < (1u << 30)) {
+        const uint32_t magic = B(ip) | B(ip + 1) << 8 | B(ip + 2) << 16 | B(ip + 3) << 24;
+        if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
+            ip += 8 + (B(ip + 4) | B(ip + 5) << 8 | B(ip + 6) << 16 | B(ip + 7) << 24);
+            continue;
+        }
+        if (magic != kZMagic)
+            break;
+        const uint32_t fhd = B(ip + 4);
+        const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, did = fhd & 3;
+        ip += 5 + !single + (did == 3 ? 4 : did) + (fcs_flag == 0 ? single : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8);
+        for (;;) {
+            if (clen < ip + 3)
+                break;
+            const uint32_t bh = B(ip) | B(ip + 1) << 8 | B(ip + 2) << 16;
+            const uint32_t type = (bh >> 1) & 3, bsize = bh >> 3;
+            ip += 3;
+            items += 4;
+            blocks++;
+            if (type == 2 && bsize >= 3) {
+                const uint32_t b0 = B(ip), lt = b0 & 3, sf = (b0 >> 2) & 3;
+                uint32_t sec;
+                if (lt <= 1) {
+                    const uint32_t lh = sf == 1 ? 2 : sf == 3 ? 3 : 1;
+                    const uint32_t sz = sf == 1 ? (b0 | B(ip + 1) << 8) >> 4
+                                      : sf == 3 ? (b0 | B(ip + 1) << 8 | B(ip + 2) << 16) >> 4
+                                                : b0 >> 3;
+                    sec = lt == 0 ? lh + sz : lh + 1;
+                } else {
+                    const uint32_t lhc = b0 | B(ip + 1) << 8 | B(ip + 2) << 16 | B(ip + 3) << 24;
+                    sec = sf <= 1 ? 3 + ((lhc >> 14) & 0x3FF) : sf == 2 ? 4 + (lhc >> 18)
+                                                                      : 5 + (lhc >> 22) + (B(ip + 4) << 10);
+                }
+                if (sec < bsize) {
+                    const uint32_t q = ip + sec, s0 = B(q);
+                    const uint32_t nseq = s0 < 128 ? s0 : s0 < 255 ? ((s0 - 128) << 8) + B(q + 1)
+                                                                   : (B(q + 1) | B(q + 2) << 8) + 0x7F00;
+                    items += 2ull * nseq + (2ull * nseq + 62) / 63;
+                }
+            }
+            ip += type == 1 ? 1 : bsize;
+            if ((bh & 1) || ip > clen)
+                break;
+        }
+        if (ip > clen)
+            break;
+        if ((fhd >> 2) & 1)
+            ip += 4;
+    }
+    *bound = (uint32_t)((items + 3) & ~3ull);
+    *bblk = blocks;
+}
+
+int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, const FrameDesc *d_desc,
+                            uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at)
+{
+    if (nframes == 0)
+        return 0;
+    if (nframes > kOneMaxFrames || zstd_chunks(nframes) != 1)
+        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+    (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
+    uint64_t items = 0, blocks = 0, extent = 0, dmax = 0;
+    if (zstd_scratch_reserve(s, nframes, 0, 0, 0, stream) != 0)
+        return -1;
+    if (2ull * (nframes + 1) > s->h_plan_cap) {
+        if (s->h_plan)
+            (void)hipHostFree(s->h_plan);
+        s->h_plan = nullptr;
+        s->h_plan_cap = 0;
+        if (hipHostMalloc((void **)&s->h_plan, 2 * (kOneMaxFrames + 1) * sizeof(uint64_t), hipHostMallocDefault) !=
+            hipSuccess)
+            return -1;
+        s->h_plan_cap = 2 * (kOneMaxFrames + 1);
+    }
+    uint64_t *const rb = s->h_plan, *const bb = s->h_plan + nframes + 1;
+    for (uint32_t f = 0; f < nframes; f++) {
+        const FrameDesc &d = h_desc[f];
+        uint32_t bound = 0, bblk = 0;
+        zstd_plan_frame_host(h_comp + d.c_off, d.c_size, &bound, &bblk);
+        rb[f] = items;
+        bb[f] = blocks;
+        items += bound;
+        blocks += bblk;
+        extent = std::max<uint64_t>(extent, d.d_off + d.d_size);
+        dmax = std::max<uint64_t>(dmax, d.d_size);
+    }
+    rb[nframes] = items;
+    bb[nframes] = blocks;
+    stage_mark(0, stream);
+    if (zstd_scratch_reserve(s, nframes, extent, items, blocks, stream) != 0)
+        return -1;
+    s->total[0] = items;
+    s->total[1] = extent;
+    s->total[2] = blocks;
+    s->total[3] = dmax;
+    s->total[4] = 0;   // one chunk: blocks [0, blocks)
+    s->total[5] = blocks;
+    if (hipMemcpyAsync(s->rec_base, rb, (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(s->blk_base, bb, (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) != hipSuccess)
+        return -1;
+    stage_mark(1, stream);
     return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
 }
 
