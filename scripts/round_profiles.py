@@ -7,7 +7,15 @@ and derive profiles/pmc_traffic.json for bench.py's roofline.traffic.
 HBM bytes per decode launch = sum over its kernels of 2 x FETCH_SIZE (gfx950
 reports half the bytes of a wide streaming read, MI355X_MICROARCH.md HBM
 section) + WRITE_SIZE, both in KiB from separate --pmc passes, median over
-dispatches per kernel.
+dispatches per kernel.  Round 5: when the run also holds the L2's memory-side
+request counters (passes ea_p1..3: TCC_EA0_RDREQ_{32B,64B,128B},
+TCC_EA0_WRREQ{,_64B}; scripts/gpu_round5.sh), `hbm_bytes_per_launch` is their
+exact byte count instead (reads = 32 n32 + 64 n64 + 128 n128, writes = 64 n64
++ 32 (n - n64)); the FETCH-based figure stays beside it.  The calibration
+(profiles/r05_fetch_calib.json: frames whose execute reads are known) found
+the EA read bytes equal to 2 x FETCH_SIZE (the guide's correction holds) and
+1.18x / 1.36x the known reads (whole 32 / 64-byte requests under unaligned
+16-byte pieces): memory-side bytes, not algorithmic ones.
 """
 import csv
 import glob
@@ -85,6 +93,29 @@ for (k, c), v in counters.items():
 fetch = sum(d.get("FETCH_SIZE", 0.0) for d in per.values())
 write = sum(d.get("WRITE_SIZE", 0.0) for d in per.values())
 alg = bench["roofline"]["algorithmic_bytes_per_launch"]
+# EA request bytes (exact), per launch: per kernel the median dispatch x
+# dispatches per launch, as above
+ea = {}
+if glob.glob(os.path.join(src, "ea_p1", "**", "*_counter_collection.csv"), recursive=True):
+    cnt = {}
+    for i in (1, 2, 3):
+        for f in glob.glob(os.path.join(src, f"ea_p{i}", "**", "*_counter_collection.csv"), recursive=True):
+            shutil.copy(f, os.path.join(dst, f"{tag}_ea_p{i}.csv"))
+            for row in csv.DictReader(open(f)):
+                k = part(row["Kernel_Name"])
+                if k:
+                    key = (k, row["Counter_Name"], int(row["Dispatch_Id"]))
+                    cnt[key] = cnt.get(key, 0.0) + float(row["Counter_Value"])
+    byk = {}
+    for (k, c, d), v in cnt.items():
+        byk.setdefault(k, {}).setdefault(c, []).append(v)
+    plan_d = len(byk.get(PLAN, {}).get("TCC_EA0_RDREQ_32B_sum", [])) or 1
+    for k, c in byk.items():
+        m = {n: statistics.median(v) * len(v) / plan_d for n, v in c.items()}
+        rd = 32 * m.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * m.get("TCC_EA0_RDREQ_64B_sum", 0) + \
+            128 * m.get("TCC_EA0_RDREQ_128B_sum", 0)
+        wq, w64 = m.get("TCC_EA0_WRREQ_sum", 0), m.get("TCC_EA0_WRREQ_64B_sum", 0)
+        ea[k] = {"read_bytes": rd, "write_bytes": 64 * w64 + 32 * (wq - w64)}
 out = {
     "round": tag,
     "kernel": KERNEL,
@@ -96,10 +127,19 @@ out = {
     "fetch_size_bytes_raw": fetch,
     "fetch_bytes_corrected_x2": 2 * fetch,
     "write_size_bytes": write,
-    "hbm_bytes_per_launch": 2 * fetch + write,
+    "fetch_based_bytes_per_launch": 2 * fetch + write,
     "algorithmic_bytes_per_launch": alg,
-    "traffic_over_algorithmic": (2 * fetch + write) / alg,
 }
+if ea:
+    out["ea_kernels"] = ea
+    out["ea_read_bytes"] = sum(v["read_bytes"] for v in ea.values())
+    out["ea_write_bytes"] = sum(v["write_bytes"] for v in ea.values())
+    out["hbm_bytes_per_launch"] = out["ea_read_bytes"] + out["ea_write_bytes"]
+    out["traffic_source"] = "TCC_EA0 request bytes (exact)"
+else:
+    out["hbm_bytes_per_launch"] = 2 * fetch + write
+    out["traffic_source"] = "2 x FETCH_SIZE + WRITE_SIZE"
+out["traffic_over_algorithmic"] = out["hbm_bytes_per_launch"] / alg
 json.dump(out, open(os.path.join(dst, OUT), "w"), indent=1)
 shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
 print(json.dumps(out, indent=1))
