@@ -499,7 +499,7 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // span -- no plan launch, no synchronization between plan and decode)
     if (e == hipSuccess && r->type == ZSEEK_ZSTD &&
         (n <= kOneMaxFrames ? zstd_decode_frames_host(h_desc, s.h_comp, d_desc, (uint32_t)n, s.d_comp, s.d_out,
-                                                      s.d_status, &s.zs, s.stream, d_fail)
+                                                      s.d_status, &s.zs, s.stream, d_fail, stop_last)
                             : zstd_decode_frames(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs,
                                                  s.stream, d_fail)) != 0)
         e = hipErrorLaunchFailure;

@@ -1554,19 +1554,19 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
 int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *lit,
                         uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                         const uint32_t *nitems, int32_t *d_status, hipStream_t stream, bool one,
-                        uint32_t max_dsize)
+                        uint32_t max_dsize, uint32_t stop_last)
 {
     if (nframes == 0)
         return 0;
     if (one) {   // frames of <= 64 KiB a workgroup each, bigger ones a wave
         hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, nullptr,
-                           d_out, rec_base, items, nitems, d_status, nullptr, 0xFFFFFFFFu, 0u, lit);
+                           d_out, rec_base, items, nitems, d_status, nullptr, stop_last, 0u, lit);
         if (max_dsize <= kFMax)
             return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     hipLaunchKernelGGL((seq_exec_kernel<0, 4096, false>), dim3((nframes + kXW - 1) / kXW), dim3(64 * kXW), 0,
                        stream, d_desc, nframes, nullptr, d_out, rec_base, items, nitems, d_status, lit, nullptr,
-                       nullptr, nullptr, nullptr, 0xFFFFFFFFu, one ? kFMax + 1 : 0u);
+                       nullptr, nullptr, nullptr, stop_last, one ? kFMax + 1 : 0u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -227,7 +227,7 @@ int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
 int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *lit,
                         uint8_t *d_out, const uint64_t *rec_base, const uint64_t *items,
                         const uint32_t *nitems, int32_t *d_status, hipStream_t stream, bool one = false,
-                        uint32_t max_dsize = 0xFFFFFFFFu);
+                        uint32_t max_dsize = 0xFFFFFFFFu, uint32_t stop_last = 0xFFFFFFFFu);
 
 // zstd decoder (zstd_decode.hip): plan (item bounds -> rec_base[0..n]) and
 // decode (frame kernel -> items + literal scratch, execute, checksums).
@@ -274,9 +274,11 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 // d_fail_at (optional): per failed frame, the output offset of its failing
 // block's start (its end for the end-of-frame checks); the execute still
 // writes the bytes before it.
+// stop_last: the batch's last frame executed only up to that many bytes (a
+// no-cache read's end; its checksum then not checked)
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
-                       uint32_t *d_fail_at = nullptr);
+                       uint32_t *d_fail_at = nullptr, uint32_t stop_last = 0xFFFFFFFFu);
 // plan + synchronize + reserve + decode
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
@@ -288,7 +290,8 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 // no synchronization.  nframes <= kOneMaxFrames.
 int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, const FrameDesc *d_desc,
                             uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
-                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at);
+                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at,
+                            uint32_t stop_last = 0xFFFFFFFFu);
 
 // Parse phase, streaming lane-per-frame (lz4_scan.hip), for the frames
 // under max_csize compressed bytes (the short frames of config 3).

@@ -2713,7 +2713,7 @@ __global__ __launch_bounds__(256) void zstd_check_kernel(const FrameDesc *__rest
                                                          const uint8_t *__restrict__ out,
                                                          const uint64_t *__restrict__ ck,
                                                          int32_t *__restrict__ status,
-                                                         uint32_t *__restrict__ fail_at)
+                                                         uint32_t *__restrict__ fail_at, uint32_t stop_last)
 {
     __shared__ uint64_t buf[4][128];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2724,6 +2724,11 @@ __global__ __launch_bounds__(256) void zstd_check_kernel(const FrameDesc *__rest
     if (!(c >> 63) || uni((uint32_t)status[f]) != (uint32_t)ST_OK)
         return;
     const FrameDesc d = desc[f];
+    // (a no-cache read's last frame executed only up to the request's end:
+    // libzstd's streaming decoder never reaches the frame's end and its
+    // checksum there either)
+    if (f + 1 == n && stop_last < d.d_size)
+        return;
     const uint32_t o0 = (uint32_t)(c >> 32) & 0x7FFFFFFFu, want = (uint32_t)c;
     const uint8_t *p = out + d.d_off + o0;
     const uint32_t len = d.d_size - o0;
@@ -2988,7 +2993,7 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 // frame kernel is.  s must hold the last plan of these frames.
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
-                       uint32_t *d_fail_at)
+                       uint32_t *d_fail_at, uint32_t stop_last)
 {
     if (nframes == 0)
         return 0;
@@ -3158,12 +3163,14 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, f1, s->ops,
                                s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at, f0);
         hipEvent_t tx = kernel_span_begin(stream);
+        const uint32_t stop = c + 1 == K ? stop_last : 0xFFFFFFFFu;   // (the batch's last frame)
         if (launch_seq_exec_lit(d_desc + f0, m, s->lit, d_out, s->rec_base + f0, s->items, s->nitems + f0,
-                                d_status + f0, stream, one, (uint32_t)std::min<uint64_t>(s->total[3], 0xFFFFFFFFu)) != 0)
+                                d_status + f0, stream, one, (uint32_t)std::min<uint64_t>(s->total[3], 0xFFFFFFFFu),
+                                stop) != 0)
             rc = -1;
         kernel_span_end(SPAN_ZEXEC, tx, stream);
         hipLaunchKernelGGL(zstd_check_kernel, dim3((m + 3) / 4), dim3(256), 0, stream, d_desc + f0, m, d_out,
-                           s->ck + f0, d_status + f0, d_fail_at ? d_fail_at + f0 : nullptr);
+                           s->ck + f0, d_status + f0, d_fail_at ? d_fail_at + f0 : nullptr, stop);
     }
     stage_mark(3, stream);
     stage_mark(4, stream);
@@ -3257,7 +3264,7 @@ static void zstd_plan_frame_host(const uint8_t *c, uint32_t clen, uint32_t *boun
 
 int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, const FrameDesc *d_desc,
                             uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
-                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at)
+                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at, uint32_t stop_last)
 {
     if (nframes == 0)
         return 0;
@@ -3305,7 +3312,7 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
         hipMemcpyAsync(s->blk_base, bb, (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) != hipSuccess)
         return -1;
     stage_mark(1, stream);
-    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last);
 }
 
 }   // namespace zsk
