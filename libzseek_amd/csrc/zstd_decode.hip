@@ -134,8 +134,9 @@ __device__ __forceinline__ int32_t hibit(uint32_t v)
 #ifdef ZSK_TUNING
 // tuning builds: the frame kernel's cycles, lane 0 at section ends: [0]
 // kernel, [1] Huffman descriptions, [2] sequence tables (+ slot cells), [3]
-// window stagings, [4] frames; printed under ZSEEK_ZFRAME_TIMERS
-__device__ unsigned long long g_zftime[8];
+// window stagings, [4] frames, [5..7] the weights description: normalized
+// counts, table, walk; printed under ZSEEK_ZFRAME_TIMERS
+__device__ unsigned long long g_zftime[12];
 #define ZF_T0(v) const uint64_t v = __builtin_readcyclecounter();
 #define ZF_ADD(i, v)                                                                                  \
     if (lane_id() == 0)                                                                               \
@@ -189,16 +190,6 @@ __device__ __forceinline__ uint32_t wb(const ZLds &L, uint32_t wx, const In &I, 
     return *lp<uint8_t>(L.win + (I.s0 + p - wx));
 }
 
-// 32 window bits from bit `bit` (LSB first), from two aligned dword reads;
-// bits past the window's 256 bytes read as 0
-__device__ __forceinline__ uint32_t win32(const ZLds &L, uint32_t bit)
-{
-    const uint32_t d = bit >> 5;
-    const uint32_t lo = d < 64 ? *lp<uint32_t>(L.win + 4 * d) : 0u;
-    const uint32_t hi = d + 1 < 64 ? *lp<uint32_t>(L.win + 4 * d + 4) : 0u;
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (bit & 31));
-}
-
 // ---- FSE tables -----------------------------------------------------------------
 // Normalized counts from the window at bit 0 of window offset wofs,
 // RFC 8878 §4.1.1 / FSE_readNCount.  Returns bytes used, or 0 on error
@@ -212,12 +203,15 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
 {
     uint32_t pos = 8 * wofs, wp = pos + 64;   // forces the first load
     uint64_t W = 0;
+    // the window's 64 dwords one per lane: a reload is two readlanes, not an
+    // LDS round trip (the walk is a lone wave's serial chain)
+    const uint32_t wv = *lp<uint32_t>(L.win + 4 * lane_id());
     auto bits = [&](uint32_t n) -> uint32_t {   // n <= 16 bits at pos, not consumed
         if (pos - wp >= 32) {
             wp = pos & ~31u;
             const uint32_t d = wp >> 5;
-            const uint32_t lo = d < 64 ? uni(*lp<uint32_t>(L.win + 4 * d)) : 0u;
-            const uint32_t hi = d + 1 < 64 ? uni(*lp<uint32_t>(L.win + 4 * d + 4)) : 0u;
+            const uint32_t lo = d < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)d) : 0u;
+            const uint32_t hi = d + 1 < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)(d + 1)) : 0u;
             W = ((uint64_t)hi << 32) | lo;
         }
         return (uint32_t)(W >> (pos - wp)) & ((1u << n) - 1);
@@ -434,19 +428,35 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
             return 0;
         uint32_t tl = 0, nsym = 0;
         uint32_t hs = 0;
+        ZF_T0(tq0)
         norm_clear(L, 256);
         hs = read_ncount(L, wofs, hb, 255, 6, &tl, &nsym, &err);
+        ZF_ADD(5, tq0)
         hs = uni(hs);
         if (uni(err))
             return 0;
         tl = uni(tl);
         nsym = uni(nsym);
+        ZF_T0(tq1)
         fse_build(L, L.wfse, nsym, tl);
+        ZF_ADD(6, tq1)
+        ZF_T0(tq2)
         {
             // backward stream inside the window: two interleaved states
             // (wave-uniform, as read_ncount; lane 0 stores the weights)
             const uint32_t b0 = wofs + hs, bn = hb - hs;
             const uint32_t lastb = bn ? uni(*lp<uint8_t>(L.win + b0 + bn - 1)) : 0;
+            // the window's dwords and the weights' FSE cells (<= 64) one per
+            // lane: the walk reads them by readlane, not LDS round trips
+            const uint32_t wv = *lp<uint32_t>(L.win + 4 * lane);
+            const uint32_t fv = *lp<uint32_t>(L.wfse + (lane < (1u << tl) ? lane : 0u));
+            auto w32 = [&](uint32_t bit) -> uint32_t {   // win32 from the registers
+                const uint32_t d = bit >> 5;
+                const uint32_t lo = d < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)d) : 0u;
+                const uint32_t hi = d + 1 < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)wv, (int)(d + 1)) : 0u;
+                return (uint32_t)((((uint64_t)hi << 32) | lo) >> (bit & 31));
+            };
+            auto cellw = [&](uint32_t st) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)fv, (int)st); };
             if (!lastb) {
                 err = 1;
             } else {
@@ -455,7 +465,7 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
                 auto rb = [&](uint32_t n) -> uint32_t {
                     pos -= (int32_t)n;
                     const int32_t x = (int32_t)(8 * b0) + pos;
-                    uint32_t v = uni(x >= 0 ? win32(L, (uint32_t)x) : win32(L, 0) << (uint32_t)(-x)) & ((1u << n) - 1);
+                    uint32_t v = (x >= 0 ? w32((uint32_t)x) : w32(0) << (uint32_t)(-x)) & ((1u << n) - 1);
                     if (pos < 0)
                         v = -pos >= (int32_t)n ? 0u : v & (~0u << (uint32_t)(-pos));
                     return v;
@@ -471,28 +481,29 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
                         err = 1;
                         break;
                     }
-                    uint32_t c = uni(*lp<uint32_t>(L.wfse + s1));
+                    uint32_t c = cellw(s1);
                     put(c);
                     s1 = (c >> 16) + rb((c >> 8) & 0xFF);
                     if (pos < 0) {
-                        put(uni(*lp<uint32_t>(L.wfse + s2)));
+                        put(cellw(s2));
                         break;
                     }
                     if (nw > 253) {
                         err = 1;
                         break;
                     }
-                    c = uni(*lp<uint32_t>(L.wfse + s2));
+                    c = cellw(s2);
                     put(c);
                     s2 = (c >> 16) + rb((c >> 8) & 0xFF);
                     if (pos < 0) {
-                        put(uni(*lp<uint32_t>(L.wfse + s1)));
+                        put(cellw(s1));
                         break;
                     }
                 }
             }
         }
         wave_lds_sync();   // lane 0's weights before every lane reads them
+        ZF_ADD(7, tq2)
         used = 1 + hb;
     } else {
         nw = hb - 127;
@@ -851,12 +862,16 @@ __device__ __forceinline__ uint32_t seq_table(ZLds &L, Frame &F, uint32_t t, uin
         const uint32_t wx = stage_win(L, F.I, p);
         uint32_t tl = 0, nsym = 0, e = 0, used = 0;
         norm_clear(L, max_sym + 1);
+        ZF_T0(tn0)
         used = read_ncount(L, F.I.s0 + p - wx, avail, max_sym, max_log, &tl, &nsym, &e);
+        ZF_ADD(8, tn0)
         if (uni(e) || uni(used) == 0) {
             *err = ZE_CORRUPT;
             return ~0u;
         }
+        ZF_T0(tn1)
         fse_build(L, tab, uni(nsym), uni(tl));
+        ZF_ADD(9, tn1)
         F.tlog[t] = uni(tl);
         F.tvalid |= 1u << t;
         return uni(used);
@@ -929,6 +944,7 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_
         // the three tables -> the block's slot as u16 cells: symbol | next-state
         // rank ns << 6 (nbits and base follow from ns and the table log)
         uint16_t *dst = reinterpret_cast<uint16_t *>(F.slots + g * kZSlot + kSlotFse);
+        ZF_T0(tn2)
         wave_lds_sync();
 #pragma unroll
         for (uint32_t t = 0; t < 3; t++) {
@@ -940,6 +956,7 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_
             }
         }
         tl = F.tlog[0] | F.tlog[1] << 4 | F.tlog[2] << 8;
+        ZF_ADD(10, tn2)
         ZF_ADD(2, t0)
     }
     if (!put_op(F, OP_SEQ, nseq, q, qe > q ? qe - q : 0, F.lo, litn, (uint32_t)g, tl))
@@ -3036,14 +3053,16 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             static const bool ztimers = getenv("ZSEEK_ZFRAME_TIMERS") != nullptr;
             static int zcalls = 0;
             if (ztimers && ++zcalls % 100 == 0) {
-                unsigned long long z[8] = {0};
+                unsigned long long z[12] = {0};
                 (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_zftime), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
                 (void)hipStreamSynchronize(stream);
                 const double fr = z[4] ? (double)z[4] : 1.0;
                 fprintf(stderr,
                         "zstd frame kernel cycles per frame: total %.0f huffman descriptions %.0f sequence tables %.0f "
-                        "window stagings %.0f (%llu frames)\n",
-                        z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4]);
+                        "window stagings %.0f | weights: ncount %.0f build %.0f walk %.0f | sequence tables: "
+                        "ncount %.0f build %.0f cells out %.0f (%llu frames)\n",
+                        z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[5] / fr, z[6] / fr, z[7] / fr, z[8] / fr,
+                        z[9] / fr, z[10] / fr, z[4]);
             }
         }
 #endif
