@@ -251,6 +251,7 @@ struct ZstdScratch {
     uint64_t *total = nullptr;     // pinned host copy of d_total
     uint64_t *h_plan = nullptr;    // pinned: a host plan's rec_base then blk_base (zstd_decode_frames_host)
     uint64_t h_plan_cap = 0;       //   (u64 entries)
+    uint64_t *d_plan = nullptr;    // its device copy (one upload), 2 (kOneMaxFrames + 1) entries
     hipStream_t side = nullptr;    // the Huffman kernel's stream (beside the sequence replay)
     hipStream_t sq = nullptr;      // the sequence kernel's stream
     static constexpr int kChunks = 8;   // most chunks a decode runs in

@@ -2959,7 +2959,9 @@ void zstd_scratch_release_memory(ZstdScratch *s)
         (void)hipHostFree(s->total);
     if (s->h_plan)
         (void)hipHostFree(s->h_plan);
-    s->h_plan = nullptr;
+    if (s->d_plan)
+        (void)hipFree(s->d_plan);
+    s->h_plan = s->d_plan = nullptr;
     s->h_plan_cap = 0;
     s->bound = s->bblk = s->nitems = s->stop = nullptr;
     s->rec_base = s->blk_base = s->ck = s->d_total = s->total = nullptr;
@@ -3296,10 +3298,13 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
     if (2ull * (nframes + 1) > s->h_plan_cap) {
         if (s->h_plan)
             (void)hipHostFree(s->h_plan);
-        s->h_plan = nullptr;
+        if (s->d_plan)
+            (void)hipFree(s->d_plan);
+        s->h_plan = s->d_plan = nullptr;
         s->h_plan_cap = 0;
         if (hipHostMalloc((void **)&s->h_plan, 2 * (kOneMaxFrames + 1) * sizeof(uint64_t), hipHostMallocDefault) !=
-            hipSuccess)
+                hipSuccess ||
+            hipMalloc((void **)&s->d_plan, 2 * (kOneMaxFrames + 1) * sizeof(uint64_t)) != hipSuccess)
             return -1;
         s->h_plan_cap = 2 * (kOneMaxFrames + 1);
     }
@@ -3326,12 +3331,19 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
     s->total[3] = dmax;
     s->total[4] = 0;   // one chunk: blocks [0, blocks)
     s->total[5] = blocks;
-    if (hipMemcpyAsync(s->rec_base, rb, (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) !=
-            hipSuccess ||
-        hipMemcpyAsync(s->blk_base, bb, (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) != hipSuccess)
+    // both offset arrays in one upload; this launch's kernels take them from
+    // the upload's device copy (the scratch's own arrays are left alone)
+    if (hipMemcpyAsync(s->d_plan, rb, 2 * (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) !=
+        hipSuccess)
         return -1;
     stage_mark(1, stream);
-    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last);
+    uint64_t *const keep_rb = s->rec_base, *const keep_bb = s->blk_base;
+    s->rec_base = s->d_plan;
+    s->blk_base = s->d_plan + nframes + 1;
+    const int rc = launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last);
+    s->rec_base = keep_rb;
+    s->blk_base = keep_bb;
+    return rc;
 }
 
 }   // namespace zsk
