@@ -458,7 +458,7 @@ def main():
     dom = None
     if stages and kname:
         dk = [k for k, v in stages.items() if v["kernel"] == kname]
-        if dk:
+        if dk and stages[dk[0]]["median_ms"] > 0:   # (a library without per-stage timing reports 0)
             dms = stages[dk[0]]["median_ms"] / 1e3
             dom = {"kernel": kname, "median_ms": round(dms * 1e3, 4),
                    "achieved": round(alg_bytes / dms / 1e9, 1),

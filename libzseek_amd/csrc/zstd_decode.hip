@@ -2086,12 +2086,6 @@ __device__ __forceinline__ void sr_done(SRd &b)
     b.cur = b.base + b.nb;
 }
 
-__device__ __forceinline__ uint32_t fse_next(SRd &b, uint32_t e, uint32_t tl)
-{
-    const uint32_t ns = e >> 6;
-    const uint32_t nbits = tl + (uint32_t)__builtin_clz(ns) - 31;
-    return ((ns << nbits) - (1u << tl)) + sr_take(b, nbits);
-}
 
 // 32 frames per wave (lanes 32..63 idle), one wave per workgroup: each
 // frame's three FSE tables are copied into 1600 bytes of LDS when they fit
@@ -2535,26 +2529,38 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 const uint32_t ofv = (1u << ofc) + sr_take(b, ofc);
                                 const uint32_t mlcode = codes[36 + mlc], llcode = codes[llc];
                                 sr_fill(b);
-                                const uint32_t ml = (mlcode & 0xFFFFFF) + sr_take(b, mlcode >> 24);
-                                const uint32_t ll = (llcode & 0xFFFFFF) + sr_take(b, llcode >> 24);
+                                // the ML and LL extra bits (<= 32, ML above LL) in one extract
+                                const uint32_t mlb = mlcode >> 24, llb = llcode >> 24;
+                                const uint32_t X = (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)(mlb + llb)) & 63));
+                                b.nb -= (int32_t)(mlb + llb);
+                                const uint32_t ll = (llcode & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, 0u, llb);
+                                const uint32_t ml = (mlcode & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, llb, mlb);
                                 // repeat offsets as selects (RFC 8878 §3.1.2.5): a new
                                 // offset (ofv > 3) or repeat idx 0..3; idx 0 keeps the
                                 // history, idx 1 swaps the first two, 2 and 3 rotate
+                                // (selects by the index bits: a nested ?: chain
+                                // compiled to branches)
                                 const bool fresh = ofv > 3;
                                 const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
-                                uint32_t off = fresh ? ofv - 3
-                                               : idx == 0 ? rep0
-                                               : idx == 1 ? rep1
-                                               : idx == 2 ? rep2
-                                                          : max(rep0 - 1, 1u);   // rep0 - 1, 0 read as 1
+                                const uint32_t r01 = (idx & 1) ? rep1 : rep0,
+                                               r23 = (idx & 1) ? max(rep0 - 1, 1u) : rep2;   // rep0 - 1, 0 read as 1
+                                const uint32_t off = fresh ? ofv - 3 : (idx & 2) ? r23 : r01;
                                 const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
                                 rep2 = sh2 ? rep1 : rep2;
                                 rep1 = sh1 ? rep0 : rep1;
                                 rep0 = sh1 ? off : rep0;
                                 sr_fill(b);
-                                sll = fse_next(b, ell, tll);
-                                sml = fse_next(b, eml, tml);
-                                sof = fse_next(b, eof, tof);
+                                // the three next states (fse_next's bits, <= 26: LL, ML,
+                                // OF from the top) in one extract
+                                const uint32_t nsl = ell >> 6, nsm = eml >> 6, nso = eof >> 6;
+                                const uint32_t bl = tll + (uint32_t)__builtin_clz(nsl) - 31,
+                                               bm = tml + (uint32_t)__builtin_clz(nsm) - 31,
+                                               bo = tof + (uint32_t)__builtin_clz(nso) - 31;
+                                const uint32_t Y = (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)(bl + bm + bo)) & 63));
+                                b.nb -= (int32_t)(bl + bm + bo);
+                                sll = ((nsl << bl) - (1u << tll)) + __builtin_amdgcn_ubfe(Y, bm + bo, bl);
+                                sml = ((nsm << bm) - (1u << tml)) + __builtin_amdgcn_ubfe(Y, bo, bm);
+                                sof = ((nso << bo) - (1u << tof)) + __builtin_amdgcn_ubfe(Y, 0u, bo);
                                 if (GM & 1)
                                     ell_n = TLf(sll);
                                 if (GM & 2)
