@@ -246,25 +246,24 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
         }
         const int32_t mx = 2 * threshold - 1 - remaining;
         const int32_t v = (int32_t)bits(nbits);
-        int32_t count;
-        if ((v & (threshold - 1)) < mx) {
-            count = v & (threshold - 1);
-            pos += nbits - 1;
-        } else {
-            count = v & (2 * threshold - 1);
-            if (count >= threshold)
-                count -= mx;
-            pos += nbits;
-        }
+        // (both field widths as selects, no branch per symbol)
+        const bool lo = (v & (threshold - 1)) < mx;
+        const int32_t wide = v & (2 * threshold - 1);
+        int32_t count = lo ? v & (threshold - 1) : wide >= threshold ? wide - mx : wide;
+        pos += lo ? nbits - 1 : nbits;
         count--;
         remaining -= count < 0 ? -count : count;
         if (count && lane_id() == 0)
             *lp<int16_t>(&L.norm[sym]) = (int16_t)count;
         sym++;
         prev0 = count == 0;
-        while (remaining < threshold) {
-            nbits--;
-            threshold >>= 1;
+        // FSE_readNCount's `while (remaining < threshold) { nbBits--;
+        // threshold >>= 1; }`: remaining stays >= 1 (a count never exceeds
+        // it), so the field width becomes min(nbits, log2(remaining) + 1)
+        {
+            const uint32_t w1 = 32u - (uint32_t)__builtin_clz((uint32_t)remaining);
+            nbits = min(nbits, w1);
+            threshold = 1 << (nbits - 1);
         }
         if (pos > 8 * 256) {   // ran off the window: no valid description is that long
             *err = ZE_CORRUPT;
