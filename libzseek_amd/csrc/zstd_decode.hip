@@ -663,6 +663,25 @@ struct Frame {
     uint32_t nblk, blk_cap;
     uint8_t *slots;
     HufJob *jobs;
+    // the one-frame route's helper wave (HelpBox below): a posted Huffman
+    // description (its block's jobs and table log completed at the block's end)
+    struct HelpBox *help = nullptr;
+    bool posted = false;
+    uint32_t post_ns = 0;
+};
+
+// The one-frame route's frame kernel runs a second wave beside the frame's:
+// a block's Huffman description (a serial walk of its weights, ~60K cycles)
+// is decoded there while the frame's wave parses the block's sequence
+// section (the FSE tables, ~90K) -- the description's size is known from its
+// first byte, so nothing after it waits for its decode.  One box in LDS per
+// workgroup; the waves meet at two barriers per posted description (A: posted
+// or done, B: decoded).
+struct HelpBox {
+    uint32_t kind;   // 1 = decode the description at q (qn bytes) into slot g; 0 = done
+    uint32_t q, qn;
+    uint32_t g;
+    uint32_t hs, lg;   // result: bytes used (0 = corrupt), table log
 };
 
 // append an op (wave-uniform; lane 0 writes).  The last slot is kept for the
@@ -764,13 +783,37 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint
         if (ns == 4 && size == 0)
             return ZE_CORRUPT;
         const uint32_t x2 = ns == 4 ? huf_select_x2(size, csize) : 0u;
-        uint32_t lg = 0;
-        ZF_T0(t0)
-        const uint32_t hs =
-            huf_read(L, F.I, wx, q, qn, &lg, reinterpret_cast<uint16_t *>(F.slots + g * kZSlot));
-        ZF_ADD(1, t0)
-        if (!hs)
-            return ZE_CORRUPT;
+        uint32_t lg = 0, hs = 0;
+        if (F.help) {
+            // the helper wave decodes it; its size from its first byte (the
+            // size checks huf_read makes before decoding)
+            const uint32_t h0 = uni(wb(L, wx, F.I, q));
+            if (h0 < 128) {
+                if (1 + h0 > qn)
+                    return ZE_CORRUPT;
+                hs = 1 + h0;
+            } else {
+                const uint32_t bytes = (h0 - 127 + 1) / 2;
+                if (1 + bytes > qn)
+                    return ZE_CORRUPT;
+                hs = 1 + bytes;
+            }
+            if (lane == 0) {
+                F.help->kind = 1;
+                F.help->q = q;
+                F.help->qn = qn;
+                F.help->g = (uint32_t)g;
+            }
+            __syncthreads();   // A: posted
+            F.posted = true;
+            lg = 1;   // (placeholder: the log arrives at the block's end)
+        } else {
+            ZF_T0(t0)
+            hs = huf_read(L, F.I, wx, q, qn, &lg, reinterpret_cast<uint16_t *>(F.slots + g * kZSlot));
+            ZF_ADD(1, t0)
+            if (!hs)
+                return ZE_CORRUPT;
+        }
         F.huf_log = lg;
         F.huf_slot = (uint32_t)g | x2 << 27;
         q += hs;
@@ -814,9 +857,10 @@ __device__ __forceinline__ uint32_t literals(ZLds &L, Frame &F, uint64_t g, uint
         J.len = lane == 0 ? len[0] : lane == 1 ? len[1] : lane == 2 ? len[2] : len[3];
         J.cnt = cnt;
         J.lim = cnt < room ? cnt : room;
-        J.tab = F.huf_slot | lg << 28;
+        J.tab = F.huf_slot | (F.posted ? 0u : lg << 28);   // (posted: the log is or-ed in later)
         F.jobs[4 * g + lane] = J;
     }
+    F.post_ns = ns;
     *huf = true;
     *used = lh + csize;
     *litn = size;
@@ -885,7 +929,7 @@ __device__ __forceinline__ uint32_t seq_table(ZLds &L, Frame &F, uint32_t t, uin
 // One compressed block [p, p + n): literals, then the sequence section's
 // header and tables -> the block's slot and ops.  Returns 0 or a zstd error.
 // Wave-wide.
-__device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_t n)
+__device__ __forceinline__ uint32_t block_body(ZLds &L, Frame &F, uint32_t p, uint32_t n)
 {
     const uint32_t lane = lane_id();
     if (n >= kZBlockMax)
@@ -962,6 +1006,32 @@ __device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_
         return ZE_GENERIC;
     F.lo += litn;
     return 0;
+}
+
+// A block; with the helper wave, its posted Huffman description joined at the
+// end: a corrupt description is the block's error (libzstd decodes the
+// literals before the sequences), its ops dropped and its jobs cleared, else
+// the table log goes into the block's jobs.
+__device__ __forceinline__ uint32_t block(ZLds &L, Frame &F, uint32_t p, uint32_t n)
+{
+    const uint32_t nop0 = F.nop;
+    const uint32_t e = block_body(L, F, p, n);
+    if (!F.posted)
+        return e;
+    __syncthreads();   // B: decoded
+    F.posted = false;
+    const uint32_t lane = lane_id(), hs = F.help->hs, lg = F.help->lg, g = F.help->g;
+    if (!hs) {
+        if (lane < 4)
+            F.jobs[4 * g + lane] = HufJob{0, 0, 0, 0, 0, 0};
+        F.nop = nop0;
+        F.huf_log = 0;
+        return ZE_CORRUPT;
+    }
+    F.huf_log = lg;
+    if (lane < F.post_ns)
+        F.jobs[4 * g + lane].tab |= lg << 28;
+    return e;
 }
 
 // One seek-table entry: every zstd frame in it (ZSTD_decompressDCtx) -> ops.
@@ -1269,21 +1339,52 @@ __global__ __launch_bounds__(1024) void zstd_scan_kernel(const uint32_t *__restr
 // (raw / RLE literals straight into the scratch), Huffman and FSE tables
 // (built in LDS, stored to the block's slot), Huffman stream jobs and the op
 // list the sequence kernel replays.
+// HELP: one frame per workgroup, wave 1 the helper wave (HelpBox above);
+// else kZW frames per workgroup, one per wave.
+template <bool HELP>
 __global__ __launch_bounds__(64 * kZW) __attribute__((amdgpu_waves_per_eu(4))) void zstd_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ lit, uint64_t lit_cap, const uint64_t *__restrict__ rec_base,
     uint64_t capacity, const uint64_t *__restrict__ blk_base, uint8_t *__restrict__ ops,
     uint8_t *__restrict__ slots, uint8_t *__restrict__ jobs, uint32_t f0)
 {
+    static_assert(kZW >= 2, "the helper wave needs a second ZLds");
     __shared__ ZLds lds[kZW];
+    __shared__ HelpBox box;
     ZF_T0(tk)
     const uint32_t w = threadIdx.x >> 6;
-    const uint32_t f = uni(f0 + blockIdx.x * kZW + w);   // frames [f0, n)
+    const uint32_t f = HELP ? uni(f0 + blockIdx.x) : uni(f0 + blockIdx.x * kZW + w);   // frames [f0, n)
     if (f >= n)
-        return;
+        return;   // (HELP: the whole workgroup)
     ZLds &L = lds[w];
     const FrameDesc d = desc[f];
     Frame F;
+    if (HELP && w == 1) {
+        // helper: the frame's In, then the posted descriptions until done
+        const uintptr_t fa = reinterpret_cast<uintptr_t>(comp + d.c_off);
+        F.I.base4 = reinterpret_cast<const uint8_t *>(fa & ~(uintptr_t)3);
+        F.I.s0 = (uint32_t)(fa & 3);
+        F.I.amax = d.c_size ? (F.I.s0 + d.c_size - 1) & ~3u : 0;
+        for (;;) {
+            __syncthreads();   // A
+            if (uni(box.kind) == 0)
+                break;
+            const uint32_t q = uni(box.q), qn = uni(box.qn), g = uni(box.g);
+            const uint32_t wx = stage_win(L, F.I, q);
+            uint32_t lg = 0;
+            ZF_T0(t0)
+            const uint32_t hs = huf_read(L, F.I, wx, q, qn, &lg, reinterpret_cast<uint16_t *>(slots + (uint64_t)g * kZSlot));
+            ZF_ADD(1, t0)
+            if (lane_id() == 0) {
+                box.hs = hs;
+                box.lg = lg;
+            }
+            __syncthreads();   // B
+        }
+        return;
+    }
+    if (HELP)
+        F.help = &box;
     const uintptr_t fa = reinterpret_cast<uintptr_t>(comp + d.c_off);
     F.I.base4 = reinterpret_cast<const uint8_t *>(fa & ~(uintptr_t)3);
     F.I.s0 = (uint32_t)(fa & 3);
@@ -1324,6 +1425,11 @@ __global__ __launch_bounds__(64 * kZW) __attribute__((amdgpu_waves_per_eu(4))) v
         put_op(F, OP_ERR, (uint32_t)zerr(e));
     else
         put_op(F, OP_DONE);
+    if (HELP) {
+        if (lane_id() == 0)
+            box.kind = 0;
+        __syncthreads();   // A: done
+    }
     ZF_ADD(0, tk)
 #ifdef ZSK_TUNING
     if (lane_id() == 0)
@@ -3052,9 +3158,20 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             continue;
         const uint64_t b0 = s->total[4 + c], b1 = s->total[5 + c];
         hipEvent_t tf = kernel_span_begin(stream);   // (per-kernel spans: timing on only)
-        hipLaunchKernelGGL(zstd_frame_kernel, dim3((m + kZW - 1) / kZW), dim3(64 * kZW), 0, stream, d_desc, f1,
-                           d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops, s->slots,
-                           s->hjobs, f0);
+        // (the one-frame route: a workgroup per frame, its second wave the
+        // Huffman descriptions' helper; env ZSEEK_FRAME_HELP=0: off)
+        static const bool help_off = [] {
+            const char *v = getenv("ZSEEK_FRAME_HELP");
+            return v && !strcmp(v, "0");
+        }();
+        if (one && !help_off)
+            hipLaunchKernelGGL(zstd_frame_kernel<true>, dim3(m), dim3(64 * kZW), 0, stream, d_desc, f1, d_comp,
+                               s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base, s->ops, s->slots,
+                               s->hjobs, f0);
+        else
+            hipLaunchKernelGGL(zstd_frame_kernel<false>, dim3((m + kZW - 1) / kZW), dim3(64 * kZW), 0, stream,
+                               d_desc, f1, d_comp, s->lit, s->lit_cap, s->rec_base, s->items_cap, s->blk_base,
+                               s->ops, s->slots, s->hjobs, f0);
 #ifdef ZSK_TUNING
         {
             static const bool ztimers = getenv("ZSEEK_ZFRAME_TIMERS") != nullptr;
