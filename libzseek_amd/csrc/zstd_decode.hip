@@ -2258,7 +2258,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     __shared__ __attribute__((aligned(16))) uint16_t ftab[CELLS && !ONE ? LANES * CELLS : 8];
     __shared__ __attribute__((aligned(16))) uint8_t sstage[ONE ? kSeqStage + 32 : 16];
     __shared__ uint64_t xtab[ONE ? kSeqOneCells : 1];   // ONE: the expanded cells (below)
-    __shared__ __attribute__((aligned(16))) uint32_t srec[ONE ? 64 * 4 : 4];   // ONE: a batch's records
+    __shared__ __attribute__((aligned(16))) uint32_t srec[ONE ? 65 * 8 : 4];   // ONE: a batch's records (from [1])
 #ifdef ZSK_TUNING
     const uint64_t tk0 = __builtin_readcyclecounter(), rt0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tloop = 0, nseqs = 0;
@@ -2361,19 +2361,22 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         const uint16_t *TL = gt + kFseOff[0], *TO = gt + kFseOff[1], *TM = gt + kFseOff[2];
                       if constexpr (ONE) {
                         // the one-frame replay: every cell expanded once by the
-                        // wave into 8 bytes -- next-state base (16 bits), its bit
-                        // count (7), a bad-symbol flag (bit 23), the value's extra
-                        // bits (8) | the value's baseline (32) -- so a sequence's
-                        // chain is one LDS read per table (no code-table read,
-                        // no next-state arithmetic); each sequence's next cells
-                        // are read as soon as its states are known, ahead of its
-                        // checks and item stores.  Same bit order, values and
-                        // checks as the loop below.
+                        // wave into 8 bytes -- lo: the LDS address of its next
+                        // state's base cell; hi: the state's bit count (bits
+                        // 0-3, bit 4 clear: a bitfield extract's width or offset
+                        // operand as it is), the value's extra bits (8-12), a
+                        // bad-symbol flag (13), the symbol (16-21), the cell's
+                        // whole bit count (value + state, 24-29) -- so a
+                        // sequence's chain is one LDS read per table and its next
+                        // cells' addresses two ops away from the bits (no
+                        // code-table read, no next-state arithmetic).  Same bit
+                        // order, values and checks as the loop below.
                         const uint32_t xb = ldsaddr(xtab), ncell = nll + nof + nml;
                         wave_lds_sync();
                         for (uint32_t cix = lane; cix < ncell; cix += 64) {
                             const uint32_t t = cix < nll ? 0u : cix < nll + nof ? 1u : 2u;
-                            const uint32_t x = cix - (t == 0 ? 0u : t == 1 ? nll : nll + nof);
+                            const uint32_t toff = t == 0 ? 0u : t == 1 ? nll : nll + nof;
+                            const uint32_t x = cix - toff;
                             const uint32_t e = t == 0 ? TL[x] : t == 1 ? TO[x] : TM[x];
                             const uint32_t tl = t == 0 ? tll : t == 1 ? tof : tml;
                             const uint32_t sym = e & 63, ns = e >> 6;
@@ -2382,10 +2385,10 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             const bool bad = sym > (t == 0 ? 35u : t == 1 ? 31u : 52u);
                             // OF: value 2^code + code extra bits; LL / ML: the code table
                             const uint32_t code = bad || t == 1 ? 0u : codes[t == 0 ? sym : 36 + sym];
-                            const uint32_t base = bad ? 0u : t == 1 ? 1u << sym : code & 0xFFFFFF;
                             const uint32_t add = bad ? 0u : t == 1 ? sym : code >> 24;
-                            const uint32_t lo32 = (nbase & 0xFFFF) | (nbits & 0x7F) << 16 | (bad ? 1u : 0u) << 23 | add << 24;
-                            *la<uint64_t>(xb + 8 * cix) = (uint64_t)base << 32 | lo32;
+                            const uint32_t hi32 = nbits | add << 8 | (bad ? 1u : 0u) << 13 | (bad ? 0u : sym) << 16 |
+                                                  (add + nbits) << 24;
+                            *la<uint64_t>(xb + 8 * cix) = (uint64_t)hi32 << 32 | (xb + 8 * (toff + nbase));
                         }
                         wave_lds_sync();
                         // (an opaque per-lane zero in the addresses keeps the chain
@@ -2399,70 +2402,107 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         auto XO = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * (nll + x) + zv); };
                         auto XM = [&](uint32_t x) { return *la<uint64_t>(xb + 8 * (nll + nof + x) + zv); };
                         sr_load<ONE>(b);
-                        uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
-                        sr_done(b);
-                        sr_issue<ONE>(b);
-                        uint64_t cl = XL(sll), co = XO(sof), cm = XM(sml);
+                        uint64_t cl, co, cm;
+                        {
+                            const uint32_t sll = sr_take(b, tll), sof = sr_take(b, tof), sml = sr_take(b, tml);
+                            sr_done(b);
+                            cl = XL(sll);
+                            co = XO(sof);
+                            cm = XM(sml);
+                        }
+                        // the window: stream dwords [(cur >> 5) - 3, + 4), the
+                        // staged zeros below the stream for a cursor past its start
+                        const uint32_t sl = b.sl;
+                        auto win = [&](int32_t cur) {
+                            const int32_t k0 = (cur >> 5) - 3;
+                            return *la<u32x4_a4>(sl + 4u * (uint32_t)(k0 > -4 ? k0 : -4) + zv);
+                        };
+                        int32_t cur = b.cur;
+                        u32x4 W = win(cur);
 #ifdef ZSK_TUNING
                         const uint64_t tl0 = __builtin_readcyclecounter();
                         nseqs += nseq;
 #endif
                         // batches of up to 64 sequences: (1) the chain, wave-
-                        // uniform -- cells, bits, next states and repeat offsets
-                        // -> one 16-byte record per sequence in LDS, stopping at
-                        // a bad cell; (2) lane q takes record q: item slots, the
-                        // output / literal prefix sums, the replay's four checks
-                        // in its order, the first failing sequence by ballot, and
-                        // the items of the sequences before it (a lane's own
-                        // stores).  Everything the serial loop below leaves --
-                        // items, o, lp_, S.k, err -- is the same.
+                        // uniform -- cells, state bits, next states -> one 20-byte
+                        // record per sequence in LDS: its 64 value bits and its
+                        // cells' hi words (a bad cell goes on: its state fields
+                        // are valid); (2) lane q takes record q: the values,
+                        // repeat offsets, item slots, the output / literal prefix
+                        // sums, the replay's
+                        // checks in its order (a bad cell first), the first
+                        // failing sequence by ballot, and the items of the
+                        // sequences before it (a lane's own stores).  Everything
+                        // the serial loop below leaves -- items, o, lp_, S.k,
+                        // err -- is the same.
                         const uint32_t rec = ldsaddr(srec);
                         for (uint32_t i = 0; i < nseq && !err;) {
                             const uint32_t nb = min(64u, nseq - i);
                             uint32_t nd = 0;
-                            bool afail = false;
                             wave_lds_sync();   // the last batch's records read
+                            // (a sequence's record is stored at the start of the
+                            // next one, ahead of that one's reads: a store after
+                            // them would hold the wait for them; record q at
+                            // [q + 1], [0] taking the first, empty, store)
+                            u32x4 pend = (u32x4){0, 0, 0, 0};
+                            uint32_t pendh = 0;
                             for (; nd < nb; nd++) {
-                                sr_use<ONE>(b);
-                                // (a ballot: the exit stays a uniform branch, not
-                                // an exec-mask loop exit)
-                                if (__ballot((((uint32_t)cl | (uint32_t)co | (uint32_t)cm) >> 23) & 1)) {
-                                    afail = true;
-                                    break;
-                                }
-                                uint32_t ofv, ml, ll;
-                                {
-                                    ofv = (uint32_t)(co >> 32) + sr_take(b, (uint32_t)co >> 24);
-                                    sr_fill(b);
-                                    // the ML and LL extra bits (<= 32, ML above
-                                    // LL) in one extract, then the three state
-                                    // fields (<= 26: LL, ML, OF from the top)
-                                    const uint32_t mlb = (uint32_t)cm >> 24, llb = (uint32_t)cl >> 24;
-                                    const uint32_t X = (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)(mlb + llb)) & 63));
-                                    b.nb -= (int32_t)(mlb + llb);
-                                    ll = (uint32_t)(cl >> 32) + __builtin_amdgcn_ubfe(X, 0u, llb);
-                                    ml = (uint32_t)(cm >> 32) + __builtin_amdgcn_ubfe(X, llb, mlb);
-                                    sr_fill(b);
-                                    const uint32_t lln = ((uint32_t)cl >> 16) & 0x7F, mln = ((uint32_t)cm >> 16) & 0x7F,
-                                                   ofn = ((uint32_t)co >> 16) & 0x7F;
-                                    const uint32_t Y =
-                                        (uint32_t)(b.C >> ((uint32_t)(b.nb - (int32_t)(lln + mln + ofn)) & 63));
-                                    b.nb -= (int32_t)(lln + mln + ofn);
-                                    sof = ((uint32_t)co & 0xFFFF) + __builtin_amdgcn_ubfe(Y, 0u, ofn);
-                                    sml = ((uint32_t)cm & 0xFFFF) + __builtin_amdgcn_ubfe(Y, ofn, mln);
-                                    sll = ((uint32_t)cl & 0xFFFF) + __builtin_amdgcn_ubfe(Y, ofn + mln, lln);
-                                    sr_done(b);
-                                    sr_issue<ONE>(b);
-                                }
-                                cl = XL(sll);
-                                co = XO(sof);
-                                cm = XM(sml);
-                                *la<u32x4>(rec + 16 * nd) = (u32x4){ofv, ml, ll, 0u};
+                                *la<u32x4>(rec + 32 * nd) = pend;
+                                *la<uint32_t>(rec + 32 * nd + 16) = pendh;
+                                // the 96 stream bits below cur, top-aligned: bit
+                                // 95 of N3:N2:N1 is stream bit cur - 1 (the
+                                // align takes the shift's low five bits)
+                                const uint32_t N3 = __builtin_amdgcn_alignbit(W.w, W.z, (uint32_t)cur),
+                                               N2 = __builtin_amdgcn_alignbit(W.z, W.y, (uint32_t)cur),
+                                               N1 = __builtin_amdgcn_alignbit(W.y, W.x, (uint32_t)cur);
+                                const uint64_t H = (uint64_t)N3 << 32 | N2, M = (uint64_t)N2 << 32 | N1;
+                                const uint32_t hl = (uint32_t)(cl >> 32), hm = (uint32_t)(cm >> 32), ho = (uint32_t)(co >> 32);
+                                // the sequence's bits: OF, ML, LL values, then the
+                                // LL, ML, OF states (T <= 31 + 16 + 16 + 26 = 89)
+                                const uint32_t T = (hl >> 24) + (hm >> 24) + (ho >> 24);
+                                const uint32_t yH = (uint32_t)(H >> ((64 - T) & 63)), yM = (uint32_t)(M >> ((96 - T) & 63));
+                                // (a select in asm: the compiler made the choice an
+                                // if / else over the exec mask, twice the ops)
+                                uint32_t Y;
+                                asm("v_cmp_ge_u32 vcc, 64, %1\n\tv_cndmask_b32 %0, %2, %3, vcc"
+                                    : "=v"(Y)
+                                    : "v"(T), "v"(yM), "v"(yH)
+                                    : "vcc");
+                                // (the extract takes offset and width from the low
+                                // five bits: the state counts straight from hi)
+                                const uint32_t ao = (uint32_t)co + (__builtin_amdgcn_ubfe(Y, 0, ho) << 3),
+                                               am = (uint32_t)cm + (__builtin_amdgcn_ubfe(Y, ho, hm) << 3),
+                                               al = (uint32_t)cl + (__builtin_amdgcn_ubfe(Y, ho + hm, hl) << 3);
+                                const int32_t cur2 = cur - (int32_t)T;
+                                // the next sequence's reads; this one's values
+                                // are the vector phase's, from H and the cells
+                                const u32x4 W2 = win(cur2);
+                                const uint64_t cl2 = *la<uint64_t>(al), cm2 = *la<uint64_t>(am), co2 = *la<uint64_t>(ao);
+                                pend = (u32x4){N3, N2, ho, hm};
+                                pendh = hl;
+                                cl = cl2;
+                                cm = cm2;
+                                co = co2;
+                                W = W2;
+                                cur = cur2;
                             }
+                            *la<u32x4>(rec + 32 * nd) = pend;
+                            *la<uint32_t>(rec + 32 * nd + 16) = pendh;
                             wave_lds_sync();
                             const bool on = lane < nd;
-                            const u32x4 R = on ? *la<u32x4>(rec + 16 * lane) : (u32x4){0, 0, 0, 0};
-                            const uint32_t ofv = R.x, ml = R.y, ll = R.z;
+                            uint32_t ofv = 0, ml = 0, ll = 0, bad = 0;
+                            if (on) {
+                                const u32x4 R = *la<u32x4>(rec + 32 * (lane + 1));
+                                const uint32_t hl = *la<uint32_t>(rec + 32 * (lane + 1) + 16), ho = R.z, hm = R.w;
+                                const uint32_t ob = __builtin_amdgcn_ubfe(ho, 8, 5), mb = __builtin_amdgcn_ubfe(hm, 8, 5),
+                                               lb = __builtin_amdgcn_ubfe(hl, 8, 5), vb = ob + mb + lb;
+                                const uint64_t H = (uint64_t)R.x << 32 | R.y;
+                                const uint32_t X = (uint32_t)(H >> ((64 - vb) & 63));
+                                ofv = (1u << ob) + __builtin_amdgcn_ubfe(R.x, 32 - ob, ob);
+                                ll = (codes[__builtin_amdgcn_ubfe(hl, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, 0, lb);
+                                ml = (codes[36 + __builtin_amdgcn_ubfe(hm, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, lb, mb);
+                                bad = ((ho | hm | hl) >> 13) & 1;
+                            }
                             // repeat offsets (RFC 8878 §3.1.2.5) by a scan: each
                             // sequence maps the history (a, b, c) = (rep0, rep1,
                             // rep2) to a new one -- a new offset v: (v, a, b);
@@ -2547,7 +2587,8 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             const uint32_t ni = ext ? 2 + pad : 1;
                             const uint32_t ill = wave_incl_add(ll), iol = wave_incl_add(ll + ml);
                             const uint32_t lpq = lp_ + ill - ll, oq = o + iol - (ll + ml);
-                            const uint32_t kind = ll + ml > cap - oq ? (uint32_t)ZE_DST_SMALL
+                            const uint32_t kind = bad                ? (uint32_t)ZE_CORRUPT
+                                                  : ll + ml > cap - oq ? (uint32_t)ZE_DST_SMALL
                                                   : le - lpq < ll    ? (uint32_t)ZE_CORRUPT
                                                   : off > oq + ll    ? (uint32_t)ZE_CORRUPT
                                                   : kq + ni > S.cap  ? (uint32_t)ZE_GENERIC
@@ -2571,11 +2612,10 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             } else {
                                 if (nd)
                                     S.k = lane_val(kq + ni, (int)nd - 1);
-                                if (afail)
-                                    err = ZE_CORRUPT;
                             }
                             i += nd;
                         }
+                        b.cur = cur;
 #ifdef ZSK_TUNING
                         tloop += __builtin_readcyclecounter() - tl0;
 #endif
