@@ -2258,7 +2258,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     __shared__ __attribute__((aligned(16))) uint16_t ftab[CELLS && !ONE ? LANES * CELLS : 8];
     __shared__ __attribute__((aligned(16))) uint8_t sstage[ONE ? kSeqStage + 32 : 16];
     __shared__ uint64_t xtab[ONE ? kSeqOneCells : 1];   // ONE: the expanded cells (below)
-    __shared__ __attribute__((aligned(16))) uint32_t srec[ONE ? 65 * 8 : 4];   // ONE: a batch's records (from [1])
+    __shared__ __attribute__((aligned(16))) uint32_t srec[ONE ? 64 * 8 : 4];   // ONE: a batch's records
 #ifdef ZSK_TUNING
     const uint64_t tk0 = __builtin_readcyclecounter(), rt0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tloop = 0, nseqs = 0;
@@ -2424,10 +2424,10 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         nseqs += nseq;
 #endif
                         // batches of up to 64 sequences: (1) the chain, wave-
-                        // uniform -- cells, state bits, next states -> one 20-byte
+                        // uniform -- cells, state bits, next states -> one 32-byte
                         // record per sequence in LDS: its 64 value bits and its
-                        // cells' hi words (a bad cell goes on: its state fields
-                        // are valid); (2) lane q takes record q: the values,
+                        // three cells (a bad cell goes on: its state fields are
+                        // valid); (2) lane q takes record q: the values,
                         // repeat offsets, item slots, the output / literal prefix
                         // sums, the replay's
                         // checks in its order (a bad cell first), the first
@@ -2438,29 +2438,32 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                         const uint32_t rec = ldsaddr(srec);
                         for (uint32_t i = 0; i < nseq && !err;) {
                             const uint32_t nb = min(64u, nseq - i);
-                            uint32_t nd = 0;
+                            const uint32_t nd = nb;
                             wave_lds_sync();   // the last batch's records read
-                            // (a sequence's record is stored at the start of the
-                            // next one, ahead of that one's reads: a store after
-                            // them would hold the wait for them; record q at
-                            // [q + 1], [0] taking the first, empty, store)
-                            u32x4 pend = (u32x4){0, 0, 0, 0};
-                            uint32_t pendh = 0;
-                            for (; nd < nb; nd++) {
-                                *la<u32x4>(rec + 32 * nd) = pend;
-                                *la<uint32_t>(rec + 32 * nd + 16) = pendh;
+                            // (lane 0 alone runs the chain: every lane's copy of
+                            // a uniform read or store costs the LDS 64 times the
+                            // bytes; the chain's registers are lane 0's)
+                            if (lane == 0)
+                            for (uint32_t q = 0; q < nb; q++) {
                                 // the 96 stream bits below cur, top-aligned: bit
                                 // 95 of N3:N2:N1 is stream bit cur - 1 (the
                                 // align takes the shift's low five bits)
                                 const uint32_t N3 = __builtin_amdgcn_alignbit(W.w, W.z, (uint32_t)cur),
                                                N2 = __builtin_amdgcn_alignbit(W.z, W.y, (uint32_t)cur),
                                                N1 = __builtin_amdgcn_alignbit(W.y, W.x, (uint32_t)cur);
-                                const uint64_t H = (uint64_t)N3 << 32 | N2, M = (uint64_t)N2 << 32 | N1;
+                                const uint64_t H = (uint64_t)N3 << 32 | N2;
                                 const uint32_t hl = (uint32_t)(cl >> 32), hm = (uint32_t)(cm >> 32), ho = (uint32_t)(co >> 32);
                                 // the sequence's bits: OF, ML, LL values, then the
                                 // LL, ML, OF states (T <= 31 + 16 + 16 + 26 = 89)
-                                const uint32_t T = (hl >> 24) + (hm >> 24) + (ho >> 24);
-                                const uint32_t yH = (uint32_t)(H >> ((64 - T) & 63)), yM = (uint32_t)(M >> ((96 - T) & 63));
+                                // (byte-select adds: the three counts are the cells' top bytes)
+                                uint32_t T;
+                                asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+                                    "v_add_u32_sdwa %0, %0, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+                                    : "=&v"(T)
+                                    : "v"(hl), "v"(hm), "v"(ho));
+                                // (T <= 64: from N3:N2; else at bit 96 - T < 32 of N2:N1)
+                                const uint32_t yH = (uint32_t)(H >> ((64 - T) & 63)),
+                                               yM = __builtin_amdgcn_alignbit(N2, N1, 0u - T);
                                 // (a select in asm: the compiler made the choice an
                                 // if / else over the exec mask, twice the ops)
                                 uint32_t Y;
@@ -2474,31 +2477,33 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                                am = (uint32_t)cm + (__builtin_amdgcn_ubfe(Y, ho, hm) << 3),
                                                al = (uint32_t)cl + (__builtin_amdgcn_ubfe(Y, ho + hm, hl) << 3);
                                 const int32_t cur2 = cur - (int32_t)T;
-                                // the next sequence's reads; this one's values
-                                // are the vector phase's, from H and the cells
+                                // the record (this sequence's values are the
+                                // vector phase's, from H and the cells), stored
+                                // ahead of the next sequence's reads: after them,
+                                // the wait for them would wait for it too
+                                *la<uint64_t>(rec + 32 * q) = H;
+                                *la<uint64_t>(rec + 32 * q + 8) = cl;
+                                *la<uint64_t>(rec + 32 * q + 16) = cm;
+                                *la<uint64_t>(rec + 32 * q + 24) = co;
                                 const u32x4 W2 = win(cur2);
                                 const uint64_t cl2 = *la<uint64_t>(al), cm2 = *la<uint64_t>(am), co2 = *la<uint64_t>(ao);
-                                pend = (u32x4){N3, N2, ho, hm};
-                                pendh = hl;
                                 cl = cl2;
                                 cm = cm2;
                                 co = co2;
                                 W = W2;
                                 cur = cur2;
                             }
-                            *la<u32x4>(rec + 32 * nd) = pend;
-                            *la<uint32_t>(rec + 32 * nd + 16) = pendh;
                             wave_lds_sync();
                             const bool on = lane < nd;
                             uint32_t ofv = 0, ml = 0, ll = 0, bad = 0;
                             if (on) {
-                                const u32x4 R = *la<u32x4>(rec + 32 * (lane + 1));
-                                const uint32_t hl = *la<uint32_t>(rec + 32 * (lane + 1) + 16), ho = R.z, hm = R.w;
+                                const u32x4 R = *la<u32x4>(rec + 32 * lane), R2 = *la<u32x4>(rec + 32 * lane + 16);
+                                const uint32_t hl = R.w, hm = R2.y, ho = R2.w;
                                 const uint32_t ob = __builtin_amdgcn_ubfe(ho, 8, 5), mb = __builtin_amdgcn_ubfe(hm, 8, 5),
                                                lb = __builtin_amdgcn_ubfe(hl, 8, 5), vb = ob + mb + lb;
-                                const uint64_t H = (uint64_t)R.x << 32 | R.y;
+                                const uint64_t H = (uint64_t)R.y << 32 | R.x;
                                 const uint32_t X = (uint32_t)(H >> ((64 - vb) & 63));
-                                ofv = (1u << ob) + __builtin_amdgcn_ubfe(R.x, 32 - ob, ob);
+                                ofv = (1u << ob) + __builtin_amdgcn_ubfe(R.y, 32 - ob, ob);
                                 ll = (codes[__builtin_amdgcn_ubfe(hl, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, 0, lb);
                                 ml = (codes[36 + __builtin_amdgcn_ubfe(hm, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, lb, mb);
                                 bad = ((ho | hm | hl) >> 13) & 1;
@@ -2615,7 +2620,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                             }
                             i += nd;
                         }
-                        b.cur = cur;
+                        b.cur = __builtin_amdgcn_readlane(cur, 0);
 #ifdef ZSK_TUNING
                         tloop += __builtin_readcyclecounter() - tl0;
 #endif
