@@ -201,6 +201,10 @@ __device__ __forceinline__ uint32_t wb(const ZLds &L, uint32_t wx, const In &I, 
 __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t avail, uint32_t max_sym,
                                                 uint32_t max_log, uint32_t *tlog, uint32_t *nsym, uint32_t *err)
 {
+    // (uniform in the compiler's eyes: else the walk is a divergent loop,
+    // every branch an exec-mask save / restore)
+    wofs = uni(wofs);
+    avail = uni(avail);
     uint32_t pos = 8 * wofs, wp = pos + 64;   // forces the first load
     uint64_t W = 0;
     // the window's 64 dwords one per lane: a reload is two readlanes, not an
@@ -420,7 +424,7 @@ __device__ __forceinline__ uint32_t huf_read(ZLds &L, const In &I, uint32_t wx, 
 {
     const uint32_t lane = lane_id();
     const uint32_t hb = uni(wb(L, wx, I, p));
-    const uint32_t wofs = I.s0 + p - wx + 1;   // window offset of the description body
+    const uint32_t wofs = uni(I.s0 + p - wx + 1);   // window offset of the description body (uniform: see read_ncount)
     uint32_t nw = 0, used = 0, err = 0;
     if (hb < 128) {
         if (1 + hb > avail || wofs + hb > 256)
