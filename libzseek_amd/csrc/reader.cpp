@@ -410,11 +410,15 @@ void ht_report()
 {
     static const bool on = getenv("ZSEEK_HOST_TIMERS") != nullptr;
     const uint64_t b = g_ht[4].load();
-    if (!on || b == 0 || b % 200)
+    // (the first 20 batches -- allocations, first launches -- left out)
+    if (b == 20)
+        for (int i : {0, 1, 2, 3, 5})
+            g_ht[i] = 0;
+    if (!on || b <= 20 || b % 200)
         return;
     fprintf(stderr, "host per batch (us): read %.1f enqueue %.1f to-wait %.1f wait %.1f after %.1f (%llu batches)\n",
-            g_ht[0] / 1e3 / b, g_ht[1] / 1e3 / b, g_ht[5] / 1e3 / b, g_ht[2] / 1e3 / b, g_ht[3] / 1e3 / b,
-            (unsigned long long)b);
+            g_ht[0] / 1e3 / (b - 20), g_ht[1] / 1e3 / (b - 20), g_ht[5] / 1e3 / (b - 20), g_ht[2] / 1e3 / (b - 20),
+            g_ht[3] / 1e3 / (b - 20), (unsigned long long)(b - 20));
 }
 thread_local uint64_t t_queued = 0;
 #define HT_T(v) const uint64_t v = ht_now();

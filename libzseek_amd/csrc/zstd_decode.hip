@@ -1900,20 +1900,30 @@ constexpr uint32_t kHufOneStage = 65536;    // stream bytes staged (else the ser
 constexpr uint32_t kHufOneOut = 32768;      // symbols staged (else the serial walk)
 constexpr uint32_t kHufOneMaxLg = 12;
 
-__global__ __launch_bounds__(kHufOneT) void zstd_huf_one_kernel(const uint8_t *__restrict__ jobs,
-                                                                const uint8_t *__restrict__ comp,
-                                                                const uint8_t *__restrict__ slots,
-                                                                uint8_t *__restrict__ lit,
-                                                                uint8_t *__restrict__ hbad)
+// its LDS (a struct: the one-frame decode kernel below shares it with the
+// sequence replay's, as a union)
+struct HufOneLds {
+    __attribute__((aligned(16))) uint8_t sst[16 + kHufOneStage + 32];
+    __attribute__((aligned(16))) uint8_t obuf[kHufOneOut + 16];
+    __attribute__((aligned(16))) uint16_t tab[1u << kHufOneMaxLg];
+    uint32_t cand[kHufOneT * kHufOneMaxLg];   // exit offset | symbols << 8, per chunk and entry
+    uint32_t ent[kHufOneT];                   // true entry | output base << 4
+    uint32_t verdict;
+    __attribute__((aligned(16))) uint8_t rings[kRS * 1024];   // the serial walk's ring
+};
+
+// job j by the workgroup's kHufOneT threads (t = thread index)
+__device__ __forceinline__ void huf_one_body(HufOneLds &H, uint32_t j, uint32_t t, const uint8_t *__restrict__ jobs,
+                                             const uint8_t *__restrict__ comp, const uint8_t *__restrict__ slots,
+                                             uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t sst[16 + kHufOneStage + 32];
-    __shared__ __attribute__((aligned(16))) uint8_t obuf[kHufOneOut + 16];
-    __shared__ __attribute__((aligned(16))) uint16_t tab[1u << kHufOneMaxLg];
-    __shared__ uint32_t cand[kHufOneT * kHufOneMaxLg];   // exit offset | symbols << 8, per chunk and entry
-    __shared__ uint32_t ent[kHufOneT];                   // true entry | output base << 4
-    __shared__ uint32_t verdict;
-    __shared__ __attribute__((aligned(16))) uint8_t rings[kRS * 1024];   // the serial walk's ring
-    const uint32_t j = blockIdx.x, t = threadIdx.x;
+    auto &sst = H.sst;
+    auto &obuf = H.obuf;
+    auto &tab = H.tab;
+    auto &cand = H.cand;
+    auto &ent = H.ent;
+    auto &verdict = H.verdict;
+    auto &rings = H.rings;
     const HufJob J = reinterpret_cast<const HufJob *>(jobs)[j];
     if (J.len == 0) {
         if (t == 0)
@@ -2036,6 +2046,16 @@ __global__ __launch_bounds__(kHufOneT) void zstd_huf_one_kernel(const uint8_t *_
             lit[J.dst + J.cnt - 1] = (uint8_t)(xr >> 8);
     }
     hbad[j] = bad ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kHufOneT) void zstd_huf_one_kernel(const uint8_t *__restrict__ jobs,
+                                                                const uint8_t *__restrict__ comp,
+                                                                const uint8_t *__restrict__ slots,
+                                                                uint8_t *__restrict__ lit,
+                                                                uint8_t *__restrict__ hbad)
+{
+    __shared__ HufOneLds H;
+    huf_one_body(H, blockIdx.x, threadIdx.x, jobs, comp, slots, lit, hbad);
 }
 
 // ---- sequences: one lane per seek-table entry ------------------------------------------
@@ -2250,19 +2270,31 @@ constexpr uint32_t kSeqStage = 131072 + 64;   // > a block's largest sequences s
 __device__ unsigned long long g_sdiag[8];
 #endif
 
+// its LDS (a struct: the one-frame decode kernel below shares it with the
+// Huffman job's, as a union)
+template <uint32_t LANES, uint32_t CELLS, bool ONE>
+struct SeqLds {
+    uint32_t codes[89];
+    __attribute__((aligned(16))) uint16_t ftab[CELLS && !ONE ? LANES * CELLS : 8];
+    __attribute__((aligned(16))) uint8_t sstage[ONE ? kSeqStage + 32 : 16];
+    uint64_t xtab[ONE ? kSeqOneCells : 1];                 // ONE: the expanded cells (below)
+    __attribute__((aligned(16))) uint32_t srec[ONE ? 64 * 8 : 4];   // ONE: a batch's records
+};
+
+// the replay of workgroup bid (one wave: threads 0-63)
 template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false>
-__global__ __launch_bounds__(64) void zstd_seq_kernel(
-    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
-    uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
+__device__ __forceinline__ void seq_body(
+    SeqLds<LANES, CELLS, ONE> &SH, uint32_t bid, const FrameDesc *__restrict__ desc, uint32_t n,
+    const uint8_t *__restrict__ comp, uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
     const uint8_t *__restrict__ slots, uint32_t *__restrict__ stop,
     const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
     int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at, uint32_t f0)
 {
-    __shared__ uint32_t codes[89];
-    __shared__ __attribute__((aligned(16))) uint16_t ftab[CELLS && !ONE ? LANES * CELLS : 8];
-    __shared__ __attribute__((aligned(16))) uint8_t sstage[ONE ? kSeqStage + 32 : 16];
-    __shared__ uint64_t xtab[ONE ? kSeqOneCells : 1];   // ONE: the expanded cells (below)
-    __shared__ __attribute__((aligned(16))) uint32_t srec[ONE ? 64 * 8 : 4];   // ONE: a batch's records
+    auto &codes = SH.codes;
+    auto &ftab = SH.ftab;
+    auto &sstage = SH.sstage;
+    auto &xtab = SH.xtab;
+    auto &srec = SH.srec;
 #ifdef ZSK_TUNING
     const uint64_t tk0 = __builtin_readcyclecounter(), rt0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tloop = 0, nseqs = 0;
@@ -2271,7 +2303,7 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
     __syncthreads();
     const uint32_t lane = threadIdx.x;
-    const uint32_t f = ONE ? f0 + blockIdx.x : f0 + blockIdx.x * LANES + lane;   // frames [f0, n)
+    const uint32_t f = ONE ? f0 + bid : f0 + bid * LANES + lane;   // frames [f0, n)
     const bool act = (ONE || lane < LANES) && f < n;
     FrameDesc d = {0, 0, 0, 0};
     if (act)
@@ -2485,10 +2517,14 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                 // vector phase's, from H and the cells), stored
                                 // ahead of the next sequence's reads: after them,
                                 // the wait for them would wait for it too
-                                *la<uint64_t>(rec + 32 * q) = H;
-                                *la<uint64_t>(rec + 32 * q + 8) = cl;
-                                *la<uint64_t>(rec + 32 * q + 16) = cm;
-                                *la<uint64_t>(rec + 32 * q + 24) = co;
+                                // (two paired stores in asm: the compiler's own
+                                // choice varied with the kernel it sat in, up to
+                                // four stores and four address moves)
+                                asm volatile("ds_write2_b64 %0, %1, %2 offset1:1\n\t"
+                                             "ds_write2_b64 %0, %3, %4 offset0:2 offset1:3"
+                                             :
+                                             : "v"(rec + 32 * q), "v"(H), "v"(cl), "v"(cm), "v"(co)
+                                             : "memory");
                                 const u32x4 W2 = win(cur2);
                                 const uint64_t cl2 = *la<uint64_t>(al), cm2 = *la<uint64_t>(am), co2 = *la<uint64_t>(ao);
                                 cl = cl2;
@@ -2830,6 +2866,47 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
     stop[f] = kstop;
     if (fail_at)
         fail_at[f] = st == ST_OK ? 0 : fa;
+}
+
+template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false>
+__global__ __launch_bounds__(64) void zstd_seq_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
+    uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
+    const uint8_t *__restrict__ slots, uint32_t *__restrict__ stop,
+    const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
+    int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at, uint32_t f0)
+{
+    __shared__ SeqLds<LANES, CELLS, ONE> SH;
+    seq_body<LANES, CELLS, GM, ONE>(SH, blockIdx.x, desc, n, comp, ops, blk_base, slots, stop, rec_base, items,
+                                    nitems, status, ck, fail_at, f0);
+}
+
+// The one-frame route's replay and Huffman streams in one launch: workgroups
+// [0, m) replay frame f0 + b on their first wave (the others leave), the rest
+// decode Huffman job b - m with all kHufOneT threads -- no second stream, so
+// no event between the frame kernel and them or between them and the
+// literal fix-up (~8-11 us each on the request's timeline).  LDS: the union.
+__global__ __launch_bounds__(kHufOneT) void zstd_one_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
+    uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
+    const uint8_t *__restrict__ slots, uint32_t *__restrict__ stop,
+    const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
+    int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at, uint32_t f0,
+    uint32_t m, const uint8_t *__restrict__ jobs, uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
+{
+    __shared__ union {
+        SeqLds<1, 0, true> s;
+        HufOneLds h;
+    } U;
+    const uint32_t b = blockIdx.x;
+    if (b < m) {
+        if (threadIdx.x >= 64)
+            return;
+        seq_body<1, 0, 0, true>(U.s, b, desc, n, comp, ops, blk_base, slots, stop, rec_base, items, nitems, status,
+                                ck, fail_at, f0);
+    } else {
+        huf_one_body(U.h, b - m, threadIdx.x, jobs, comp, slots, lit, hbad);
+    }
 }
 
 // After the Huffman and sequence kernels (which run side by side): a frame
@@ -3189,7 +3266,14 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
     }();
     const bool one = !one_off && nframes <= kOneMaxFrames;
     // (the one-frame route's sequence replay on the caller's stream, right
-    // behind the frame kernel: a cross-stream hand-off cost ~30 us each way)
+    // behind the frame kernel: a cross-stream hand-off cost ~30 us each way;
+    // with its Huffman jobs in the same launch, zstd_one_kernel -- env
+    // ZSEEK_ONE_FUSE=0: the Huffman kernel on the side stream, as before)
+    static const bool fuse_off = [] {
+        const char *v = getenv("ZSEEK_ONE_FUSE");
+        return v && !strcmp(v, "0");
+    }();
+    const bool fuse = one && !fuse_off;
     hipStream_t const hs = serial ? stream : s->side, qs = serial || one ? stream : s->sq;
 #ifdef ZSK_TUNING
     static const int diag = getenv("ZSEEK_ZSTD_HUF_DIAG") ? atoi(getenv("ZSEEK_ZSTD_HUF_DIAG")) : 0;
@@ -3240,11 +3324,33 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         }
 #endif
         kernel_span_end(SPAN_ZFRAME, tf, stream);
+        const uint32_t nj = (uint32_t)(4 * (b1 - b0));
+        if (fuse) {
+            hipEvent_t tq = kernel_span_begin(stream);
+            hipLaunchKernelGGL(zstd_one_kernel, dim3(m + nj), dim3(kHufOneT), 0, stream, d_desc, f1, d_comp, s->ops,
+                               s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems, d_status, s->ck,
+                               d_fail_at, f0, m, s->hjobs + 4 * b0 * sizeof(HufJob), s->lit, s->hbad + 4 * b0);
+            kernel_span_end(SPAN_ZSEQ, tq, stream);
+#ifdef ZSK_TUNING
+            static const bool timers = getenv("ZSEEK_SEQ_TIMERS") != nullptr;
+            static int calls = 0;
+            if (timers && ++calls % 100 == 0) {
+                unsigned long long z[8] = {0};
+                (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_sdiag), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+                (void)hipStreamSynchronize(stream);
+                const double fr = z[4] ? (double)z[4] : 1.0, sq = z[2] ? (double)z[2] : 1.0;
+                fprintf(stderr,
+                        "one-frame sequences: kernel %.0f cycles (%.1f us, %.0f MHz) per frame, loop %.0f cycles "
+                        "(%.0f per sequence, %.0f sequences per frame)\n",
+                        z[0] / fr, z[3] / fr / 100.0, z[3] ? z[0] * 100.0 / z[3] : 0.0, z[1] / fr, z[1] / sq, sq / fr);
+            }
+#endif
+            continue;
+        }
         if (hipEventRecord(s->ev_f[c], stream) != hipSuccess || hipStreamWaitEvent(qs, s->ev_f[c], 0) != hipSuccess)
             return drain();
         // the Huffman streams decode beside the sequence replay (neither reads
         // the other's output); zstd_lit_fix_kernel joins them
-        const uint32_t nj = (uint32_t)(4 * (b1 - b0));
         if (nj) {
             if (hipStreamWaitEvent(hs, s->ev_f[c], 0) != hipSuccess)
                 return drain();
@@ -3348,8 +3454,8 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         if (m == 0)
             continue;
         const uint64_t b0 = s->total[4 + c], b1 = s->total[5 + c];
-        if (hipStreamWaitEvent(stream, s->ev_s[c], 0) != hipSuccess ||
-            (b1 > b0 && hipStreamWaitEvent(stream, s->ev_h[c], 0) != hipSuccess))
+        if (!fuse && (hipStreamWaitEvent(stream, s->ev_s[c], 0) != hipSuccess ||
+                      (b1 > b0 && hipStreamWaitEvent(stream, s->ev_h[c], 0) != hipSuccess)))
             return drain();
         if (b1 > b0)
             hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, f1, s->ops,
