@@ -246,7 +246,8 @@ struct ZstdScratch {
     uint8_t *slots = nullptr;      // per-block decoding tables (kZSlot bytes each)
     uint8_t *hbad = nullptr;       // per Huffman stream: 1 = corrupt
     // [0] item total, [1] output extent, [2] blocks, [3] largest frame (d_size), [4 + k] blk_base
-    // at chunk boundary k (zstd_decode.hip: the decode runs in chunks)
+    // at chunk boundary k (zstd_decode.hip: the decode runs in chunks); past
+    // those, zstd_one_kernel's finished-workgroup counter (zero between launches)
     uint64_t *d_total = nullptr;
     uint64_t *total = nullptr;     // pinned host copy of d_total
     uint64_t *h_plan = nullptr;    // pinned: a host plan's rec_base then blk_base (zstd_decode_frames_host)
@@ -276,10 +277,11 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 // block's start (its end for the end-of-frame checks); the execute still
 // writes the bytes before it.
 // stop_last: the batch's last frame executed only up to that many bytes (a
-// no-cache read's end; its checksum then not checked)
+// no-cache read's end; its checksum then not checked); cks false: no frame
+// carries a content checksum (a host plan saw them all), no check launch
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
-                       uint32_t *d_fail_at = nullptr, uint32_t stop_last = 0xFFFFFFFFu);
+                       uint32_t *d_fail_at = nullptr, uint32_t stop_last = 0xFFFFFFFFu, bool cks = true);
 // plan + synchronize + reserve + decode
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,

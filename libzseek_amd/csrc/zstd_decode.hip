@@ -2881,49 +2881,68 @@ __global__ __launch_bounds__(64) void zstd_seq_kernel(
                                     nitems, status, ck, fail_at, f0);
 }
 
+__device__ __forceinline__ void lit_fix(uint32_t f, const uint8_t *__restrict__ ops,
+                                        const uint64_t *__restrict__ blk_base, const uint8_t *__restrict__ hbad,
+                                        const uint32_t *__restrict__ stop, int32_t *__restrict__ status,
+                                        uint32_t *__restrict__ nitems, uint32_t *__restrict__ fail_at);
+
 // The one-frame route's replay and Huffman streams in one launch: workgroups
 // [0, m) replay frame f0 + b on their first wave (the others leave), the rest
 // decode Huffman job b - m with all kHufOneT threads -- no second stream, so
 // no event between the frame kernel and them or between them and the
 // literal fix-up (~8-11 us each on the request's timeline).  LDS: the union.
+// The workgroup finishing last (a counter in `done`, zero between launches:
+// the last one resets it) runs the literal fix-up (zstd_lit_fix_kernel's
+// work) -- every replay and Huffman job is done by then; nothing waits.
 __global__ __launch_bounds__(kHufOneT) void zstd_one_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
     const uint8_t *__restrict__ slots, uint32_t *__restrict__ stop,
     const uint64_t *__restrict__ rec_base, uint64_t *__restrict__ items, uint32_t *__restrict__ nitems,
     int32_t *__restrict__ status, uint64_t *__restrict__ ck, uint32_t *__restrict__ fail_at, uint32_t f0,
-    uint32_t m, const uint8_t *__restrict__ jobs, uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad)
+    uint32_t m, const uint8_t *__restrict__ jobs, uint8_t *__restrict__ lit, uint8_t *__restrict__ hbad,
+    uint32_t *__restrict__ done)
 {
     __shared__ union {
         SeqLds<1, 0, true> s;
         HufOneLds h;
     } U;
-    const uint32_t b = blockIdx.x;
+    __shared__ uint32_t last;
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
     if (b < m) {
-        if (threadIdx.x >= 64)
+        if (t >= 64)
             return;
         seq_body<1, 0, 0, true>(U.s, b, desc, n, comp, ops, blk_base, slots, stop, rec_base, items, nitems, status,
                                 ck, fail_at, f0);
     } else {
-        huf_one_body(U.h, b - m, threadIdx.x, jobs, comp, slots, lit, hbad);
+        huf_one_body(U.h, b - m, t, jobs, comp, slots, lit, hbad);
     }
+    // (thread 0 wrote what the fix-up reads: status, items, stop, hbad)
+    __syncthreads();
+    if (t == 0) {
+        __threadfence();
+        last = atomicAdd(done, 1u) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last)
+        return;
+    __threadfence();
+    if (t < 64)
+        for (uint32_t f = f0 + t; f < n; f += 64)
+            lit_fix(f, ops, blk_base, hbad, stop, status, nitems, fail_at);
+    if (t == 0)
+        *done = 0;
 }
 
 // After the Huffman and sequence kernels (which run side by side): a frame
 // whose replay passed a literals op of a block with a corrupt Huffman stream
 // fails there, as libzstd does — that block's literals are decoded before its
 // sequences — with the items and output offset the replay had at that op.
-__global__ __launch_bounds__(256) void zstd_lit_fix_kernel(uint32_t n, const uint8_t *__restrict__ ops,
-                                                           const uint64_t *__restrict__ blk_base,
-                                                           const uint8_t *__restrict__ hbad,
-                                                           const uint32_t *__restrict__ stop,
-                                                           int32_t *__restrict__ status,
-                                                           uint32_t *__restrict__ nitems,
-                                                           uint32_t *__restrict__ fail_at, uint32_t f0)
+__device__ __forceinline__ void lit_fix(uint32_t f, const uint8_t *__restrict__ ops,
+                                        const uint64_t *__restrict__ blk_base, const uint8_t *__restrict__ hbad,
+                                        const uint32_t *__restrict__ stop, int32_t *__restrict__ status,
+                                        uint32_t *__restrict__ nitems, uint32_t *__restrict__ fail_at)
 {
-    const uint32_t f = f0 + blockIdx.x * 256 + threadIdx.x;   // frames [f0, n)
-    if (f >= n)
-        return;
     const ZOp *op = reinterpret_cast<const ZOp *>(ops) + op_base(blk_base, f);
     const uint32_t ks = stop[f];
     for (uint32_t k = 0; k < ks; k++) {
@@ -2936,6 +2955,19 @@ __global__ __launch_bounds__(256) void zstd_lit_fix_kernel(uint32_t n, const uin
             return;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void zstd_lit_fix_kernel(uint32_t n, const uint8_t *__restrict__ ops,
+                                                           const uint64_t *__restrict__ blk_base,
+                                                           const uint8_t *__restrict__ hbad,
+                                                           const uint32_t *__restrict__ stop,
+                                                           int32_t *__restrict__ status,
+                                                           uint32_t *__restrict__ nitems,
+                                                           uint32_t *__restrict__ fail_at, uint32_t f0)
+{
+    const uint32_t f = f0 + blockIdx.x * 256 + threadIdx.x;   // frames [f0, n)
+    if (f < n)
+        lit_fix(f, ops, blk_base, hbad, stop, status, nitems, fail_at);
 }
 
 // XXH64 of [o0, cap) of a frame's output for frames flagged by the frame
@@ -3157,7 +3189,8 @@ int zstd_scratch_reserve(ZstdScratch *s, uint32_t frames, uint64_t out_bytes, ui
             hipMalloc((void **)&s->nitems, sizeof(uint32_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->ck, sizeof(uint64_t) * cap) != hipSuccess ||
             hipMalloc((void **)&s->stop, sizeof(uint32_t) * cap) != hipSuccess ||
-            hipMalloc((void **)&s->d_total, (5 + ZstdScratch::kChunks) * sizeof(uint64_t)) != hipSuccess ||
+            hipMalloc((void **)&s->d_total, (6 + ZstdScratch::kChunks) * sizeof(uint64_t)) != hipSuccess ||
+            hipMemset(s->d_total, 0, (6 + ZstdScratch::kChunks) * sizeof(uint64_t)) != hipSuccess ||
             hipHostMalloc((void **)&s->total, (5 + ZstdScratch::kChunks) * sizeof(uint64_t), hipHostMallocDefault) !=
                 hipSuccess)
             return -1;
@@ -3249,7 +3282,7 @@ int launch_zstd_plan(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
 // frame kernel is.  s must hold the last plan of these frames.
 int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
-                       uint32_t *d_fail_at, uint32_t stop_last)
+                       uint32_t *d_fail_at, uint32_t stop_last, bool cks)
 {
     if (nframes == 0)
         return 0;
@@ -3329,7 +3362,8 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
             hipEvent_t tq = kernel_span_begin(stream);
             hipLaunchKernelGGL(zstd_one_kernel, dim3(m + nj), dim3(kHufOneT), 0, stream, d_desc, f1, d_comp, s->ops,
                                s->blk_base, s->slots, s->stop, s->rec_base, s->items, s->nitems, d_status, s->ck,
-                               d_fail_at, f0, m, s->hjobs + 4 * b0 * sizeof(HufJob), s->lit, s->hbad + 4 * b0);
+                               d_fail_at, f0, m, s->hjobs + 4 * b0 * sizeof(HufJob), s->lit, s->hbad + 4 * b0,
+                               reinterpret_cast<uint32_t *>(s->d_total + 5 + ZstdScratch::kChunks));
             kernel_span_end(SPAN_ZSEQ, tq, stream);
 #ifdef ZSK_TUNING
             static const bool timers = getenv("ZSEEK_SEQ_TIMERS") != nullptr;
@@ -3457,7 +3491,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         if (!fuse && (hipStreamWaitEvent(stream, s->ev_s[c], 0) != hipSuccess ||
                       (b1 > b0 && hipStreamWaitEvent(stream, s->ev_h[c], 0) != hipSuccess)))
             return drain();
-        if (b1 > b0)
+        if (b1 > b0 && !fuse)   // (fused: the last workgroup's)
             hipLaunchKernelGGL(zstd_lit_fix_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, f1, s->ops,
                                s->blk_base, s->hbad, s->stop, d_status, s->nitems, d_fail_at, f0);
         hipEvent_t tx = kernel_span_begin(stream);
@@ -3467,8 +3501,9 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                                 stop) != 0)
             rc = -1;
         kernel_span_end(SPAN_ZEXEC, tx, stream);
-        hipLaunchKernelGGL(zstd_check_kernel, dim3((m + 3) / 4), dim3(256), 0, stream, d_desc + f0, m, d_out,
-                           s->ck + f0, d_status + f0, d_fail_at ? d_fail_at + f0 : nullptr, stop);
+        if (cks)   // (a host plan that met no content checksum: nothing to check)
+            hipLaunchKernelGGL(zstd_check_kernel, dim3((m + 3) / 4), dim3(256), 0, stream, d_desc + f0, m, d_out,
+                               s->ck + f0, d_status + f0, d_fail_at ? d_fail_at + f0 : nullptr, stop);
     }
     stage_mark(3, stream);
     stage_mark(4, stream);
@@ -3502,7 +3537,7 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 // block + 2 per sequence + the pairs' padding, rounded up to 4) and blocks,
 // from the frame headers, block headers, literals section headers and
 // sequence counts -- the same walk, the same arithmetic.
-static void zstd_plan_frame_host(const uint8_t *c, uint32_t clen, uint32_t *bound, uint32_t *bblk)
+static void zstd_plan_frame_host(const uint8_t *c, uint32_t clen, uint32_t *bound, uint32_t *bblk, bool *cks)
 {
     auto B = [&](uint32_t p) -> uint32_t { return p < clen ? (uint32_t)c[p] : 0u; };
     uint64_t items = 8;
@@ -3553,8 +3588,10 @@ static void zstd_plan_frame_host(const uint8_t *c, uint32_t clen, uint32_t *boun
         }
         if (ip > clen)
             break;
-        if ((fhd >> 2) & 1)
+        if ((fhd >> 2) & 1) {
             ip += 4;
+            *cks = true;   // a content checksum: the check kernel runs
+        }
     }
     *bound = (uint32_t)((items + 3) & ~3ull);
     *bblk = blocks;
@@ -3586,10 +3623,11 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
         s->h_plan_cap = 2 * (kOneMaxFrames + 1);
     }
     uint64_t *const rb = s->h_plan, *const bb = s->h_plan + nframes + 1;
+    bool cks = false;
     for (uint32_t f = 0; f < nframes; f++) {
         const FrameDesc &d = h_desc[f];
         uint32_t bound = 0, bblk = 0;
-        zstd_plan_frame_host(h_comp + d.c_off, d.c_size, &bound, &bblk);
+        zstd_plan_frame_host(h_comp + d.c_off, d.c_size, &bound, &bblk, &cks);
         rb[f] = items;
         bb[f] = blocks;
         items += bound;
@@ -3617,7 +3655,8 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
     uint64_t *const keep_rb = s->rec_base, *const keep_bb = s->blk_base;
     s->rec_base = s->d_plan;
     s->blk_base = s->d_plan + nframes + 1;
-    const int rc = launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last);
+    const int rc =
+        launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last, cks);
     s->rec_base = keep_rb;
     s->blk_base = keep_bb;
     return rc;
