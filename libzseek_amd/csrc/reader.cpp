@@ -462,7 +462,10 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // the descriptors ride behind the compressed span (past its 256-byte
     // read slack) in the same pinned buffer and the same upload
     const uint64_t doff = (csz + 256 + 255) & ~255ull;
-    if (!s.reserve(doff + n * sizeof(FrameDesc), dsz, br.h_len, n, ck, J.err)) {
+    // (zstd, a request's few frames: the host plan rides behind them too)
+    const bool zplan = r->type == ZSEEK_ZSTD && n <= kOneMaxFrames;
+    const uint64_t poff = doff + n * sizeof(FrameDesc), up = poff + (zplan ? 16 * (n + 1) : 0);
+    if (!s.reserve(up, dsz, br.h_len, n, ck, J.err)) {
         J.io_failed = true;
         return false;
     }
@@ -489,8 +492,11 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     uint32_t *d_fail = reinterpret_cast<uint32_t *>(s.d_status + n);
     s.h_from = br.h_from;
     s.h_len = br.h_len;
+    ZstdHostPlan zp{};
+    if (zplan)
+        zstd_host_plan(h_desc, s.h_comp, (uint32_t)n, reinterpret_cast<uint64_t *>(s.h_comp + poff), &zp);
     hipError_t e = hipSuccess;
-    e = hipMemcpyAsync(s.d_comp, s.h_comp, doff + n * sizeof(FrameDesc), hipMemcpyHostToDevice, s.stream);
+    e = hipMemcpyAsync(s.d_comp, s.h_comp, up, hipMemcpyHostToDevice, s.stream);
     // (the LZ4 two-phase decoder's plan kernel initializes both itself, the
     // zstd sequence kernel writes both for every frame)
     const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
@@ -502,8 +508,9 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // (zstd: a request's few frames are planned on the host from the pinned
     // span -- no plan launch, no synchronization between plan and decode)
     if (e == hipSuccess && r->type == ZSEEK_ZSTD &&
-        (n <= kOneMaxFrames ? zstd_decode_frames_host(h_desc, s.h_comp, d_desc, (uint32_t)n, s.d_comp, s.d_out,
-                                                      s.d_status, &s.zs, s.stream, d_fail, stop_last)
+        (zplan ? zstd_decode_frames_planned(zp, reinterpret_cast<const uint64_t *>(s.d_comp + poff), d_desc,
+                                            (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream, d_fail,
+                                            stop_last)
                             : zstd_decode_frames(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs,
                                                  s.stream, d_fail)) != 0)
         e = hipErrorLaunchFailure;

@@ -295,6 +295,19 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
                             uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
                             ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at,
                             uint32_t stop_last = 0xFFFFFFFFu);
+// ... in two steps, for a caller that uploads the plan with its own bytes:
+// the plan (2 (nframes + 1) u64: item slot offsets, then block slot offsets)
+// into h_plan before the upload, then the decode with the plan's device copy
+struct ZstdHostPlan {
+    uint64_t items, blocks, extent, dmax;
+    bool cks;   // some frame carries a content checksum
+};
+void zstd_host_plan(const FrameDesc *h_desc, const uint8_t *h_comp, uint32_t nframes, uint64_t *h_plan,
+                    ZstdHostPlan *P);
+int zstd_decode_frames_planned(const ZstdHostPlan &P, const uint64_t *d_plan, const FrameDesc *d_desc,
+                               uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                               ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at,
+                               uint32_t stop_last = 0xFFFFFFFFu);
 
 // Parse phase, streaming lane-per-frame (lz4_scan.hip), for the frames
 // under max_csize compressed bytes (the short frames of config 3).

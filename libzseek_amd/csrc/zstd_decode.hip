@@ -3597,32 +3597,11 @@ static void zstd_plan_frame_host(const uint8_t *c, uint32_t clen, uint32_t *boun
     *bblk = blocks;
 }
 
-int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, const FrameDesc *d_desc,
-                            uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
-                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at, uint32_t stop_last)
+void zstd_host_plan(const FrameDesc *h_desc, const uint8_t *h_comp, uint32_t nframes, uint64_t *h_plan,
+                    ZstdHostPlan *P)
 {
-    if (nframes == 0)
-        return 0;
-    if (nframes > kOneMaxFrames || zstd_chunks(nframes) != 1)
-        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
-    (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
     uint64_t items = 0, blocks = 0, extent = 0, dmax = 0;
-    if (zstd_scratch_reserve(s, nframes, 0, 0, 0, stream) != 0)
-        return -1;
-    if (2ull * (nframes + 1) > s->h_plan_cap) {
-        if (s->h_plan)
-            (void)hipHostFree(s->h_plan);
-        if (s->d_plan)
-            (void)hipFree(s->d_plan);
-        s->h_plan = s->d_plan = nullptr;
-        s->h_plan_cap = 0;
-        if (hipHostMalloc((void **)&s->h_plan, 2 * (kOneMaxFrames + 1) * sizeof(uint64_t), hipHostMallocDefault) !=
-                hipSuccess ||
-            hipMalloc((void **)&s->d_plan, 2 * (kOneMaxFrames + 1) * sizeof(uint64_t)) != hipSuccess)
-            return -1;
-        s->h_plan_cap = 2 * (kOneMaxFrames + 1);
-    }
-    uint64_t *const rb = s->h_plan, *const bb = s->h_plan + nframes + 1;
+    uint64_t *const rb = h_plan, *const bb = h_plan + nframes + 1;
     bool cks = false;
     for (uint32_t f = 0; f < nframes; f++) {
         const FrameDesc &d = h_desc[f];
@@ -3637,29 +3616,71 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
     }
     rb[nframes] = items;
     bb[nframes] = blocks;
+    *P = ZstdHostPlan{items, blocks, extent, dmax, cks};
+}
+
+int zstd_decode_frames_planned(const ZstdHostPlan &P, const uint64_t *d_plan, const FrameDesc *d_desc,
+                               uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                               ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at, uint32_t stop_last)
+{
+    if (nframes == 0)
+        return 0;
+    if (nframes > kOneMaxFrames || zstd_chunks(nframes) != 1)
+        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+    (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
     stage_mark(0, stream);
-    if (zstd_scratch_reserve(s, nframes, extent, items, blocks, stream) != 0)
+    if (zstd_scratch_reserve(s, nframes, P.extent, P.items, P.blocks, stream) != 0)
         return -1;
-    s->total[0] = items;
-    s->total[1] = extent;
-    s->total[2] = blocks;
-    s->total[3] = dmax;
+    s->total[0] = P.items;
+    s->total[1] = P.extent;
+    s->total[2] = P.blocks;
+    s->total[3] = P.dmax;
     s->total[4] = 0;   // one chunk: blocks [0, blocks)
-    s->total[5] = blocks;
-    // both offset arrays in one upload; this launch's kernels take them from
-    // the upload's device copy (the scratch's own arrays are left alone)
-    if (hipMemcpyAsync(s->d_plan, rb, 2 * (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) !=
-        hipSuccess)
-        return -1;
+    s->total[5] = P.blocks;
     stage_mark(1, stream);
+    // this launch's kernels take both offset arrays from the plan's upload
+    // (the scratch's own arrays are left alone)
     uint64_t *const keep_rb = s->rec_base, *const keep_bb = s->blk_base;
-    s->rec_base = s->d_plan;
-    s->blk_base = s->d_plan + nframes + 1;
+    s->rec_base = const_cast<uint64_t *>(d_plan);
+    s->blk_base = const_cast<uint64_t *>(d_plan) + nframes + 1;
     const int rc =
-        launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last, cks);
+        launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last, P.cks);
     s->rec_base = keep_rb;
     s->blk_base = keep_bb;
     return rc;
+}
+
+int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, const FrameDesc *d_desc,
+                            uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out, int32_t *d_status,
+                            ZstdScratch *s, hipStream_t stream, uint32_t *d_fail_at, uint32_t stop_last)
+{
+    if (nframes == 0)
+        return 0;
+    if (nframes > kOneMaxFrames || zstd_chunks(nframes) != 1)
+        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+    if (2ull * (nframes + 1) > s->h_plan_cap) {
+        if (s->h_plan)
+            (void)hipHostFree(s->h_plan);
+        if (s->d_plan)
+            (void)hipFree(s->d_plan);
+        s->h_plan = s->d_plan = nullptr;
+        s->h_plan_cap = 0;
+        if (hipHostMalloc((void **)&s->h_plan, 2 * (kOneMaxFrames + 1) * sizeof(uint64_t), hipHostMallocDefault) !=
+                hipSuccess ||
+            hipMalloc((void **)&s->d_plan, 2 * (kOneMaxFrames + 1) * sizeof(uint64_t)) != hipSuccess)
+            return -1;
+        s->h_plan_cap = 2 * (kOneMaxFrames + 1);
+    }
+    // (a previous call's upload from h_plan must be done before it is rewritten)
+    if (hipStreamSynchronize(stream) != hipSuccess)
+        return -1;
+    ZstdHostPlan P;
+    zstd_host_plan(h_desc, h_comp, nframes, s->h_plan, &P);
+    if (hipMemcpyAsync(s->d_plan, s->h_plan, 2 * (nframes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, stream) !=
+        hipSuccess)
+        return -1;
+    return zstd_decode_frames_planned(P, s->d_plan, d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at,
+                                      stop_last);
 }
 
 }   // namespace zsk
