@@ -118,6 +118,9 @@ struct Slot {
     size_t h_ck_cap = 0;
     uint8_t *h_out = nullptr;      // pinned bounce of decoded bytes (host destinations)
     size_t h_out_cap = 0;
+    // the device mappings of h_comp, h_status, h_out (hipHostGetDevicePointer,
+    // taken when they are allocated): small uploads and downloads as kernels
+    void *h_comp_dev = nullptr, *h_status_dev = nullptr, *h_out_dev = nullptr;
     uint8_t *d_comp = nullptr;
     size_t d_comp_cap = 0;
     uint8_t *d_out = nullptr;

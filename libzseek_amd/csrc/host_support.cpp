@@ -493,6 +493,7 @@ bool Slot::reserve(size_t comp, size_t out, size_t host_out, size_t nframes, boo
         set_error(errbuf, "allocate GPU decode buffers failed");
         return false;
     }
+    const void *const c0 = h_comp, *const s0 = h_status, *const o0 = h_out;
     if (!grow_host(&h_comp, &h_comp_cap, comp) ||
         !grow_host(&h_status, &h_status_cap, 2 * nframes) ||
         (ck && !grow_host(&h_ck, &h_ck_cap, nframes)) ||
@@ -500,6 +501,18 @@ bool Slot::reserve(size_t comp, size_t out, size_t host_out, size_t nframes, boo
         set_error(errbuf, "allocate pinned staging failed");
         return false;
     }
+    // (re)allocated: their device mappings (none: the copies go by DMA)
+    auto map = [](void *h, void **dev) {
+        *dev = nullptr;
+        if (h && hipHostGetDevicePointer(dev, h, 0) != hipSuccess)
+            *dev = nullptr;
+    };
+    if (h_comp != c0 || (h_comp && !h_comp_dev))
+        map(h_comp, &h_comp_dev);
+    if (h_status != s0 || (h_status && !h_status_dev))
+        map(h_status, &h_status_dev);
+    if (h_out != o0 || (h_out && !h_out_dev))
+        map(h_out, &h_out_dev);
     return true;
 }
 
@@ -533,6 +546,7 @@ void Slot::destroy()
     h_comp = h_out = nullptr;
     h_status = nullptr;
     h_ck = nullptr;
+    h_comp_dev = h_status_dev = h_out_dev = nullptr;
     d_comp = d_out = nullptr;
     d_status = nullptr;
     d_ck = nullptr;

@@ -496,7 +496,14 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     if (zplan)
         zstd_host_plan(h_desc, s.h_comp, (uint32_t)n, reinterpret_cast<uint64_t *>(s.h_comp + poff), &zp);
     hipError_t e = hipSuccess;
-    e = hipMemcpyAsync(s.d_comp, s.h_comp, up, hipMemcpyHostToDevice, s.stream);
+    // (a small upload as a kernel on the stream: no DMA hand-off before the
+    // decode's first kernel, host_io.hip; env ZSEEK_HOST_DMA=1: always DMA,
+    // the download too)
+    static const bool host_dma = getenv("ZSEEK_HOST_DMA") != nullptr;
+    if (host_dma)
+        e = hipMemcpyAsync(s.d_comp, s.h_comp, up, hipMemcpyHostToDevice, s.stream);
+    else if (upload_small(s.d_comp, s.h_comp, s.h_comp_dev, up, s.stream) != 0)
+        e = hipErrorLaunchFailure;
     // (the LZ4 two-phase decoder's plan kernel initializes both itself, the
     // zstd sequence kernel writes both for every frame)
     const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
@@ -535,18 +542,25 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
             launch_frame_checksums(d_desc, (uint32_t)n, s.d_out, s.d_ck, s.d_status, s.stream) != 0)
             e = hipErrorLaunchFailure;
     }
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(s.h_status, s.d_status, 2 * n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
     // decoded bytes out: straight into a device destination (a peer copy from
     // another lane's device), or into the slot's pinned bounce once the host
-    // copies of its previous batch are done
+    // copies of its previous batch are done; the status words and the bounce
+    // part in one small-download kernel (host_io.hip) when they are small
     if (e == hipSuccess && br.route == COPY_DEVICE)
         e = hipMemcpyAsync(J.buf + br.dst_off, s.d_out + br.src_off, br.len, hipMemcpyDeviceToDevice, s.stream);
     else if (e == hipSuccess && br.route == COPY_PEER)
         e = hipMemcpyPeerAsync(J.buf + br.dst_off, J.dst_dev, s.d_out + br.src_off, g.device, br.len, s.stream);
-    if (e == hipSuccess && s.h_len) {
+    if (e == hipSuccess && s.h_len)
         pool_wait(&s.copies);
-        e = hipMemcpyAsync(s.h_out, s.d_out + s.h_from, s.h_len, hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess && host_dma) {
+        e = hipMemcpyAsync(s.h_status, s.d_status, 2 * n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
+        if (e == hipSuccess && s.h_len)
+            e = hipMemcpyAsync(s.h_out, s.d_out + s.h_from, s.h_len, hipMemcpyDeviceToHost, s.stream);
+    } else if (e == hipSuccess &&
+               download_small(reinterpret_cast<uint32_t *>(s.h_status), s.h_status_dev,
+                              reinterpret_cast<const uint32_t *>(s.d_status), (uint32_t)(2 * n), s.h_out, s.h_out_dev,
+                              s.d_out + s.h_from, s.h_len, s.stream) != 0) {
+        e = hipErrorLaunchFailure;
     }
     if (e == hipSuccess)
         e = hipEventRecord(s.done, s.stream);
