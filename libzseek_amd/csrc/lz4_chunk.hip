@@ -121,10 +121,10 @@ __device__ __forceinline__ uint32_t rd1(const Src &S, Win &W, uint32_t x)
 // Advances p to the next token (the block end after a literals-only last
 // sequence or when the bytes cannot be a sequence) and adds the sequence's
 // output bytes and items.
-__device__ __forceinline__ void skel(const Src &S, Win &W, uint32_t &p, uint32_t iend,
-                                     uint32_t &out, uint32_t &nitem)
+// (t4: the four bytes at p, read by the caller)
+__device__ __forceinline__ void skel_at(const Src &S, Win &W, uint32_t &p, uint32_t iend, uint32_t &out,
+                                        uint32_t &nitem, uint32_t t4)
 {
-    const uint32_t t4 = rd4(S, W, p);
     const uint32_t tok = t4 & 0xFF;
     uint32_t lit = tok >> 4, pp = p + 1;
     if (lit == 15) {
@@ -158,6 +158,12 @@ __device__ __forceinline__ void skel(const Src &S, Win &W, uint32_t &p, uint32_t
     out += lit + ml;
     nitem += (lit > 255 || ml > 258) ? 2 : 1;
     p = endr || q >= iend ? iend : q;
+}
+
+__device__ __forceinline__ void skel(const Src &S, Win &W, uint32_t &p, uint32_t iend, uint32_t &out,
+                                     uint32_t &nitem)
+{
+    skel_at(S, W, p, iend, out, nitem, rd4(S, W, p));
 }
 
 struct Blk {
@@ -402,14 +408,21 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
         }
         sync();
         ZSK_CT(2)
-        // pass 2: continue to the first position another lane visited
+        // pass 2: continue to the first position another lane visited (the
+        // chunk by a reciprocal multiply, not a division; the map word and
+        // the token read together, one round trip)
+        const uint32_t mC = (uint32_t)((0x100000000ull + C - 1) / C);
         if (act) {
             while (p < B.iend) {
-                const uint32_t c = (p - B.ib) / C;
-                const uint32_t r = p - (B.ib + c * C);
-                if (r < mlen && ((*lp<uint32_t>(mapbase + c * (MW * 4) + 4 * (r >> 5)) >> (r & 31)) & 1))
+                const uint32_t x = p - B.ib;
+                uint32_t c = __umulhi(x, mC);
+                c -= c * C > x ? 1u : 0u;
+                const uint32_t r = x - c * C;
+                const uint32_t mw = *lp<uint32_t>(mapbase + c * (MW * 4) + 4 * ((r < mlen ? r : 0u) >> 5));
+                const uint32_t t4 = rd4(S, W, p);
+                if (r < mlen && ((mw >> (r & 31)) & 1))
                     break;
-                skel(S, W, p, B.iend, tout, tnit);
+                skel_at(S, W, p, B.iend, tout, tnit, t4);
 #ifdef ZSK_TUNING
                 n2_++;
 #endif
