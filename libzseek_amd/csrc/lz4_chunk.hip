@@ -91,9 +91,12 @@ __device__ __forceinline__ __attribute__((address_space(3))) T *lp(uint32_t a)
     return (__attribute__((address_space(3))) T *)(uintptr_t)a;
 }
 
+// KS 1: the frame is known to be staged (the one-frame route's parse
+// instantiates the block parse both ways, so its hot loops carry no test)
+template <int KS = 0>
 __device__ __forceinline__ uint32_t rd4(const Src &S, Win &W, uint32_t x)
 {
-    if (S.staged) {   // (wave-uniform) the frame staged whole: one LDS round trip
+    if (KS == 1 || S.staged) {   // (wave-uniform) the frame staged whole: one LDS round trip
         const uint32_t a = S.lds + (x & ~3u);
         return __builtin_amdgcn_alignbyte(*lp<uint32_t>(a + 4), *lp<uint32_t>(a), x & 3);
     }
@@ -112,9 +115,10 @@ __device__ __forceinline__ uint32_t rd4(const Src &S, Win &W, uint32_t x)
     return __builtin_amdgcn_alignbyte(*lp<uint32_t>(a + 4), *lp<uint32_t>(a), o & 3);
 }
 
+template <int KS = 0>
 __device__ __forceinline__ uint32_t rd1(const Src &S, Win &W, uint32_t x)
 {
-    return rd4(S, W, x) & 0xFF;
+    return rd4<KS>(S, W, x) & 0xFF;
 }
 
 // One sequence of a chain, no validation (passes 1, 2 and the count).
@@ -122,6 +126,7 @@ __device__ __forceinline__ uint32_t rd1(const Src &S, Win &W, uint32_t x)
 // sequence or when the bytes cannot be a sequence) and adds the sequence's
 // output bytes and items.
 // (t4: the four bytes at p, read by the caller)
+template <int KS = 0>
 __device__ __forceinline__ void skel_at(const Src &S, Win &W, uint32_t &p, uint32_t iend, uint32_t &out,
                                         uint32_t &nitem, uint32_t t4)
 {
@@ -132,7 +137,7 @@ __device__ __forceinline__ void skel_at(const Src &S, Win &W, uint32_t &p, uint3
         pp++;
         lit += e;
         while (e == 255 && pp < iend) {
-            e = rd1(S, W, pp);
+            e = rd1<KS>(S, W, pp);
             pp++;
             lit += e;
         }
@@ -143,11 +148,11 @@ __device__ __forceinline__ void skel_at(const Src &S, Win &W, uint32_t &p, uint3
     uint32_t q = pp + lit;
     uint32_t ml = tok & 15;
     if (!endr && ml == 15) {
-        uint32_t e = (rd4(S, W, q) >> 16) & 0xFF;
+        uint32_t e = (rd4<KS>(S, W, q) >> 16) & 0xFF;
         q += 3;
         ml += e;
         while (e == 255 && q < iend) {
-            e = rd1(S, W, q);
+            e = rd1<KS>(S, W, q);
             q++;
             ml += e;
         }
@@ -160,10 +165,11 @@ __device__ __forceinline__ void skel_at(const Src &S, Win &W, uint32_t &p, uint3
     p = endr || q >= iend ? iend : q;
 }
 
+template <int KS = 0>
 __device__ __forceinline__ void skel(const Src &S, Win &W, uint32_t &p, uint32_t iend, uint32_t &out,
                                      uint32_t &nitem)
 {
-    skel_at(S, W, p, iend, out, nitem, rd4(S, W, p));
+    skel_at<KS>(S, W, p, iend, out, nitem, rd4<KS>(S, W, p));
 }
 
 struct Blk {
@@ -199,13 +205,14 @@ __device__ __forceinline__ void put_item(uint64_t *it, uint32_t &k, uint32_t lsr
 // (ST_BLOCK_ERR for a block failure, ST_DST_OVERFLOW), in liblz4's order.
 // A sequence's rules fold into one status and one exit from the loop (fewer
 // divergent exits for the wave to track).
+template <int KS = 0>
 __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B, uint32_t p,
                                               uint32_t y, uint32_t op, uint64_t *it, uint32_t k)
 {
     const uint32_t iend = B.iend;
     int32_t st = -1;
     while (p < y) {
-        const uint32_t t4 = rd4(S, W, p);
+        const uint32_t t4 = rd4<KS>(S, W, p);
         const uint32_t tok = t4 & 0xFF;
         p++;
         uint32_t lit = tok >> 4;
@@ -218,7 +225,7 @@ __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B
             p++;
             lit += e;
             while (e == 255 && p < iend) {
-                e = rd1(S, W, p);
+                e = rd1<KS>(S, W, p);
                 p++;
                 lit += e;
             }
@@ -237,7 +244,7 @@ __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B
         const uint32_t lsrc = p;
         const uint32_t mb = op + lit;
         p += lit;
-        const uint32_t o4 = rd4(S, W, p);
+        const uint32_t o4 = rd4<KS>(S, W, p);
         const uint32_t off = o4 & 0xFFFF;
         p += 2;
         uint32_t ml = tok & 15;
@@ -250,7 +257,7 @@ __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B
                     break;
                 }
                 if (!first)
-                    e = rd1(S, W, p);
+                    e = rd1<KS>(S, W, p);
                 p++;
                 ml += e;
                 if (p >= iend - (kLastLiterals - 1)) {
@@ -322,7 +329,7 @@ __device__ unsigned long long g_ctime[16];
 // ONE: the workgroup's kOneLanes lanes (lane = thread index) take the block,
 // the wave-wide steps (owners, scans, the first failure) going through LDS
 // scratch at `coll` (3 x 256 + 16 words) with workgroup barriers.
-template <bool ONE>
+template <bool ONE, int KS = 0>
 __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane, uint32_t mapbase,
                                uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op, uint32_t recbase,
                                uint32_t coll, uint32_t lead)
@@ -393,14 +400,21 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
         if (act) {
             while (p < t) {
                 const uint32_t r = p - s;
-                if (r < mlen)
-                    __hip_atomic_fetch_or(lp<uint32_t>(mymap + 4 * (r >> 5)), 1u << (r & 31),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                if (ONE && r < mlen && nrec < kR) {
-                    *lp<uint64_t>(myrec + 8 * nrec) = ((uint64_t)tout << 32) | (tnit << 16) | r;
-                    nrec++;
+                const bool in = r < mlen;
+                // (no branches: outside the map an OR of 0 into its first
+                // word; every position stored, counted only inside the chunk
+                // -- a lead-in position's record sits in slot 0 until the
+                // chunk's first overwrites it -- the slot saturating at the
+                // last, a later record, a consistent pair in ascending
+                // order, overwriting it)
+                __hip_atomic_fetch_or(lp<uint32_t>(mymap + 4 * (in ? r >> 5 : 0u)), in ? 1u << (r & 31) : 0u,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                if (ONE) {
+                    *lp<uint64_t>(myrec + 8 * (nrec < kR ? nrec : kR - 1)) =
+                        ((uint64_t)tout << 32) | (tnit << 16) | (r & 0xFFFF);
+                    nrec += r < C && nrec < kR ? 1u : 0u;
                 }
-                skel(S, W, p, B.iend, tout, tnit);
+                skel<KS>(S, W, p, B.iend, tout, tnit);
 #ifdef ZSK_TUNING
                 n1_++;
 #endif
@@ -419,10 +433,10 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
                 c -= c * C > x ? 1u : 0u;
                 const uint32_t r = x - c * C;
                 const uint32_t mw = *lp<uint32_t>(mapbase + c * (MW * 4) + 4 * ((r < mlen ? r : 0u) >> 5));
-                const uint32_t t4 = rd4(S, W, p);
+                const uint32_t t4 = rd4<KS>(S, W, p);
                 if (r < mlen && ((mw >> (r & 31)) & 1))
                     break;
-                skel_at(S, W, p, B.iend, tout, tnit, t4);
+                skel_at<KS>(S, W, p, B.iend, tout, tnit, t4);
 #ifdef ZSK_TUNING
                 n2_++;
 #endif
@@ -536,7 +550,7 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
     if (tru && !counted) {
         uint32_t p = entry;
         while (p < y)
-            skel(S, W, p, B.iend, out, nit);
+            skel<KS>(S, W, p, B.iend, out, nit);
     }
     ZSK_CT(4)
     uint32_t otot, ktot;
@@ -546,7 +560,7 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
     // emit: the validated parse, items in place
     int32_t st = -1;
     if (tru)
-        st = emit_range(S, W, B, entry, y, op + oinc - out, it, k + kinc - nit);
+        st = emit_range<KS>(S, W, B, entry, y, op + oinc - out, it, k + kinc - nit);
 #ifdef ZSK_TUNING
     ZSK_CT(5)
     ZSK_CN(8, n1_)
@@ -834,9 +848,13 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
                 st = block_fail(B, bsid, max_block);
                 break;
             }
+            // (ONE: a staged frame's parse without the staged test per read)
             const int32_t bs =
-                chunk_block<ONE>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
-                                 (uint32_t)(uintptr_t)coll, lead);
+                ONE && S.staged
+                    ? chunk_block<ONE, 1>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
+                                          (uint32_t)(uintptr_t)coll, lead)
+                    : chunk_block<ONE, 0>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
+                                          (uint32_t)(uintptr_t)coll, lead);
             if (bs == ST_BLOCK_ERR)
                 st = block_fail(B, bsid, max_block);
             else if (bs >= 0)
