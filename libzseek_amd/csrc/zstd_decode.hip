@@ -226,7 +226,9 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
         *err = ZE_CORRUPT;
         return 0;
     }
-    int32_t remaining = (1 << tl) + 1, threshold = 1 << tl;
+    // (threshold = 1 << (nbits - 1) throughout: derived, not carried -- one
+    // loop value fewer in the frame kernel's tight scalar register budget)
+    int32_t remaining = (1 << tl) + 1;
     uint32_t nbits = tl + 1, sym = 0;
     bool prev0 = false;
     while (remaining > 1 && sym <= max_sym) {
@@ -248,6 +250,7 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
             }
             sym = n0;   // the skipped counts stay 0
         }
+        const int32_t threshold = 1 << (nbits - 1);
         const int32_t mx = 2 * threshold - 1 - remaining;
         const int32_t v = (int32_t)bits(nbits);
         // (both field widths as selects, no branch per symbol)
@@ -264,11 +267,7 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
         // FSE_readNCount's `while (remaining < threshold) { nbBits--;
         // threshold >>= 1; }`: remaining stays >= 1 (a count never exceeds
         // it), so the field width becomes min(nbits, log2(remaining) + 1)
-        {
-            const uint32_t w1 = 32u - (uint32_t)__builtin_clz((uint32_t)remaining);
-            nbits = min(nbits, w1);
-            threshold = 1 << (nbits - 1);
-        }
+        nbits = min(nbits, 32u - (uint32_t)__builtin_clz((uint32_t)remaining));
         if (pos > 8 * 256) {   // ran off the window: no valid description is that long
             *err = ZE_CORRUPT;
             return 0;
