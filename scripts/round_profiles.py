@@ -99,7 +99,8 @@ ea = {}
 if glob.glob(os.path.join(src, "ea_p1", "**", "*_counter_collection.csv"), recursive=True):
     cnt = {}
     for i in (1, 2, 3):
-        for f in glob.glob(os.path.join(src, f"ea_p{i}", "**", "*_counter_collection.csv"), recursive=True):
+        # (the newest pass only: gpurun_out/ keeps earlier calls' files too)
+        for f in [one(f"ea_p{i}/*/*_counter_collection.csv")]:
             shutil.copy(f, os.path.join(dst, f"{tag}_ea_p{i}.csv"))
             for row in csv.DictReader(open(f)):
                 k = part(row["Kernel_Name"])
