@@ -434,3 +434,68 @@ def test_zstd_x2_fixtures_pread(gpu, zs, cache):
             assert hashlib.sha256(out[:pos].tobytes()).hexdigest() == want["sha"]
             if n < 0:
                 assert r.error == want["error"]
+
+
+def _seekable(frames, sizes):
+    """a seekable image of the given compressed frames (seek table without
+    checksums: entries of compressed / decompressed size, then the footer)"""
+    import struct
+    table = b"".join(struct.pack("<II", len(f), s) for f, s in zip(frames, sizes))
+    table += struct.pack("<IBI", len(frames), 0, 0x8F92EAB1)
+    return b"".join(frames) + struct.pack("<II", 0x184D2A5E, len(table)) + table
+
+
+@pytest.mark.parametrize("cache", [0, 1])
+def test_zstd_content_checksum_like_reference(gpu, zs, zstd, ref, cache):
+    """Frames carrying a content checksum, one of them wrong: every query,
+    read the way callers read (pread again after a short read, until the
+    count, EOF or an error), gives the reference library's bytes and then its
+    error text -- through the one-frame route (its host plan sees the
+    checksum flags and runs the check kernel; a no-cache read that stops
+    before the frame's end never reaches the checksum, as libzstd's
+    streaming decoder does not).  (One pread may return more than the
+    reference's -- several frames, not one -- a legal short-read difference.)"""
+    data = zs.synth_buffer(5 * 65536).tobytes()
+    frames = [compress(zstd, data[i * 65536:(i + 1) * 65536], {P_LEVEL: 3, P_CHECKSUM: 1}) for i in range(5)]
+    bad = bytearray(frames[2])
+    bad[-1] ^= 0x5A   # the checksum's last byte
+    frames[2] = bytes(bad)
+    img = _seekable(frames, [65536] * 5)
+
+    def drive(pread, count, off):
+        got, err = b"", None
+        while len(got) < count:
+            rc, b, e = pread(count - len(got), off + len(got))
+            if rc < 0:
+                err = e
+                break
+            if rc == 0:
+                break
+            got += b
+        return got, err
+
+    def ours_pread(r):
+        def f(n, o):
+            try:
+                b = r.pread(n, o)
+                return len(b), b, None
+            except zs.ZseekError as e:
+                return -1, b"", str(e)
+        return f
+
+    def ref_pread(r):
+        def f(n, o):
+            rc, b = r.pread(n, o)
+            return rc, b, (r.error if rc < 0 else None)
+        return f
+
+    queries = [(100, 2 * 65536), (65536, 2 * 65536), (3 * 65536, 65536), (65536 - 10, 2 * 65536 + 10),
+               (10, 3 * 65536 - 10), (5 * 65536, 0), (200, 4 * 65536)]
+    for count, off in queries:
+        ours = zs.Reader(np.frombuffer(img, np.uint8), cache)
+        theirs = ref.open(img, cache)
+        try:
+            assert drive(ours_pread(ours), count, off) == drive(ref_pread(theirs), count, off), (count, off)
+        finally:
+            ours.close()
+            theirs.close()
