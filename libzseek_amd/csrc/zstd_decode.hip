@@ -2095,7 +2095,8 @@ __device__ __forceinline__ bool lemit(LSink &S, uint32_t src, uint32_t lit, uint
     const bool ok = S.k + n <= S.cap;
     const uint64_t e0 = ((uint64_t)off << 32) | src | kItemExt, e1 = ((uint64_t)ml << 32) | lit;
     const uint64_t sh = ((uint64_t)(off | lit << 16 | (ml ? ml - 3 : 0) << 24) << 32) | src;
-    lput3(S, ok && (!ONE || lane_id() == 0) ? n : 0, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
+    // (ONE: thread 0's -- lane 0 of the first wave -- land)
+    lput3(S, ok && (!ONE || threadIdx.x == 0) ? n : 0, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
     S.k += ok ? n : 0;
     return ok;
 }
@@ -2277,11 +2278,14 @@ struct SeqLds {
     __attribute__((aligned(16))) uint16_t ftab[CELLS && !ONE ? LANES * CELLS : 8];
     __attribute__((aligned(16))) uint8_t sstage[ONE ? kSeqStage + 32 : 16];
     uint64_t xtab[ONE ? kSeqOneCells : 1];                 // ONE: the expanded cells (below)
-    __attribute__((aligned(16))) uint32_t srec[ONE ? 64 * 8 : 4];   // ONE: a batch's records
+    __attribute__((aligned(16))) uint32_t srec[ONE ? 2 * 64 * 8 : 4];   // ONE: a batch's records (two buffers)
+    uint32_t xflag;     // (two waves) a failure: stop
+    uint32_t xst[8];    // (two waves) the replay state handed over
 };
 
-// the replay of workgroup bid (one wave: threads 0-63)
-template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false>
+// the replay of workgroup bid (one wave: threads 0-63; TWO: two, the
+// one-frame replay's chain on wave 0 and its vector phase on wave 1)
+template <uint32_t LANES, uint32_t CELLS, uint32_t GM = 0, bool ONE = false, bool TWO = false>
 __device__ __forceinline__ void seq_body(
     SeqLds<LANES, CELLS, ONE> &SH, uint32_t bid, const FrameDesc *__restrict__ desc, uint32_t n,
     const uint8_t *__restrict__ comp, uint8_t *__restrict__ ops, const uint64_t *__restrict__ blk_base,
@@ -2296,12 +2300,14 @@ __device__ __forceinline__ void seq_body(
     auto &srec = SH.srec;
 #ifdef ZSK_TUNING
     const uint64_t tk0 = __builtin_readcyclecounter(), rt0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t tloop = 0, nseqs = 0;
+    uint64_t tloop = 0, nseqs = 0, tchain = 0;
 #endif
     for (uint32_t i = threadIdx.x; i < 89; i += 64)
         codes[i] = i < 36 ? c_ll[i] : c_ml[i - 36];
+    if (threadIdx.x == 0)
+        SH.xflag = 0;
     __syncthreads();
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t f = ONE ? f0 + bid : f0 + bid * LANES + lane;   // frames [f0, n)
     const bool act = (ONE || lane < LANES) && f < n;
     FrameDesc d = {0, 0, 0, 0};
@@ -2370,16 +2376,24 @@ __device__ __forceinline__ void seq_body(
                         // below the stream zeroed too (the window's "bits below
                         // the stream read as 0" without a branch per sequence)
                         const uint32_t x0 = sx & ~3u, nb = (sx & 3u) + P.c, sl = ldsaddr(sstage) + 16;
+                        // (TWO: wave 0 stages, then a barrier -- wave 1 reads
+                        // the same bytes, so both waves take the same branches)
+                        const bool stager = !TWO || threadIdx.x < 64;
+                        if constexpr (TWO)
+                            __syncthreads();   // (the last block's stage read by both)
                         wave_lds_sync();
-                        for (uint32_t q = 16 * lane; q < nb; q += 1024)
-                            *la<u32x4_a4>(sl + q) =
-                                __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, x0 + q, 0, 0));
+                        if (stager)
+                            for (uint32_t q = 16 * lane; q < nb; q += 1024)
+                                *la<u32x4_a4>(sl + q) =
+                                    __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, x0 + q, 0, 0));
                         wave_lds_sync();
-                        if (lane == 0) {
+                        if (stager && lane == 0) {
                             *la<u32x4>(sl - 16) = (u32x4){0, 0, 0, 0};
                             *la<uint32_t>(sl) &= above(8 * (int32_t)(sx & 3u), 0);
                         }
                         wave_lds_sync();
+                        if constexpr (TWO)
+                            __syncthreads();
                         b.sl = sl;
                         staged = true;
                     }
@@ -2408,7 +2422,7 @@ __device__ __forceinline__ void seq_body(
                         // order, values and checks as the loop below.
                         const uint32_t xb = ldsaddr(xtab), ncell = nll + nof + nml;
                         wave_lds_sync();
-                        for (uint32_t cix = lane; cix < ncell; cix += 64) {
+                        for (uint32_t cix = lane; cix < ((!TWO || threadIdx.x < 64) ? ncell : 0u); cix += 64) {
                             const uint32_t t = cix < nll ? 0u : cix < nll + nof ? 1u : 2u;
                             const uint32_t toff = t == 0 ? 0u : t == 1 ? nll : nll + nof;
                             const uint32_t x = cix - toff;
@@ -2426,6 +2440,8 @@ __device__ __forceinline__ void seq_body(
                             *la<uint64_t>(xb + 8 * cix) = (uint64_t)hi32 << 32 | (xb + 8 * (toff + nbase));
                         }
                         wave_lds_sync();
+                        if constexpr (TWO)
+                            __syncthreads();   // (wave 0's cells, seen by both)
                         // (an opaque per-lane zero in the addresses keeps the chain
                         // in VGPRs: scalarized, each LDS result waited for and
                         // copied to SGPRs at once -- the window's and the cells'
@@ -2471,193 +2487,257 @@ __device__ __forceinline__ void seq_body(
                         // the serial loop below leaves -- items, o, lp_, S.k,
                         // err -- is the same.
                         const uint32_t rec = ldsaddr(srec);
-                        for (uint32_t i = 0; i < nseq && !err;) {
-                            const uint32_t nb = min(64u, nseq - i);
-                            const uint32_t nd = nb;
-                            wave_lds_sync();   // the last batch's records read
-                            // (lane 0 alone runs the chain: every lane's copy of
-                            // a uniform read or store costs the LDS 64 times the
-                            // bytes; the chain's registers are lane 0's)
-                            if (lane == 0)
-                            for (uint32_t q = 0; q < nb; q++) {
-                                // the 96 stream bits below cur, top-aligned: bit
-                                // 95 of N3:N2:N1 is stream bit cur - 1 (the
-                                // align takes the shift's low five bits)
-                                const uint32_t N3 = __builtin_amdgcn_alignbit(W.w, W.z, (uint32_t)cur),
-                                               N2 = __builtin_amdgcn_alignbit(W.z, W.y, (uint32_t)cur),
-                                               N1 = __builtin_amdgcn_alignbit(W.y, W.x, (uint32_t)cur);
-                                const uint64_t H = (uint64_t)N3 << 32 | N2;
-                                const uint32_t hl = (uint32_t)(cl >> 32), hm = (uint32_t)(cm >> 32), ho = (uint32_t)(co >> 32);
-                                // the sequence's bits: OF, ML, LL values, then the
-                                // LL, ML, OF states (T <= 31 + 16 + 16 + 26 = 89)
-                                // (byte-select adds: the three counts are the cells' top bytes)
-                                uint32_t T;
-                                asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
-                                    "v_add_u32_sdwa %0, %0, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
-                                    : "=&v"(T)
-                                    : "v"(hl), "v"(hm), "v"(ho));
-                                // (T <= 64: from N3:N2; else at bit 96 - T < 32 of N2:N1)
-                                const uint32_t yH = (uint32_t)(H >> ((64 - T) & 63)),
-                                               yM = __builtin_amdgcn_alignbit(N2, N1, 0u - T);
-                                // (a select in asm: the compiler made the choice an
-                                // if / else over the exec mask, twice the ops)
-                                uint32_t Y;
-                                asm("v_cmp_ge_u32 vcc, 64, %1\n\tv_cndmask_b32 %0, %2, %3, vcc"
-                                    : "=v"(Y)
-                                    : "v"(T), "v"(yM), "v"(yH)
-                                    : "vcc");
-                                // (the extract takes offset and width from the low
-                                // five bits: the state counts straight from hi)
-                                const uint32_t ao = (uint32_t)co + (__builtin_amdgcn_ubfe(Y, 0, ho) << 3),
-                                               am = (uint32_t)cm + (__builtin_amdgcn_ubfe(Y, ho, hm) << 3),
-                                               al = (uint32_t)cl + (__builtin_amdgcn_ubfe(Y, ho + hm, hl) << 3);
-                                const int32_t cur2 = cur - (int32_t)T;
-                                // the record (this sequence's values are the
-                                // vector phase's, from H and the cells), stored
-                                // ahead of the next sequence's reads: after them,
-                                // the wait for them would wait for it too
-                                // (two paired stores in asm: the compiler's own
-                                // choice varied with the kernel it sat in, up to
-                                // four stores and four address moves)
-                                asm volatile("ds_write2_b64 %0, %1, %2 offset1:1\n\t"
-                                             "ds_write2_b64 %0, %3, %4 offset0:2 offset1:3"
-                                             :
-                                             : "v"(rec + 32 * q), "v"(H), "v"(cl), "v"(cm), "v"(co)
-                                             : "memory");
-                                const u32x4 W2 = win(cur2);
-                                const uint64_t cl2 = *la<uint64_t>(al), cm2 = *la<uint64_t>(am), co2 = *la<uint64_t>(ao);
-                                cl = cl2;
-                                cm = cm2;
-                                co = co2;
-                                W = W2;
-                                cur = cur2;
-                            }
-                            wave_lds_sync();
-                            const bool on = lane < nd;
-                            uint32_t ofv = 0, ml = 0, ll = 0, bad = 0;
-                            if (on) {
-                                const u32x4 R = *la<u32x4>(rec + 32 * lane), R2 = *la<u32x4>(rec + 32 * lane + 16);
-                                const uint32_t hl = R.w, hm = R2.y, ho = R2.w;
-                                const uint32_t ob = __builtin_amdgcn_ubfe(ho, 8, 5), mb = __builtin_amdgcn_ubfe(hm, 8, 5),
-                                               lb = __builtin_amdgcn_ubfe(hl, 8, 5), vb = ob + mb + lb;
-                                const uint64_t H = (uint64_t)R.y << 32 | R.x;
-                                const uint32_t X = (uint32_t)(H >> ((64 - vb) & 63));
-                                ofv = (1u << ob) + __builtin_amdgcn_ubfe(R.y, 32 - ob, ob);
-                                ll = (codes[__builtin_amdgcn_ubfe(hl, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, 0, lb);
-                                ml = (codes[36 + __builtin_amdgcn_ubfe(hm, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, lb, mb);
-                                bad = ((ho | hm | hl) >> 13) & 1;
-                            }
-                            // repeat offsets (RFC 8878 §3.1.2.5) by a scan: each
-                            // sequence maps the history (a, b, c) = (rep0, rep1,
-                            // rep2) to a new one -- a new offset v: (v, a, b);
-                            // index 0: (a, b, c); 1: (b, a, c); 2: (c, a, b); 3:
-                            // (a - 1 but >= 1, a, b) -- and its offset is the new
-                            // first entry.  A composed map keeps, per entry,
-                            // either a value (tag 3) or "old entry t less d"
-                            // (tag t, d decrements: max(x - d, 1), as repeated
-                            // decrements of values >= 1 compose).  Six shuffle
-                            // steps compose each lane's prefix; applied to the
-                            // batch's starting history they give every offset.
-                            uint32_t tg[3], vl[3];
-                            {
-                                const bool fresh = ofv > 3;
-                                const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
-                                tg[0] = fresh ? 3u : idx == 3 ? 0u : idx;
-                                vl[0] = fresh ? ofv - 3 : idx == 3 ? 1u : 0u;
-                                tg[1] = !fresh && idx == 0 ? 1u : 0u;
-                                tg[2] = !fresh && idx <= 1 ? 2u : 1u;
-                                vl[1] = vl[2] = 0;
-                                if (!on) {   // identity
-                                    tg[0] = 0;
-                                    tg[1] = 1;
-                                    tg[2] = 2;
-                                    vl[0] = 0;
+                        // the chain of a batch of nb sequences: records at rb
+                        auto chain = [&](uint32_t rb, uint32_t nb) {
+                                if (lane == 0)
+                                for (uint32_t q = 0; q < nb; q++) {
+                                    // the 96 stream bits below cur, top-aligned: bit
+                                    // 95 of N3:N2:N1 is stream bit cur - 1 (the
+                                    // align takes the shift's low five bits)
+                                    const uint32_t N3 = __builtin_amdgcn_alignbit(W.w, W.z, (uint32_t)cur),
+                                                   N2 = __builtin_amdgcn_alignbit(W.z, W.y, (uint32_t)cur),
+                                                   N1 = __builtin_amdgcn_alignbit(W.y, W.x, (uint32_t)cur);
+                                    const uint64_t H = (uint64_t)N3 << 32 | N2;
+                                    const uint32_t hl = (uint32_t)(cl >> 32), hm = (uint32_t)(cm >> 32), ho = (uint32_t)(co >> 32);
+                                    // the sequence's bits: OF, ML, LL values, then the
+                                    // LL, ML, OF states (T <= 31 + 16 + 16 + 26 = 89)
+                                    // (byte-select adds: the three counts are the cells' top bytes)
+                                    uint32_t T;
+                                    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+                                        "v_add_u32_sdwa %0, %0, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+                                        : "=&v"(T)
+                                        : "v"(hl), "v"(hm), "v"(ho));
+                                    // (T <= 64: from N3:N2; else at bit 96 - T < 32 of N2:N1)
+                                    const uint32_t yH = (uint32_t)(H >> ((64 - T) & 63)),
+                                                   yM = __builtin_amdgcn_alignbit(N2, N1, 0u - T);
+                                    // (a select in asm: the compiler made the choice an
+                                    // if / else over the exec mask, twice the ops)
+                                    uint32_t Y;
+                                    asm("v_cmp_ge_u32 vcc, 64, %1\n\tv_cndmask_b32 %0, %2, %3, vcc"
+                                        : "=v"(Y)
+                                        : "v"(T), "v"(yM), "v"(yH)
+                                        : "vcc");
+                                    // (the extract takes offset and width from the low
+                                    // five bits: the state counts straight from hi)
+                                    const uint32_t ao = (uint32_t)co + (__builtin_amdgcn_ubfe(Y, 0, ho) << 3),
+                                                   am = (uint32_t)cm + (__builtin_amdgcn_ubfe(Y, ho, hm) << 3),
+                                                   al = (uint32_t)cl + (__builtin_amdgcn_ubfe(Y, ho + hm, hl) << 3);
+                                    const int32_t cur2 = cur - (int32_t)T;
+                                    // the record (this sequence's values are the
+                                    // vector phase's, from H and the cells), stored
+                                    // ahead of the next sequence's reads: after them,
+                                    // the wait for them would wait for it too
+                                    // (two paired stores in asm: the compiler's own
+                                    // choice varied with the kernel it sat in, up to
+                                    // four stores and four address moves)
+                                    asm volatile("ds_write2_b64 %0, %1, %2 offset1:1\n\t"
+                                                 "ds_write2_b64 %0, %3, %4 offset0:2 offset1:3"
+                                                 :
+                                                 : "v"(rb + 32 * q), "v"(H), "v"(cl), "v"(cm), "v"(co)
+                                                 : "memory");
+                                    const u32x4 W2 = win(cur2);
+                                    const uint64_t cl2 = *la<uint64_t>(al), cm2 = *la<uint64_t>(am), co2 = *la<uint64_t>(ao);
+                                    cl = cl2;
+                                    cm = cm2;
+                                    co = co2;
+                                    W = W2;
+                                    cur = cur2;
                                 }
-                            }
-#pragma unroll
-                            for (uint32_t sft = 1; sft < 64; sft <<= 1) {
-                                uint32_t pt[3], pv[3];
-#pragma unroll
-                                for (int q = 0; q < 3; q++) {
-                                    pt[q] = (uint32_t)__shfl_up((int)tg[q], sft, 64);
-                                    pv[q] = (uint32_t)__shfl_up((int)vl[q], sft, 64);
+                        };
+                        // the vector phase of a batch of nd records at rb
+                        auto vphase = [&](uint32_t rb, uint32_t nd) {
+                                const bool on = lane < nd;
+                                uint32_t ofv = 0, ml = 0, ll = 0, bad = 0;
+                                if (on) {
+                                    const u32x4 R = *la<u32x4>(rb + 32 * lane), R2 = *la<u32x4>(rb + 32 * lane + 16);
+                                    const uint32_t hl = R.w, hm = R2.y, ho = R2.w;
+                                    const uint32_t ob = __builtin_amdgcn_ubfe(ho, 8, 5), mb = __builtin_amdgcn_ubfe(hm, 8, 5),
+                                                   lb = __builtin_amdgcn_ubfe(hl, 8, 5), vb = ob + mb + lb;
+                                    const uint64_t H = (uint64_t)R.y << 32 | R.x;
+                                    const uint32_t X = (uint32_t)(H >> ((64 - vb) & 63));
+                                    ofv = (1u << ob) + __builtin_amdgcn_ubfe(R.y, 32 - ob, ob);
+                                    ll = (codes[__builtin_amdgcn_ubfe(hl, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, 0, lb);
+                                    ml = (codes[36 + __builtin_amdgcn_ubfe(hm, 16, 6)] & 0xFFFFFF) + __builtin_amdgcn_ubfe(X, lb, mb);
+                                    bad = ((ho | hm | hl) >> 13) & 1;
                                 }
-                                if (lane >= sft) {
-#pragma unroll
-                                    for (int q = 0; q < 3; q++) {   // mine after the earlier prefix
-                                        const uint32_t t = tg[q], v = vl[q];
-                                        const uint32_t et = t == 0 ? pt[0] : t == 1 ? pt[1] : pt[2];
-                                        const uint32_t ev = t == 0 ? pv[0] : t == 1 ? pv[1] : pv[2];
-                                        tg[q] = t == 3 ? 3u : et;
-                                        vl[q] = t == 3 ? v : et == 3 ? (ev > v ? ev - v : 1u) : ev + v;
+                                // repeat offsets (RFC 8878 §3.1.2.5) by a scan: each
+                                // sequence maps the history (a, b, c) = (rep0, rep1,
+                                // rep2) to a new one -- a new offset v: (v, a, b);
+                                // index 0: (a, b, c); 1: (b, a, c); 2: (c, a, b); 3:
+                                // (a - 1 but >= 1, a, b) -- and its offset is the new
+                                // first entry.  A composed map keeps, per entry,
+                                // either a value (tag 3) or "old entry t less d"
+                                // (tag t, d decrements: max(x - d, 1), as repeated
+                                // decrements of values >= 1 compose).  Six shuffle
+                                // steps compose each lane's prefix; applied to the
+                                // batch's starting history they give every offset.
+                                uint32_t tg[3], vl[3];
+                                {
+                                    const bool fresh = ofv > 3;
+                                    const uint32_t idx = fresh ? 0u : ofv - 1 + (ll == 0);
+                                    tg[0] = fresh ? 3u : idx == 3 ? 0u : idx;
+                                    vl[0] = fresh ? ofv - 3 : idx == 3 ? 1u : 0u;
+                                    tg[1] = !fresh && idx == 0 ? 1u : 0u;
+                                    tg[2] = !fresh && idx <= 1 ? 2u : 1u;
+                                    vl[1] = vl[2] = 0;
+                                    if (!on) {   // identity
+                                        tg[0] = 0;
+                                        tg[1] = 1;
+                                        tg[2] = 2;
+                                        vl[0] = 0;
                                     }
                                 }
-                            }
-                            auto apply = [&](uint32_t t, uint32_t v) -> uint32_t {
-                                if (t == 3)
-                                    return v;
-                                const uint32_t x = t == 0 ? rep0 : t == 1 ? rep1 : rep2;
-                                return x > v ? x - v : 1u;
-                            };
-                            const uint32_t off = apply(tg[0], vl[0]);
-                            if (nd) {
-                                const uint32_t n0 = lane_val(off, (int)nd - 1),
-                                               n1v = lane_val(apply(tg[1], vl[1]), (int)nd - 1),
-                                               n2v = lane_val(apply(tg[2], vl[2]), (int)nd - 1);
-                                rep0 = n0;
-                                rep1 = n1v;
-                                rep2 = n2v;
-                            }
-                            // item slots (lemit's rule: an extended pair never
-                            // starts in slot 63 of a 64-slot group, a zero item
-                            // pads it): a scan without pads, then, only if some
-                            // extended pair lands on slot 63, the slots again
-                            // sequence by sequence
-                            const bool ext = on && (ll > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF);
-                            const uint32_t n1 = on ? (ext ? 2u : 1u) : 0u;
-                            uint32_t kq = S.k + wave_incl_add(n1) - n1, pad = 0;
-                            if (__ballot(ext && (kq & 63) == 63)) {
-                                uint32_t k = S.k;
-                                for (uint32_t q = 0; q < nd; q++) {
-                                    const bool eq = lane_val(ext ? 1u : 0u, (int)q) != 0;
-                                    const uint32_t pq = eq && (k & 63) == 63 ? 1u : 0u;
-                                    if (lane == q) {
-                                        kq = k;
-                                        pad = pq;
+    #pragma unroll
+                                for (uint32_t sft = 1; sft < 64; sft <<= 1) {
+                                    uint32_t pt[3], pv[3];
+    #pragma unroll
+                                    for (int q = 0; q < 3; q++) {
+                                        pt[q] = (uint32_t)__shfl_up((int)tg[q], sft, 64);
+                                        pv[q] = (uint32_t)__shfl_up((int)vl[q], sft, 64);
                                     }
-                                    k += eq ? 2 + pq : 1;
+                                    if (lane >= sft) {
+    #pragma unroll
+                                        for (int q = 0; q < 3; q++) {   // mine after the earlier prefix
+                                            const uint32_t t = tg[q], v = vl[q];
+                                            const uint32_t et = t == 0 ? pt[0] : t == 1 ? pt[1] : pt[2];
+                                            const uint32_t ev = t == 0 ? pv[0] : t == 1 ? pv[1] : pv[2];
+                                            tg[q] = t == 3 ? 3u : et;
+                                            vl[q] = t == 3 ? v : et == 3 ? (ev > v ? ev - v : 1u) : ev + v;
+                                        }
+                                    }
                                 }
+                                auto apply = [&](uint32_t t, uint32_t v) -> uint32_t {
+                                    if (t == 3)
+                                        return v;
+                                    const uint32_t x = t == 0 ? rep0 : t == 1 ? rep1 : rep2;
+                                    return x > v ? x - v : 1u;
+                                };
+                                const uint32_t off = apply(tg[0], vl[0]);
+                                if (nd) {
+                                    const uint32_t n0 = lane_val(off, (int)nd - 1),
+                                                   n1v = lane_val(apply(tg[1], vl[1]), (int)nd - 1),
+                                                   n2v = lane_val(apply(tg[2], vl[2]), (int)nd - 1);
+                                    rep0 = n0;
+                                    rep1 = n1v;
+                                    rep2 = n2v;
+                                }
+                                // item slots (lemit's rule: an extended pair never
+                                // starts in slot 63 of a 64-slot group, a zero item
+                                // pads it): a scan without pads, then, only if some
+                                // extended pair lands on slot 63, the slots again
+                                // sequence by sequence
+                                const bool ext = on && (ll > 255 || ml > 258 || (ml != 0 && ml < 4) || off > 0xFFFF);
+                                const uint32_t n1 = on ? (ext ? 2u : 1u) : 0u;
+                                uint32_t kq = S.k + wave_incl_add(n1) - n1, pad = 0;
+                                if (__ballot(ext && (kq & 63) == 63)) {
+                                    uint32_t k = S.k;
+                                    for (uint32_t q = 0; q < nd; q++) {
+                                        const bool eq = lane_val(ext ? 1u : 0u, (int)q) != 0;
+                                        const uint32_t pq = eq && (k & 63) == 63 ? 1u : 0u;
+                                        if (lane == q) {
+                                            kq = k;
+                                            pad = pq;
+                                        }
+                                        k += eq ? 2 + pq : 1;
+                                    }
+                                }
+                                const uint32_t ni = ext ? 2 + pad : 1;
+                                const uint32_t ill = wave_incl_add(ll), iol = wave_incl_add(ll + ml);
+                                const uint32_t lpq = lp_ + ill - ll, oq = o + iol - (ll + ml);
+                                const uint32_t kind = bad                ? (uint32_t)ZE_CORRUPT
+                                                      : ll + ml > cap - oq ? (uint32_t)ZE_DST_SMALL
+                                                      : le - lpq < ll    ? (uint32_t)ZE_CORRUPT
+                                                      : off > oq + ll    ? (uint32_t)ZE_CORRUPT
+                                                      : kq + ni > S.cap  ? (uint32_t)ZE_GENERIC
+                                                                         : 0u;
+                                const uint64_t em = __ballot(on && kind != 0);
+                                const uint32_t e = em ? (uint32_t)__builtin_ctzll(em) : nd;
+                                if (lane < e) {
+                                    const uint64_t e0 = ((uint64_t)off << 32) | lpq | kItemExt, e1 = ((uint64_t)ml << 32) | ll;
+                                    const uint64_t sh = ((uint64_t)(off | ll << 16 | (ml ? ml - 3 : 0) << 24) << 32) | lpq;
+                                    LSink Q = S;
+                                    Q.k = kq;
+                                    lput3(Q, ni, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
+                                }
+                                if (e > 0) {
+                                    lp_ += lane_val(ill, (int)e - 1);
+                                    o += lane_val(iol, (int)e - 1);
+                                }
+                                if (e < nd) {
+                                    err = lane_val(kind, (int)e);
+                                    S.k = lane_val(kq, (int)e);
+                                } else {
+                                    if (nd)
+                                        S.k = lane_val(kq + ni, (int)nd - 1);
+                                }
+                        };
+                        if constexpr (TWO) {
+                            // two waves (the fused launch's first two): wave 0
+                            // runs batch k's chain while wave 1 runs batch k - 1's
+                            // vector phase -- records double-buffered, one
+                            // barrier per step; a failure found by wave 1 stops
+                            // both after the step; then wave 1's replay state and
+                            // wave 0's cursor are exchanged, so both waves go on
+                            // with the same values
+                            const uint32_t wv = threadIdx.x >> 6, nbat = (nseq + 63) / 64;
+                            for (uint32_t kb = 0; kb <= nbat; kb++) {
+                                if (wv == 0 && kb < nbat) {
+#ifdef ZSK_TUNING
+                                    const uint64_t tc0 = __builtin_readcyclecounter();
+#endif
+                                    chain(rec + 2048 * (kb & 1), min(64u, nseq - 64 * kb));
+#ifdef ZSK_TUNING
+                                    tchain += __builtin_readcyclecounter() - tc0;
+#endif
+                                }
+                                if (wv == 1 && kb >= 1) {
+                                    vphase(rec + 2048 * ((kb - 1) & 1), min(64u, nseq - 64 * (kb - 1)));
+                                    if (err && lane == 0)
+                                        SH.xflag = 1;
+                                }
+                                __syncthreads();
+                                if (uni(*lp<uint32_t>(&SH.xflag)))
+                                    break;
                             }
-                            const uint32_t ni = ext ? 2 + pad : 1;
-                            const uint32_t ill = wave_incl_add(ll), iol = wave_incl_add(ll + ml);
-                            const uint32_t lpq = lp_ + ill - ll, oq = o + iol - (ll + ml);
-                            const uint32_t kind = bad                ? (uint32_t)ZE_CORRUPT
-                                                  : ll + ml > cap - oq ? (uint32_t)ZE_DST_SMALL
-                                                  : le - lpq < ll    ? (uint32_t)ZE_CORRUPT
-                                                  : off > oq + ll    ? (uint32_t)ZE_CORRUPT
-                                                  : kq + ni > S.cap  ? (uint32_t)ZE_GENERIC
-                                                                     : 0u;
-                            const uint64_t em = __ballot(on && kind != 0);
-                            const uint32_t e = em ? (uint32_t)__builtin_ctzll(em) : nd;
-                            if (lane < e) {
-                                const uint64_t e0 = ((uint64_t)off << 32) | lpq | kItemExt, e1 = ((uint64_t)ml << 32) | ll;
-                                const uint64_t sh = ((uint64_t)(off | ll << 16 | (ml ? ml - 3 : 0) << 24) << 32) | lpq;
-                                LSink Q = S;
-                                Q.k = kq;
-                                lput3(Q, ni, ext ? (pad ? 0 : e0) : sh, pad ? e0 : e1, e1);
+                            if (wv == 1 && lane == 0) {
+                                SH.xst[0] = o;
+                                SH.xst[1] = lp_;
+                                SH.xst[2] = S.k;
+                                SH.xst[3] = err;
+                                SH.xst[4] = rep0;
+                                SH.xst[5] = rep1;
+                                SH.xst[6] = rep2;
                             }
-                            if (e > 0) {
-                                lp_ += lane_val(ill, (int)e - 1);
-                                o += lane_val(iol, (int)e - 1);
+                            if (wv == 0 && lane == 0)
+                                SH.xst[7] = (uint32_t)cur;
+                            __syncthreads();
+                            o = uni(*lp<uint32_t>(&SH.xst[0]));
+                            lp_ = uni(*lp<uint32_t>(&SH.xst[1]));
+                            S.k = uni(*lp<uint32_t>(&SH.xst[2]));
+                            err = uni(*lp<uint32_t>(&SH.xst[3]));
+                            rep0 = uni(*lp<uint32_t>(&SH.xst[4]));
+                            rep1 = uni(*lp<uint32_t>(&SH.xst[5]));
+                            rep2 = uni(*lp<uint32_t>(&SH.xst[6]));
+                            cur = (int32_t)uni(*lp<uint32_t>(&SH.xst[7]));
+                            __syncthreads();   // (everyone has read; the flag reset for the next block)
+                            if (threadIdx.x == 0)
+                                SH.xflag = 0;
+                            __syncthreads();
+                        } else {
+                            for (uint32_t i = 0; i < nseq && !err;) {
+                                const uint32_t nb = min(64u, nseq - i);
+                                wave_lds_sync();   // the last batch's records read
+#ifdef ZSK_TUNING
+                                const uint64_t tc0 = __builtin_readcyclecounter();
+#endif
+                                chain(rec, nb);
+                                wave_lds_sync();
+#ifdef ZSK_TUNING
+                                tchain += __builtin_readcyclecounter() - tc0;
+#endif
+                                vphase(rec, nb);
+                                i += nb;
                             }
-                            if (e < nd) {
-                                err = lane_val(kind, (int)e);
-                                S.k = lane_val(kq, (int)e);
-                            } else {
-                                if (nd)
-                                    S.k = lane_val(kq + ni, (int)nd - 1);
-                            }
-                            i += nd;
                         }
                         b.cur = __builtin_amdgcn_readlane(cur, 0);
 #ifdef ZSK_TUNING
@@ -2848,12 +2928,13 @@ __device__ __forceinline__ void seq_body(
                 replay(span_rsrc(comp, s0, s1 - s0), s0, irsrc(i0, i1), i0);
         }
     }
-    if (ONE && lane != 0)
+    if (ONE && threadIdx.x != 0)
         return;
 #ifdef ZSK_TUNING
     if (ONE) {
         atomicAdd(&g_sdiag[0], (unsigned long long)(__builtin_readcyclecounter() - tk0));
         atomicAdd(&g_sdiag[1], (unsigned long long)tloop);
+        atomicAdd(&g_sdiag[5], (unsigned long long)tchain);
         atomicAdd(&g_sdiag[2], (unsigned long long)nseqs);
         atomicAdd(&g_sdiag[3], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - rt0));
         atomicAdd(&g_sdiag[4], 1ull);
@@ -2909,10 +2990,10 @@ __global__ __launch_bounds__(kHufOneT) void zstd_one_kernel(
     __shared__ uint32_t last;
     const uint32_t b = blockIdx.x, t = threadIdx.x;
     if (b < m) {
-        if (t >= 64)
-            return;
-        seq_body<1, 0, 0, true>(U.s, b, desc, n, comp, ops, blk_base, slots, stop, rec_base, items, nitems, status,
-                                ck, fail_at, f0);
+        // (waves 0 and 1: the replay's chain and its vector phase)
+        if (t < 128)
+            seq_body<1, 0, 0, true, true>(U.s, b, desc, n, comp, ops, blk_base, slots, stop, rec_base, items, nitems,
+                                          status, ck, fail_at, f0);
     } else {
         huf_one_body(U.h, b - m, t, jobs, comp, slots, lit, hbad);
     }
@@ -3374,8 +3455,9 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
                 const double fr = z[4] ? (double)z[4] : 1.0, sq = z[2] ? (double)z[2] : 1.0;
                 fprintf(stderr,
                         "one-frame sequences: kernel %.0f cycles (%.1f us, %.0f MHz) per frame, loop %.0f cycles "
-                        "(%.0f per sequence, %.0f sequences per frame)\n",
-                        z[0] / fr, z[3] / fr / 100.0, z[3] ? z[0] * 100.0 / z[3] : 0.0, z[1] / fr, z[1] / sq, sq / fr);
+                        "(%.0f per sequence, chain alone %.0f, %.0f sequences per frame)\n",
+                        z[0] / fr, z[3] / fr / 100.0, z[3] ? z[0] * 100.0 / z[3] : 0.0, z[1] / fr, z[1] / sq,
+                        z[5] / sq, sq / fr);
             }
 #endif
             continue;
