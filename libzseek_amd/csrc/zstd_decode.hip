@@ -260,21 +260,21 @@ __device__ __forceinline__ uint32_t read_ncount(ZLds &L, uint32_t wofs, uint32_t
         pos += lo ? nbits - 1 : nbits;
         count--;
         remaining -= count < 0 ? -count : count;
-        if (count && lane_id() == 0)
-            *lp<int16_t>(&L.norm[sym]) = (int16_t)count;
+        // (every lane, the same value: no exec-mask branch; a zero count
+        // writes the zero norm_clear left)
+        *lp<int16_t>(&L.norm[sym]) = (int16_t)count;
         sym++;
         prev0 = count == 0;
         // FSE_readNCount's `while (remaining < threshold) { nbBits--;
         // threshold >>= 1; }`: remaining stays >= 1 (a count never exceeds
         // it), so the field width becomes min(nbits, log2(remaining) + 1)
         nbits = min(nbits, 32u - (uint32_t)__builtin_clz((uint32_t)remaining));
-        if (pos > 8 * 256) {   // ran off the window: no valid description is that long
-            *err = ZE_CORRUPT;
-            return 0;
-        }
     }
+    // (ran off the window -- no valid description is that long -- checked
+    // once here: past it the walk reads zeros, the loop ends within max_sym
+    // symbols and the description is refused as before)
     const uint32_t used = (pos + 7) / 8 - wofs;
-    if (remaining != 1 || used > avail) {
+    if (pos > 8 * 256 || remaining != 1 || used > avail) {
         *err = ZE_CORRUPT;
         return 0;
     }
