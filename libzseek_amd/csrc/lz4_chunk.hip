@@ -293,11 +293,13 @@ __device__ __forceinline__ int32_t emit_range(const Src &S, Win &W, const Blk &B
 // lane's total through pass 2 minus the record at its entry -- no count pass
 // (a lane whose entry is past its records counts as before).
 constexpr uint32_t kRec = 64;
-// The one-frame route parses over all kOneWaves waves of its workgroup: lane
-// j of 256 takes chunk j (at least kOneMinChunk bytes), kOneRec records each
-constexpr uint32_t kOneLanes = 256;
-constexpr uint32_t kOneMinChunk = 128;
-constexpr uint32_t kOneRec = 32;
+// The one-frame route parses over all OW waves of its workgroup: lane j of
+// 64 OW takes chunk j (at least 32 KiB / (64 OW) bytes), 8192 / (64 OW)
+// records each (OW 4: 128-byte chunks, 32 records; OW 8: 64 and 16)
+template <uint32_t OW>
+constexpr uint32_t one_min_chunk() { return 32768 / (64 * OW); }
+template <uint32_t OW>
+constexpr uint32_t one_rec() { return 8192 / (64 * OW); }
 constexpr uint32_t kOneMapW = 4;   // map dwords per lane: a 128-bit chunk prefix
 
 #ifdef ZSK_TUNING
@@ -329,21 +331,22 @@ __device__ unsigned long long g_ctime[16];
 // ONE: the workgroup's kOneLanes lanes (lane = thread index) take the block,
 // the wave-wide steps (owners, scans, the first failure) going through LDS
 // scratch at `coll` (3 x 256 + 16 words) with workgroup barriers.
-template <bool ONE, int KS = 0>
+template <bool ONE, int KS = 0, uint32_t OW = 4>
 __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane, uint32_t mapbase,
                                uint64_t *it, uint32_t &k, uint32_t cap, uint32_t &op, uint32_t recbase,
                                uint32_t coll, uint32_t lead)
 {
-    constexpr uint32_t NL = ONE ? kOneLanes : 64;
-    constexpr uint32_t kR = ONE ? kOneRec : kRec;
+    constexpr uint32_t NL = ONE ? 64 * OW : 64;
+    constexpr uint32_t kR = ONE ? one_rec<OW>() : kRec;
+    constexpr int LG = ONE ? (OW == 8 ? 9 : 8) : 6;   // log2 NL
     const uint32_t bsize = B.iend - B.ib;
     // chunking: C bytes per lane (>= the minimum chunk), nl lanes
     uint32_t C = (bsize + NL - 1) / NL;
-    C = C < (ONE ? kOneMinChunk : kMinChunk) ? (ONE ? kOneMinChunk : kMinChunk) : (C + 3) & ~3u;
+    C = C < (ONE ? one_min_chunk<OW>() : kMinChunk) ? (ONE ? one_min_chunk<OW>() : kMinChunk) : (C + 3) & ~3u;
     const uint32_t nl = (bsize + C - 1) / C;
     // LDS scratch of the ONE route's workgroup steps
     auto cw = [&](uint32_t i) { return lp<uint32_t>(coll + 4 * i); };   // word i
-    constexpr uint32_t cY = 0, cN = 256, cE = 512, cWS = 768, cM = 776, cBad = 777, cFirst = 778;
+    constexpr uint32_t cY = 0, cN = NL, cE = 2 * NL, cWS = 3 * NL, cM = cWS + 8, cBad = cM + 1, cFirst = cM + 2;
     auto sync = [&]() {
         if constexpr (ONE)
             __syncthreads();
@@ -493,9 +496,9 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
                 // chain at distance d marks the lane at d + 2^r, top bit
                 // first, so every distance is reached; then each chain lane
                 // gives its successor the entry it stopped at
-                uint32_t J[8];
+                uint32_t J[LG];
                 J[0] = nxt;
-                for (int r = 1; r < 8; r++) {
+                for (int r = 1; r < LG; r++) {
                     *cw(cE + lane) = J[r - 1];
                     __syncthreads();
                     J[r] = J[r - 1] < NL ? *cw(cE + J[r - 1]) : NL;
@@ -503,7 +506,7 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
                 }
                 *cw(cE + lane) = lane == 0 ? 1u : 0u;   // on the chain
                 __syncthreads();
-                for (int r = 7; r >= 0; r--) {
+                for (int r = LG - 1; r >= 0; r--) {
                     const bool on = *cw(cE + lane) != 0;
                     __syncthreads();
                     if (on && J[r] < NL)
@@ -620,11 +623,11 @@ __device__ __forceinline__ uint32_t hdr_xxh32(const Src &S, Win &W, uint32_t n)
 // bytes the window reads, zeros past the resource), then wave 0 parses it
 // with every read an LDS round trip instead of an HBM / L2 one.  A frame too
 // big for the stage is parsed through the window as usual.
-constexpr uint32_t kOneWaves = 4;
 constexpr uint32_t kOneStage = 65536 + 1024;   // bytes: frames of <= kOneStage - 64 compressed
+constexpr uint32_t kWinQ = 4;                  // window: 16-byte pieces per lane
 
-template <bool ONE>
-__global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel(
+template <bool ONE, uint32_t OW = 4>
+__global__ __launch_bounds__(64 * (ONE ? OW : kCW)) void lz4_chunk_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
     const uint64_t *__restrict__ rec_base, uint64_t capacity, uint64_t *__restrict__ items,
     uint32_t *__restrict__ nitems, int32_t *__restrict__ status, uint32_t *__restrict__ fail_at,
@@ -632,11 +635,17 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
     const BlockJob *__restrict__ jobs, const BlockRes *__restrict__ jres, const uint32_t *__restrict__ njobs,
     uint32_t min_jobs, uint64_t *__restrict__ solo_total, uint32_t per_wave, uint32_t lead)
 {
+    constexpr uint32_t kOneWaves = OW;
+    constexpr uint32_t kOneLanes = 64 * OW;
+    // (ONE: the staged frame and the window share LDS -- a frame reads one
+    // or the other)
+    constexpr uint32_t nsw = ONE ? (kOneStage / 16 > kOneLanes * kWinQ ? kOneStage / 16 : kOneLanes * kWinQ)
+                                 : kCW * 64 * kWinQ;
     __shared__ __attribute__((aligned(16))) uint32_t maps[ONE ? kOneLanes * kOneMapW : kCW * 64 * kMapW];
-    __shared__ __attribute__((aligned(16))) u32x4 wins[kCW * 64 * 4];
-    __shared__ __attribute__((aligned(16))) u32x4 stage[ONE ? kOneStage / 16 : 1];
-    __shared__ __attribute__((aligned(16))) uint64_t recs[ONE ? kOneLanes * kOneRec : 1];
-    __shared__ uint32_t coll[ONE ? 3 * 256 + 16 : 1];
+    __shared__ __attribute__((aligned(16))) u32x4 stw[nsw];
+    __shared__ __attribute__((aligned(16))) uint64_t recs[ONE ? kOneLanes * one_rec<OW>() : 1];
+    __shared__ uint32_t coll[ONE ? 3 * kOneLanes + 16 : 1];
+    u32x4 *const stage = stw, *const wins = stw;
     const uint32_t lane = ONE ? threadIdx.x : threadIdx.x & 63;   // ONE: the workgroup's lanes
     const uint32_t w = ONE ? 0 : threadIdx.x >> 6;
     // one frame (wave-uniform f); a return ends that frame
@@ -851,10 +860,10 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
             // (ONE: a staged frame's parse without the staged test per read)
             const int32_t bs =
                 ONE && S.staged
-                    ? chunk_block<ONE, 1>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
-                                          (uint32_t)(uintptr_t)coll, lead)
-                    : chunk_block<ONE, 0>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
-                                          (uint32_t)(uintptr_t)coll, lead);
+                    ? chunk_block<ONE, 1, OW>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
+                                              (uint32_t)(uintptr_t)coll, lead)
+                    : chunk_block<ONE, 0, OW>(S, W, B, lane, mapbase, it, k, cap, op, (uint32_t)(uintptr_t)recs,
+                                              (uint32_t)(uintptr_t)coll, lead);
             if (bs == ST_BLOCK_ERR)
                 st = block_fail(B, bsid, max_block);
             else if (bs >= 0)
@@ -895,6 +904,21 @@ __global__ __launch_bounds__(64 * (ONE ? kOneWaves : kCW)) void lz4_chunk_kernel
 // the one-frame parse's lead-in (bytes before each chunk): env ZSEEK_ONE_LEAD
 // (tuning), default kOneLead
 constexpr uint32_t kOneLead = 64;
+// the one-frame parse's waves: 8 (64-byte chunks), or 4 (128-byte chunks,
+// the round-4 shape) under env ZSEEK_ONE_WAVES=4.  Per frame (tuning timers,
+// 64 KiB frames, lead 64): 119.8K cycles at 4 waves, 108.9K at 8 (pass 1
+// 27.5K -> 24.4K, emit 33.5K -> 22.8K), 106.8K at 16 (each step slower:
+// pass 2 + owners stays ~35K) -- not kept
+constexpr uint32_t kOneWavesDef = 8;
+static uint32_t one_waves()
+{
+    static const uint32_t v = [] {
+        const char *e = getenv("ZSEEK_ONE_WAVES");
+        return e && atoi(e) == 4 ? 4u : kOneWavesDef;
+    }();
+    return v;
+}
+
 uint32_t one_lead()
 {
     static const uint32_t v = [] {
@@ -912,10 +936,16 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     if (nframes == 0)
         return 0;
     if (one) {
-        hipLaunchKernelGGL(lz4_chunk_kernel<true>, dim3(nframes), dim3(64 * kOneWaves), 0, stream, d_desc, nframes,
-                           d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u,
-                           one_lead());
+        if (one_waves() == 8)
+            hipLaunchKernelGGL((lz4_chunk_kernel<true, 8>), dim3(nframes), dim3(64 * 8), 0, stream, d_desc, nframes,
+                               d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
+                               nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u,
+                               one_lead());
+        else
+            hipLaunchKernelGGL((lz4_chunk_kernel<true, 4>), dim3(nframes), dim3(64 * 4), 0, stream, d_desc, nframes,
+                               d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
+                               nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u,
+                               one_lead());
 #ifdef ZSK_TUNING
         if (getenv("ZSEEK_CHUNK_TIMERS")) {
             unsigned long long z[16];

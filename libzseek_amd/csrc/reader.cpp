@@ -593,6 +593,8 @@ bool finish(LaneJob &J, Slot &s)
         g_ht[5] += ht_now() - t_queued;
     const uint64_t ht2 = ht_now();
 #endif
+    // (hipEventSynchronize: polling hipEventQuery instead for a small batch
+    // measured no better, LZ4 4 KiB p50 85.6-86.2 against 83.5-84.4 us)
     hipError_t e = hipEventSynchronize(s.done);
 #ifdef ZSK_TUNING
     g_ht[2] += ht_now() - ht2;
