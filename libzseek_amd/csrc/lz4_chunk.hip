@@ -446,6 +446,11 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
             }
         }
         y = p;
+#ifdef ZSK_TUNING
+        if (ONE)
+            __syncthreads();
+        ZSK_CT(11)
+#endif
         // owners: lane j's successor is the lane whose chunk holds y_j
         const uint32_t nxt = act ? (y >= B.iend ? NL : (y - B.ib) / C) : NL;
         if constexpr (!ONE) {
@@ -491,6 +496,10 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
             if (*cw(cBad) == 0 && m < NL) {
                 entry = lane <= m ? (lane == 0 ? B.ib : *cw(cY + lane - 1)) : kNone;
             } else {
+#ifdef ZSK_TUNING
+                if (lane == 0)
+                    atomicAdd(&g_ctime[13], 1ull);
+#endif
                 // the owner chain from lane 0 by pointer jumping (successors
                 // only increase): J_r = 2^r successor steps; a lane on the
                 // chain at distance d marks the lane at d + 2^r, top bit
@@ -961,9 +970,10 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                 const double nf = (double)calls, nb = (double)(acc[12] ? acc[12] : 1);
                 fprintf(stderr,
                         "chunk one-route cycles per frame: stage %.0f hdr %.0f pass1 %.0f pass2+own %.0f count %.0f "
-                        "emit %.0f total %.0f | per block wave-max iters: pass1 %.1f pass2 %.1f (%d frames)\n",
-                        acc[0] / nf, acc[1] / nf, acc[2] / nf, acc[3] / nf, acc[4] / nf, acc[5] / nf, acc[7] / nf,
-                        acc[8] / nb, acc[9] / nb, calls);
+                        "emit %.0f total %.0f | per block wave-max iters: pass1 %.1f pass2 %.1f (%d frames) | pass2 "
+                        "alone %.0f, owner jumps in %.2f of blocks\n",
+                        acc[0] / nf, acc[1] / nf, acc[2] / nf, acc[3] / nf + acc[11] / nf, acc[4] / nf, acc[5] / nf,
+                        acc[7] / nf, acc[8] / nb, acc[9] / nb, calls, acc[11] / nf, acc[13] / nb);
             }
         }
 #endif
