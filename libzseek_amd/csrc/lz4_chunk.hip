@@ -579,6 +579,19 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
     ZSK_CN(9, n2_)
     if (ONE && lane == 0)
         atomicAdd(&g_ctime[12], 1ull);
+    if constexpr (ONE) {   // the workgroup-max iterations of passes 1 and 2
+        __shared__ uint32_t wmax_[2];
+        if (lane == 0)
+            wmax_[0] = wmax_[1] = 0;
+        __syncthreads();
+        atomicMax(&wmax_[0], n1_);
+        atomicMax(&wmax_[1], n2_);
+        __syncthreads();
+        if (lane == 0) {
+            atomicAdd(&g_ctime[14], (unsigned long long)wmax_[0]);
+            atomicAdd(&g_ctime[15], (unsigned long long)wmax_[1]);
+        }
+    }
 #endif
     if constexpr (!ONE) {
         const uint64_t fails = __ballot(st >= 0);
@@ -971,9 +984,10 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                 fprintf(stderr,
                         "chunk one-route cycles per frame: stage %.0f hdr %.0f pass1 %.0f pass2+own %.0f count %.0f "
                         "emit %.0f total %.0f | per block wave-max iters: pass1 %.1f pass2 %.1f (%d frames) | pass2 "
-                        "alone %.0f, owner jumps in %.2f of blocks\n",
+                        "alone %.0f, owner jumps in %.2f of blocks, workgroup-max iters pass1 %.1f pass2 %.1f\n",
                         acc[0] / nf, acc[1] / nf, acc[2] / nf, acc[3] / nf + acc[11] / nf, acc[4] / nf, acc[5] / nf,
-                        acc[7] / nf, acc[8] / nb, acc[9] / nb, calls, acc[11] / nf, acc[13] / nb);
+                        acc[7] / nf, acc[8] / nb, acc[9] / nb, calls, acc[11] / nf, acc[13] / nb, acc[14] / nb,
+                        acc[15] / nb);
             }
         }
 #endif
