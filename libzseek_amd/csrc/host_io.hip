@@ -28,9 +28,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kUpT = 256;   // threads per workgroup
 // 16-byte pieces per thread: one -- a ~32 KB upload spread over 8
-// workgroups (8 CUs' load paths to the host) takes 5.2 us, against 7.6 us
-// with four pieces per thread over 2 workgroups (64 x 1 over 32: 3.6 us of
-// kernel, no better per request)
+// workgroups (8 CUs' load paths to the host) takes 3.3 us (median over a
+// latency trace; 5.2 us average), against 7.6 us with four pieces per thread
+// over 2 workgroups (64 x 1 over 32: 3.6 us average, no better per request)
 constexpr uint32_t kUpV = 1;
 
 template <uint32_t T, uint32_t V>
