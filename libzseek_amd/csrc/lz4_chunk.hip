@@ -428,7 +428,9 @@ __device__ int32_t chunk_block(const Src &S, Win &W, const Blk &B, uint32_t lane
         // pass 2: continue to the first position another lane visited (the
         // chunk by a reciprocal multiply, not a division; the map word and
         // the token read together, one round trip)
-        const uint32_t mC = (uint32_t)((0x100000000ull + C - 1) / C);
+        // (ceil(2^32 / C) for C >= 2, in 32 bits: a 64-bit quotient made
+        // the loop's multiply a 64-bit one)
+        const uint32_t mC = 0xFFFFFFFFu / C + 1u;
         if (act) {
             while (p < B.iend) {
                 const uint32_t x = p - B.ib;
