@@ -813,7 +813,7 @@ def end_to_end(z, img, size):
             if got.value != size:
                 return {"error": f"short read {got.value}"}
             best = max(best, got.value / secs / 1e9)
-        L.zsk_reader_gpu_stats(r, C.byref(gs))
+        L.zsk_reader_gpu_stats_ex(r, C.byref(gs), C.sizeof(gs))
         T.zsk_tool_close_mem(C.cast(L.zseek_reader_close, C.c_void_p), r)
         res["GBps" if io == 1 else f"GBps_io{io}"] = round(best, 2)
         # host threads the read ran on: the copy / pread pool (usable CPUs - 2)

@@ -153,7 +153,11 @@ ZSEEK_EXPORT ssize_t zsk_pread_device(zseek_reader_t *reader, void *d_buf,
     size_t count, size_t offset, void *call_data,
     char errbuf[ZSEEK_ERRBUF_SIZE]);
 
-/* GPU-side counters of a reader. */
+/* GPU-side counters of a reader.  zsk_reader_gpu_stats fills the fields
+ * through `device` (the struct's layout before copy_threads / io_parts were
+ * added, so a caller built against that header is never written past its
+ * struct); zsk_reader_gpu_stats_ex(reader, stats, sizeof *stats) fills the
+ * first @size bytes of the current layout (at most its size). */
 typedef struct {
     uint64_t batches;          /* decode grids launched                 */
     uint64_t frames_decoded;   /* frames decoded on the GPU             */
@@ -167,6 +171,8 @@ typedef struct {
 
 ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader,
     zsk_gpu_stats_t *stats);
+ZSEEK_EXPORT bool zsk_reader_gpu_stats_ex(zseek_reader_t *reader,
+    zsk_gpu_stats_t *stats, size_t size);
 
 /* Largest decoded span one batch grid covers (bytes, default 64 MiB; env
  * ZSEEK_HIP_BATCH_BYTES overrides at open).  A read runs as a pipeline of

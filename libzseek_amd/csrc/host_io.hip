@@ -56,9 +56,10 @@ __global__ __launch_bounds__(T) void h2d_small_kernel(const u32x4 *__restrict__ 
 // The batch's download in one kernel: the status words (aligned u32s) and
 // the request's bytes [src, src + len) -- src at any byte, dst 16-aligned --
 // written straight into pinned host memory through its device mapping.
-// Each thread builds 16 bytes from five aligned dwords (v_alignbyte); reads
-// up to 4 bytes past src + len and writes up to 15 past dst + len (both
-// buffers' slack).
+// Each thread builds 16 bytes from five aligned dwords (v_alignbyte): the
+// last thread's 20 bytes start at most 15 bytes before src + len rounded down
+// to a dword, so it reads up to 19 bytes past src + len, and it writes up to
+// 15 past dst + len (both buffers' slack: grow_dev / grow_host add 256).
 __global__ __launch_bounds__(kUpT) void d2h_small_kernel(uint32_t *__restrict__ hst, const uint32_t *__restrict__ dst_,
                                                          uint32_t nst, u32x4 *__restrict__ hout,
                                                          const uint8_t *__restrict__ src, uint32_t len)

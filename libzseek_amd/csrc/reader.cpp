@@ -519,7 +519,7 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
                                             (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs, s.stream, d_fail,
                                             stop_last)
                             : zstd_decode_frames(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, &s.zs,
-                                                 s.stream, d_fail)) != 0)
+                                                 s.stream, d_fail, stop_last)) != 0)
         e = hipErrorLaunchFailure;
     if (e == hipSuccess && r->type == ZSEEK_LZ4) {
         if (lz4_pick_engine((uint32_t)n) == ENGINE_WAVE) {
@@ -1077,23 +1077,37 @@ extern "C" ZSEEK_EXPORT ssize_t zsk_pread_device(zseek_reader_t *reader, void *d
     return pread_frames(reader, d_buf, count, offset, call_data, errbuf, true);
 }
 
+// Writes the first `size` bytes of the counters (at most sizeof): a caller
+// built against an older, shorter zsk_gpu_stats_t gets exactly its fields.
+extern "C" ZSEEK_EXPORT bool zsk_reader_gpu_stats_ex(zseek_reader_t *reader, zsk_gpu_stats_t *out, size_t size)
+{
+    if (!reader || !out || size == 0)
+        return false;
+    zsk_gpu_stats_t s;
+    memset(&s, 0, sizeof(s));
+    {
+        std::unique_lock<std::shared_mutex> guard(reader->lock);
+        s.device = reader->lanes.empty() ? -1 : reader->lanes[0]->device;
+        s.copy_threads = copy_pool_threads();
+        s.io_parts = io_parts(reader);
+        for (auto &l : reader->lanes) {
+            s.batches += l->batches;
+            s.frames_decoded += l->frames_decoded;
+            s.bytes_decoded += l->bytes_decoded;
+            s.bytes_uploaded += l->bytes_uploaded;
+            s.device_memory += l->device_bytes();
+        }
+    }
+    memcpy(out, &s, size < sizeof(s) ? size : sizeof(s));
+    return true;
+}
+
+// The round-4 layout (through `device`): what callers of this entry point
+// were built with before copy_threads / io_parts were added;
+// zsk_reader_gpu_stats_ex returns the whole struct.
 extern "C" ZSEEK_EXPORT bool zsk_reader_gpu_stats(zseek_reader_t *reader, zsk_gpu_stats_t *s)
 {
-    if (!reader || !s)
-        return false;
-    std::unique_lock<std::shared_mutex> guard(reader->lock);
-    memset(s, 0, sizeof(*s));
-    s->device = reader->lanes.empty() ? -1 : reader->lanes[0]->device;
-    s->copy_threads = copy_pool_threads();
-    s->io_parts = io_parts(reader);
-    for (auto &l : reader->lanes) {
-        s->batches += l->batches;
-        s->frames_decoded += l->frames_decoded;
-        s->bytes_decoded += l->bytes_decoded;
-        s->bytes_uploaded += l->bytes_uploaded;
-        s->device_memory += l->device_bytes();
-    }
-    return true;
+    return zsk_reader_gpu_stats_ex(reader, s, offsetof(zsk_gpu_stats_t, copy_threads));
 }
 
 extern "C" ZSEEK_EXPORT bool zsk_reader_set_batch_bytes(zseek_reader_t *reader, size_t bytes)

@@ -290,16 +290,16 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 constexpr size_t kUploadSmallMax = 512u << 10;
 int upload_small(void *d_dst, const void *h_src, const void *h_src_dev, size_t bytes, hipStream_t stream);
 // ... and the download: nst status words d_status -> h_status, then len bytes
-// d_src (any alignment, 4 readable bytes past the end) -> h_out (pinned,
+// d_src (any alignment, 19 readable bytes past the end) -> h_out (pinned,
 // 16-aligned, 15 writable bytes of slack) as one kernel when len <=
 // kDownloadSmallMax, else two hipMemcpyAsync.  0 or -1.
 constexpr size_t kDownloadSmallMax = 256u << 10;
 int download_small(uint32_t *h_status, void *h_status_dev, const uint32_t *d_status, uint32_t nst, uint8_t *h_out,
                    void *h_out_dev, const uint8_t *d_src, size_t len, hipStream_t stream);
-// plan + synchronize + reserve + decode
+// plan + synchronize + reserve + decode (stop_last as launch_zstd_decode)
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
-                       uint32_t *d_fail_at = nullptr);
+                       uint32_t *d_fail_at = nullptr, uint32_t stop_last = 0xFFFFFFFFu);
 // The same for a request's few frames whose compressed bytes are also in host
 // memory (h_desc / h_comp: the reader's pinned upload, the same layout as
 // d_desc / d_comp): the plan -- zstd_plan_kernel's per-frame bounds, the scans,

@@ -2990,10 +2990,15 @@ __global__ __launch_bounds__(kHufOneT) void zstd_one_kernel(
     __shared__ uint32_t last;
     const uint32_t b = blockIdx.x, t = threadIdx.x;
     if (b < m) {
-        // (waves 0 and 1: the replay's chain and its vector phase)
-        if (t < 128)
-            seq_body<1, 0, 0, true, true>(U.s, b, desc, n, comp, ops, blk_base, slots, stop, rec_base, items, nitems,
-                                          status, ck, fail_at, f0);
+        // waves 0 and 1: the replay's chain and its vector phase.  Waves 2
+        // and 3 leave before any barrier: a wave that has ended no longer
+        // counts at s_barrier (CDNA), so seq_body's data-dependent barriers
+        // and the two below are met by waves 0 and 1 alone, and no wave
+        // reads `last` before thread 0 has written it.
+        if (t >= 128)
+            return;
+        seq_body<1, 0, 0, true, true>(U.s, b, desc, n, comp, ops, blk_base, slots, stop, rec_base, items, nitems,
+                                      status, ck, fail_at, f0);
     } else {
         huf_one_body(U.h, b - m, t, jobs, comp, slots, lit, hbad);
     }
@@ -3596,7 +3601,7 @@ int launch_zstd_decode(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
 // frame are only known once its block headers and sequence counts are read.
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,
-                       uint32_t *d_fail_at)
+                       uint32_t *d_fail_at, uint32_t stop_last)
 {
     if (nframes == 0)
         return 0;
@@ -3611,7 +3616,7 @@ int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t 
         return -1;
     if (zstd_scratch_reserve(s, nframes, s->total[1], s->total[0], s->total[2], stream) != 0)
         return -1;
-    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+    return launch_zstd_decode(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last);
 }
 
 // zstd_plan_kernel's per-frame bound on the host: item slots (8 + 4 per
@@ -3707,7 +3712,7 @@ int zstd_decode_frames_planned(const ZstdHostPlan &P, const uint64_t *d_plan, co
     if (nframes == 0)
         return 0;
     if (nframes > kOneMaxFrames || zstd_chunks(nframes) != 1)
-        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last);
     (void)hipGetLastError();   // a stale error of an earlier call is not this launch's
     stage_mark(0, stream);
     if (zstd_scratch_reserve(s, nframes, P.extent, P.items, P.blocks, stream) != 0)
@@ -3738,7 +3743,7 @@ int zstd_decode_frames_host(const FrameDesc *h_desc, const uint8_t *h_comp, cons
     if (nframes == 0)
         return 0;
     if (nframes > kOneMaxFrames || zstd_chunks(nframes) != 1)
-        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at);
+        return zstd_decode_frames(d_desc, nframes, d_comp, d_out, d_status, s, stream, d_fail_at, stop_last);
     if (2ull * (nframes + 1) > s->h_plan_cap) {
         if (s->h_plan)
             (void)hipHostFree(s->h_plan);

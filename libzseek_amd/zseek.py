@@ -99,7 +99,7 @@ EXPORTED = [
     "zseek_pread", "zseek_read", "zseek_reader_stats",
     "zsk_lz4_decode_frames", "zsk_lz4_decode_frames_ex", "zsk_status_string", "zsk_lz4_kernel_name",
     "zsk_lz4_parse_kernel_name", "zsk_reader_frames", "zsk_reader_type",
-    "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_set_batch_bytes",
+    "zsk_pread_device", "zsk_reader_gpu_stats", "zsk_reader_gpu_stats_ex", "zsk_reader_set_batch_bytes",
     "zsk_kernel_timing", "zsk_kernel_times", "zsk_zstd_decode_frames",
     "zsk_verify_frame_checksums", "zsk_reader_set_verify_checksums",
     "zsk_reader_set_devices", "zsk_reader_devices", "zsk_reader_set_io_threads",
@@ -167,6 +167,8 @@ def lib() -> C.CDLL:
                                    C.c_char_p]
     L.zsk_reader_gpu_stats.restype = C.c_bool
     L.zsk_reader_gpu_stats.argtypes = [C.c_void_p, C.POINTER(GpuStatsC)]
+    L.zsk_reader_gpu_stats_ex.restype = C.c_bool
+    L.zsk_reader_gpu_stats_ex.argtypes = [C.c_void_p, C.POINTER(GpuStatsC), C.c_size_t]
     L.zsk_reader_set_batch_bytes.restype = C.c_bool
     L.zsk_reader_set_batch_bytes.argtypes = [C.c_void_p, C.c_size_t]
     L.zsk_verify_frame_checksums.restype = C.c_int
@@ -454,7 +456,7 @@ class Reader:
 
     def gpu_stats(self) -> dict:
         s = GpuStatsC()
-        lib().zsk_reader_gpu_stats(self._h, C.byref(s))
+        lib().zsk_reader_gpu_stats_ex(self._h, C.byref(s), C.sizeof(s))
         return {k: getattr(s, k) for k, _ in GpuStatsC._fields_}
 
     def frames(self):

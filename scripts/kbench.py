@@ -63,7 +63,7 @@ def main():
     print(f"input {args.input} {args.size >> 20} MiB, {n} frames, comp {b.comp_end / 1e9:.3f} GB "
           f"({time.time() - t0:.1f}s)", flush=True)
     stream = torch.cuda.current_stream()
-    variants = [int(v) for v in args.variants.split(",")]
+    variants = [int(v, 0) for v in args.variants.split(",")]
     res = {v: [] for v in variants}
 
     def launch(v):

@@ -443,3 +443,27 @@ def test_checksum_table_read_by_reference(zs, oracle, ref):
         assert got == 1000 and b == data[70000:71000].tobytes()
     finally:
         r.close()
+
+
+def test_gpu_stats_respects_caller_struct_size(zs):
+    """zsk_reader_gpu_stats writes only the round-4 layout (through
+    `device`), so a caller built against the shorter struct is never written
+    past it; zsk_reader_gpu_stats_ex writes exactly the bytes it is given."""
+    import ctypes as C
+    L = zs.lib()
+    full = C.sizeof(zs.GpuStatsC)
+    old = zs.GpuStatsC.copy_threads.offset
+    with zs.Reader(golden_file("lz4_64k_direct"), 1) as r:
+        buf = (C.c_uint8 * (full + 16))(*([0xAB] * (full + 16)))
+        assert L.zsk_reader_gpu_stats(r._h, C.cast(buf, C.POINTER(zs.GpuStatsC)))
+        assert bytes(buf[old:]) == b"\xab" * (full + 16 - old)
+        assert int.from_bytes(bytes(buf[old - 4:old]), "little", signed=True) == -1   # device: no lane yet
+        buf = (C.c_uint8 * (full + 16))(*([0xAB] * (full + 16)))
+        assert L.zsk_reader_gpu_stats_ex(r._h, C.cast(buf, C.POINTER(zs.GpuStatsC)), full)
+        assert bytes(buf[full:]) == b"\xab" * 16
+        s = zs.GpuStatsC.from_buffer(buf)
+        assert s.copy_threads >= 2 and s.io_parts >= 1
+        buf = (C.c_uint8 * 8)(*([0xAB] * 8))
+        assert L.zsk_reader_gpu_stats_ex(r._h, C.cast(buf, C.POINTER(zs.GpuStatsC)), 4)
+        assert bytes(buf[4:]) == b"\xab" * 4
+        assert not L.zsk_reader_gpu_stats_ex(r._h, C.cast(buf, C.POINTER(zs.GpuStatsC)), 0)

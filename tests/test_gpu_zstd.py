@@ -499,3 +499,47 @@ def test_zstd_content_checksum_like_reference(gpu, zs, zstd, ref, cache):
         finally:
             ours.close()
             theirs.close()
+
+
+@pytest.mark.parametrize("cache", [0, 1])
+def test_zstd_content_checksum_many_frames_like_reference(gpu, zs, zstd, ref, cache):
+    """a request over more than kOneMaxFrames (64) frames takes the
+    device-planned path (zstd_decode_frames), which now passes the no-cache
+    stop too: a read ending inside a frame whose content checksum is wrong
+    returns the reference's bytes (libzstd's streaming decoder stops before the
+    checksum), one running to that frame's end its error."""
+    n, fs = 80, 16384
+    data = zs.synth_buffer(n * fs).tobytes()
+    frames = [compress(zstd, data[i * fs:(i + 1) * fs], {P_LEVEL: 3, P_CHECKSUM: 1}) for i in range(n)]
+    bad = bytearray(frames[75])
+    bad[-1] ^= 0x5A
+    frames[75] = bytes(bad)
+    img = _seekable(frames, [fs] * n)
+    queries = [(75 * fs + 100, 0), (70 * fs + 5000, 5 * fs), (76 * fs, 0), (fs * 74 - 3, fs + 7)]
+    for count, off in queries:
+        ours = zs.Reader(np.frombuffer(img, np.uint8), cache)
+        theirs = ref.open(img, cache)
+        try:
+            got, err = b"", None
+            while len(got) < count:
+                try:
+                    b = ours.pread(count - len(got), off + len(got))
+                except zs.ZseekError as e:
+                    err = str(e)
+                    break
+                if not b:
+                    break
+                got += b
+            want, werr = b"", None
+            while len(want) < count:
+                rc, b = theirs.pread(count - len(want), off + len(want))
+                if rc < 0:
+                    werr = theirs.error
+                    break
+                if rc == 0:
+                    break
+                want += b
+            assert (got, err) == (want, werr), (count, off)
+        finally:
+            ours.close()
+            theirs.close()
