@@ -543,3 +543,93 @@ def test_zstd_content_checksum_many_frames_like_reference(gpu, zs, zstd, ref, ca
         finally:
             ours.close()
             theirs.close()
+
+
+def _literal_sections(frame: bytes):
+    """[start, end) of every compressed block's literals section in one zstd
+    frame (frame header, block headers and literals headers as RFC 8878
+    lays them out)"""
+    B = lambda p: frame[p] if p < len(frame) else 0   # noqa: E731
+    fhd = B(4)
+    fcs, single, did = fhd >> 6, (fhd >> 5) & 1, fhd & 3
+    ip = 5 + (0 if single else 1) + (4 if did == 3 else did) + (single if fcs == 0 else (2, 4, 8)[fcs - 1])
+    out = []
+    while ip + 3 <= len(frame):
+        bh = B(ip) | B(ip + 1) << 8 | B(ip + 2) << 16
+        typ, size = (bh >> 1) & 3, bh >> 3
+        ip += 3
+        if typ == 2:
+            b0 = B(ip)
+            lt, sf = b0 & 3, (b0 >> 2) & 3
+            if lt <= 1:
+                lh = 2 if sf == 1 else 3 if sf == 3 else 1
+                sz = ((b0 | B(ip + 1) << 8) >> 4) if sf == 1 else \
+                    ((b0 | B(ip + 1) << 8 | B(ip + 2) << 16) >> 4) if sf == 3 else b0 >> 3
+                sec = lh + (sz if lt == 0 else 1)
+            else:
+                lhc = b0 | B(ip + 1) << 8 | B(ip + 2) << 16 | B(ip + 3) << 24
+                sec = (3 + ((lhc >> 14) & 0x3FF)) if sf <= 1 else (4 + (lhc >> 18)) if sf == 2 else \
+                    (5 + (lhc >> 22) + (B(ip + 4) << 10))
+            out.append((ip, ip + min(sec, size)))
+        ip += 1 if typ == 1 else size
+        if bh & 1:
+            break
+    return out
+
+
+@pytest.mark.parametrize("batch", [0, 40])
+def test_device_zstd_x2_corruption_sweep(gpu, zs, oracle, zstd, batch):
+    """verdict r05 item 5: >= 1,000 single-byte corruptions inside the Huffman
+    literals sections of make_zstd_x2.py's literal-heavy payloads (the
+    sections HUF_selectDecoder gives to X2), through zsk_zstd_decode_frames
+    in one launch (a lane per frame) and in batches of 40 (the one-frame
+    route): every frame's status and bytes are libzstd 1.4.9's own.  Pins on
+    the GPU that a stream the X1 walk accepts decodes the same under X2 and
+    that x2_rescue re-walks exactly the streams it rejects; the
+    oracle's X1-only mode counts the frames where X2 decides the result."""
+    import importlib.util
+    import os
+    from zstd_util import decode
+    spec = importlib.util.spec_from_file_location(
+        "make_zstd_x2", os.path.join(os.path.dirname(__file__), "golden", "make_zstd_x2.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    rng = np.random.default_rng(11)
+    frames, sizes, want = [], [], []
+    for name, data, level in mk.payloads():
+        comp = compress(zstd, data, {P_LEVEL: level}) if level is not None else compress_stream(zstd, data, 13_000)
+        spans = _literal_sections(comp)
+        assert spans, name
+        pos = np.concatenate([np.arange(a, b) for a, b in spans])
+        for p in rng.choice(pos, 260, replace=len(pos) < 260):
+            c = bytearray(comp)
+            c[int(p)] ^= int(rng.integers(1, 256))
+            frames.append(bytes(c))
+            sizes.append(len(data))
+            want.append(decode(zstd, bytes(c), len(data)))
+    assert len(frames) >= 1000
+    decisive = 0
+    oracle.lib.orc_zstd_x1_only(1)
+    try:
+        for f, n, (wb, wc) in zip(frames, sizes, want):
+            x1 = oracle.zstd_decode(f, n)
+            decisive += not (x1[1] == wc and (wc or x1[0] == wb))
+    finally:
+        oracle.lib.orc_zstd_x1_only(0)
+    assert decisive >= 10, decisive   # the sweep reaches frames X2 decides
+    if batch:
+        out, st = [], []
+        for b in range(0, len(frames), batch):
+            o, t = device_decode(zs, gpu, frames[b: b + batch], sizes[b: b + batch])
+            out += o
+            st += list(t)
+    else:
+        out, st = device_decode(zs, gpu, frames, sizes)
+    for i, (n, (wb, wc)) in enumerate(zip(sizes, want)):
+        if wc:
+            assert st[i] == ZSK_STATUS_ZSTD | wc, (i, hex(int(st[i])), wc)
+        else:
+            ok = len(wb) == n
+            assert st[i] == (0 if ok else 101), (i, hex(int(st[i])))
+            if ok:
+                assert out[i] == wb, i
