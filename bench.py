@@ -883,7 +883,8 @@ def traffic_from_profile(kernel, workload):
     workload."""
     if not kernel:
         return None
-    for name in ("pmc_traffic.json", "pmc_traffic_zstd.json", "pmc_traffic_lz4c.json"):
+    for name in ("pmc_traffic.json", "pmc_traffic_zstd.json", "pmc_traffic_lz4c.json", "pmc_traffic_f4096.json",
+                 "pmc_traffic_f1048576.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 rec = json.load(f)

@@ -6,7 +6,8 @@
 #   bash scripts/gpu.sh smoke                      __graft_entry__.smoke()
 #   bash scripts/gpu.sh bench TAG [bench args]     bench.py line -> gpurun_out/TAG/bench.json
 #   bash scripts/gpu.sh trace TAG [bench args]     rocprofv3 kernel trace + stats of bench.py --profile
-#   bash scripts/gpu.sh pmc TAG "COUNTERS" [args]  one rocprofv3 --pmc pass of bench.py --profile
+#   bash scripts/gpu.sh pmc TAG NAME "COUNTERS" [args]
+#                                                  one rocprofv3 --pmc pass of bench.py --profile -> gpurun_out/TAG/NAME
 #   bash scripts/gpu.sh evidence TAG [args]        bench + trace + FETCH/WRITE + EA passes + SQ passes
 #   bash scripts/gpu.sh kbab TAG VARIANTS [PMC_VARIANTS] [COUNTERS]
 #                                                  tuning-build A/B (scripts/gpu_kbab.sh)
@@ -35,8 +36,8 @@ trace)
       || { tail -20 gpurun_out/$tag/trace.log; exit 1; }
   python3 scripts/kernel_stats.py gpurun_out/$tag/trace > gpurun_out/$tag/kernel_medians.csv 2>&1; head -12 gpurun_out/$tag/kernel_medians.csv ;;
 pmc)
-  tag=$1; c=$2; shift 2; mkdir -p gpurun_out/$tag
-  d=gpurun_out/$tag/pmc_$(echo $c | tr ' ' '_' | cut -c1-40)
+  tag=$1; name=$2; c=$3; shift 3; mkdir -p gpurun_out/$tag
+  d=gpurun_out/$tag/$name
   timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $d -- python bench.py --profile --steps 2 --warmup 1 "$@" \
       > $d.log 2>&1 || { tail -5 $d.log; exit 1; } ;;
 evidence)
@@ -47,9 +48,10 @@ evidence)
   S1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
   S2="SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_BUSY_CYCLES"
   bash scripts/gpu.sh bench $tag "$@" && bash scripts/gpu.sh trace $tag "$@" &&
-  bash scripts/gpu.sh pmc $tag FETCH_SIZE "$@" && bash scripts/gpu.sh pmc $tag WRITE_SIZE "$@" &&
-  bash scripts/gpu.sh pmc $tag "$E1" "$@" && bash scripts/gpu.sh pmc $tag "$E2" "$@" && bash scripts/gpu.sh pmc $tag "$E3" "$@" &&
-  bash scripts/gpu.sh pmc $tag "$S1" "$@" && bash scripts/gpu.sh pmc $tag "$S2" "$@" &&
+  bash scripts/gpu.sh pmc $tag pmc_fetch FETCH_SIZE "$@" && bash scripts/gpu.sh pmc $tag pmc_write WRITE_SIZE "$@" &&
+  bash scripts/gpu.sh pmc $tag ea_p1 "$E1" "$@" && bash scripts/gpu.sh pmc $tag ea_p2 "$E2" "$@" &&
+  bash scripts/gpu.sh pmc $tag ea_p3 "$E3" "$@" &&
+  bash scripts/gpu.sh pmc $tag p1 "$S1" "$@" && bash scripts/gpu.sh pmc $tag p2 "$S2" "$@" &&
   python3 scripts/pmc_summary.py gpurun_out/$tag > gpurun_out/$tag/sq_summary.txt 2>&1 &&
   echo "evidence $tag done" ;;
 kbab)

@@ -51,7 +51,10 @@ ZSTD = "zstd" in bench["metric"]
 if ZSTD:   # zsk_zstd_decode_frames: plan + scan + frame + literal + sequence + execute + check
     LAUNCH = ("zstd_plan_kernel", "zstd_scan_kernel", "zstd_bounds_kernel", "zstd_frame_kernel", "zstd_huf_kernel",
               "zstd_seq_kernel", "zstd_lit_fix_kernel", "seq_exec_kernel", "zstd_check_kernel")
-OUT = "pmc_traffic_zstd.json" if ZSTD else "pmc_traffic.json"
+FRAME = bench["config"].get("frame_bytes", 65536)
+# config 3's frame-size sweep lines get files of their own (bench.py looks
+# for the one recorded on its workload)
+OUT = "pmc_traffic_zstd.json" if ZSTD else "pmc_traffic.json" if FRAME == 65536 else f"pmc_traffic_f{FRAME}.json"
 
 
 def part(name):
