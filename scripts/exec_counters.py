@@ -1,5 +1,5 @@
 """Per-wave instruction counters of every seq_exec dispatch in a
-gpu_exec_counters.sh run (passes p1, p2 lined up by dispatch order).
+`scripts/gpu.sh pmc` run (passes p1, p2 lined up by dispatch order).
 Optional second argument: the kernel-name fragment to select (default
 seq_exec); a third, "mean": one line, the mean over the selected dispatches."""
 import collections

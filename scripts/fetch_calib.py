@@ -20,7 +20,7 @@ One distinct frame per kind (64 KiB decoded), replicated 65,536 times (4 GiB
 decoded, config 2's geometry), so frames never share cache lines.  Run under
 `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (separate passes); then
 `python scripts/fetch_calib.py --summarize DIR` prints, per kind, the
-counter per launch against the known bytes (scripts/gpu_fetch_calib.sh).
+counter per launch against the known bytes (round 5; `scripts/gpu.sh pmc` runs such a pass).
 """
 from __future__ import annotations
 

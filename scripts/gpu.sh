@@ -11,7 +11,9 @@
 #   bash scripts/gpu.sh evidence TAG [args]        bench + trace + FETCH/WRITE + EA passes + SQ passes
 #   bash scripts/gpu.sh kbab TAG VARIANTS [PMC_VARIANTS] [COUNTERS]
 #                                                  tuning-build A/B (scripts/gpu_kbab.sh)
-#   bash scripts/gpu.sh latency TAG lz4|zstd [N]   single-frame latency probe (scripts/latency_probe.py)
+#   bash scripts/gpu.sh latency TAG lz4|zstd [N] [FRAME]
+#                                                  single-frame latency probe under a kernel trace
+#                                                  (scripts/latency_probe.py; FRAME bytes, default 64 KiB)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -57,10 +59,12 @@ evidence)
 kbab)
   tag=$1; shift; bash scripts/gpu_kbab.sh $tag "$@" ;;
 latency)
-  tag=$1; codec=$2; n=${3:-300}; mkdir -p gpurun_out/$tag
-  timeout -k 10 300 python scripts/latency_probe.py --codec $codec --n $n > gpurun_out/$tag/latency_$codec.log 2>&1 \
-      || { tail -20 gpurun_out/$tag/latency_$codec.log; exit 1; }
-  tail -5 gpurun_out/$tag/latency_$codec.log ;;
+  tag=$1; codec=$2; n=${3:-300}; fr=${4:-65536}; mkdir -p gpurun_out/$tag
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag/lat_${codec}_$fr \
+      -- python scripts/latency_probe.py $n $codec $fr > gpurun_out/$tag/lat_${codec}_$fr.log 2>&1 \
+      || { tail -20 gpurun_out/$tag/lat_${codec}_$fr.log; exit 1; }
+  grep -E "reads:" gpurun_out/$tag/lat_${codec}_$fr.log
+  python3 scripts/kernel_stats.py gpurun_out/$tag/lat_${codec}_$fr --skip 20 | cut -d, -f1,2,4,7 | head -12 ;;
 *)
   echo "unknown step $step"; exit 2 ;;
 esac

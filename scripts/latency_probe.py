@@ -1,5 +1,6 @@
 """Single-frame read latency probe: 4 KiB zseek_pread requests at random
-offsets of a 64 KiB-frame LZ4 (or, with a second argument `zstd`, zstd) image (cache off), timed per request in C
+offsets of a 64 KiB-frame (third argument: frame bytes) LZ4 (or, with a second argument `zstd`, zstd)
+image (cache off), timed per request in C
 (tools zsk_tool_latency).  Run under `rocprofv3 --kernel-trace --stats` to
 see where a request's time goes."""
 import ctypes as C
@@ -13,8 +14,9 @@ import libzseek_amd as z  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
 codec = sys.argv[2] if len(sys.argv) > 2 else "lz4"
+frame = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
 data = z.synth_buffer(256 << 20)
-img = z.zstd_seekable(data, 65536) if codec == "zstd" else z.lz4_seekable(data, 65536)
+img = z.zstd_seekable(data, frame) if codec == "zstd" else z.lz4_seekable(data, frame)
 T, L = z.tools(), z.lib()
 fn = [C.cast(f, C.c_void_p) for f in (L.zseek_reader_open_full, L.zseek_pread, L.zseek_reader_close)]
 err = C.create_string_buffer(80)

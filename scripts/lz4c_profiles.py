@@ -1,4 +1,4 @@
-"""Copy a scripts/gpu_lz4c.sh run into profiles/ (tracked) and derive
+"""Copy a `scripts/gpu.sh evidence TAG --codec lz4c` run into profiles/ (tracked) and derive
 profiles/pmc_traffic_lz4c.json for bench.py --codec lz4c's roofline.traffic.
 
   python scripts/lz4c_profiles.py r03 [gpurun_out/lz4c]

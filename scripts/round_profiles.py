@@ -1,4 +1,4 @@
-"""Copy a gpu_round.sh run's rocprofv3 summaries into profiles/ (tracked)
+"""Copy a `scripts/gpu.sh evidence` run's rocprofv3 summaries into profiles/ (tracked)
 and derive profiles/pmc_traffic.json for bench.py's roofline.traffic.
 
   python scripts/round_profiles.py r01 [gpurun_out/round]
@@ -9,7 +9,7 @@ reports half the bytes of a wide streaming read, MI355X_MICROARCH.md HBM
 section) + WRITE_SIZE, both in KiB from separate --pmc passes, median over
 dispatches per kernel.  Round 5: when the run also holds the L2's memory-side
 request counters (passes ea_p1..3: TCC_EA0_RDREQ_{32B,64B,128B},
-TCC_EA0_WRREQ{,_64B}; scripts/gpu_round5.sh), `hbm_bytes_per_launch` is their
+TCC_EA0_WRREQ{,_64B}; `scripts/gpu.sh evidence`), `hbm_bytes_per_launch` is their
 exact byte count instead (reads = 32 n32 + 64 n64 + 128 n128, writes = 64 n64
 + 32 (n - n64)); the FETCH-based figure stays beside it.  The calibration
 (profiles/r05_fetch_calib.json: frames whose execute reads are known) found

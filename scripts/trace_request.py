@@ -1,5 +1,5 @@
 """Kernel timeline of a few consecutive dispatches from a rocprofv3
---kernel-trace run (e.g. gpu_latency_probe.sh's): start offset and duration
+--kernel-trace run (e.g. `scripts/gpu.sh latency`'s): start offset and duration
 (us) of each, to see a request's launch gaps.  Args: trace dir, first row
 (default 400), rows (default 16)."""
 import csv

@@ -1,4 +1,4 @@
-"""Memory-side bytes per kernel dispatch from gpu_traffic.sh's passes: reads
+"""Memory-side bytes per kernel dispatch from `scripts/gpu.sh pmc` passes: reads
 = 32 n32 + 64 n64 + 128 n128 (TCC_EA0_RDREQ_{32B,64B,128B}), the share of
 read requests destined for DRAM (TCC_EA0_RDREQ_DRAM / TCC_EA0_RDREQ; the rest
 served by the Infinity Cache / other dies), writes = 64 n64 + 32 (n - n64)
