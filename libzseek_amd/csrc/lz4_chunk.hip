@@ -721,29 +721,44 @@ __global__ __launch_bounds__(64 * (ONE ? OW : kCW)) void lz4_chunk_kernel(
         // its items from rec_base (the job list is dropped)
         const uint32_t j0 = uni(bfirst[f]);
         if (j0 != kNoJob) {
-            const uint32_t nb = uni(bcount[f]);
-            bool bad = uni(*njobs) < min_jobs || nb == 0 || nb > 64;
-            uint32_t k = 0;
-            if (!bad && lane < nb) {
-                const BlockJob J = jobs[j0 + lane];
-                const BlockRes R = jres[j0 + lane];
-                const uint32_t mb = 1u << (8 + 2 * (J.info & 0xFF));
-                const uint32_t end = lane + 1 == nb ? d.d_size : J.bop + mb;
-                k = R.n;
-                bad = J.f != f || R.st != ST_OK || R.op != end || R.n == 0;
-            }
-            if (__ballot(bad) == 0) {
-                const uint32_t total = wave_incl_add(k);
-                if (lane == 63) {
-                    status[f] = ST_OK;
-                    nitems[f] = total;
-                    if (fail_at)
-                        fail_at[f] = 0;
+            // (ONE: wave 0 decides, the workgroup follows -- a re-parse needs
+            // every wave)
+            bool take = false;
+            if (!ONE || threadIdx.x < 64) {
+                const uint32_t l64 = threadIdx.x & 63;
+                const uint32_t nb = uni(bcount[f]);
+                bool bad = uni(*njobs) < min_jobs || nb == 0 || nb > 64;
+                uint32_t k = 0;
+                if (!bad && l64 < nb) {
+                    const BlockJob J = jobs[j0 + l64];
+                    const BlockRes R = jres[j0 + l64];
+                    const uint32_t mb = 1u << (8 + 2 * (J.info & 0xFF));
+                    const uint32_t end = l64 + 1 == nb ? d.d_size : J.bop + mb;
+                    k = R.n;
+                    bad = J.f != f || R.st != ST_OK || R.op != end || R.n == 0;
                 }
-                return;
+                take = __ballot(bad) == 0;
+                const uint32_t total = wave_incl_add(k);
+                if (l64 == 63) {
+                    if (take) {
+                        status[f] = ST_OK;
+                        nitems[f] = total;
+                        if (fail_at)
+                            fail_at[f] = 0;
+                    } else {
+                        bfirst[f] = kNoJob;
+                    }
+                }
             }
-            if (lane == 0)
-                bfirst[f] = kNoJob;
+            if constexpr (ONE) {
+                if (threadIdx.x == 0)
+                    coll[3 * kOneLanes + 15] = take ? 1u : 0u;
+                __syncthreads();
+                take = coll[3 * kOneLanes + 15] != 0;
+                __syncthreads();
+            }
+            if (take)
+                return;
         }
     }
     const uint64_t rb0 = (ONE && solo_total) ? 0 : rec_base[f];
@@ -923,6 +938,106 @@ __global__ __launch_bounds__(64 * (ONE ? OW : kCW)) void lz4_chunk_kernel(
     }
 }
 
+// The one-frame route for a frame of linked 64 KiB blocks (round 6, verdict
+// r05 item 7): a 1 MiB frame's 16 blocks went through one workgroup in turn
+// (~880 us of parse per miss).  Here the block plan's jobs (one per block,
+// lz4_block_plan_kernel) are parsed by a workgroup each, concurrently: the
+// block staged in LDS, the one-frame route's chunk parse (chunk_block<true>)
+// at the job's speculative output offset j x 64 KiB, its items into the job's
+// slots, its result into jres -- what the lean parse's block mode gives the
+// block route.  lz4_chunk_kernel<true> then accepts the frame's jobs or
+// re-parses the frame (exact status and fail_at) as for the block route.
+template <uint32_t OW>
+__global__ __launch_bounds__(64 * OW) void lz4_job_parse_kernel(const FrameDesc *__restrict__ desc,
+                                                               const uint8_t *__restrict__ comp,
+                                                               const uint64_t *__restrict__ rec_base,
+                                                               uint64_t capacity, uint64_t *__restrict__ items,
+                                                               const BlockJob *__restrict__ jobs,
+                                                               BlockRes *__restrict__ jres,
+                                                               const uint32_t *__restrict__ njobs, uint32_t lead)
+{
+    constexpr uint32_t kOneLanes = 64 * OW;
+    constexpr uint32_t nsw = kOneStage / 16 > kOneLanes * kWinQ ? kOneStage / 16 : kOneLanes * kWinQ;
+    __shared__ __attribute__((aligned(16))) uint32_t maps[kOneLanes * kOneMapW];
+    __shared__ __attribute__((aligned(16))) u32x4 stw[nsw];
+    __shared__ __attribute__((aligned(16))) uint64_t recs[kOneLanes * one_rec<OW>()];
+    __shared__ uint32_t coll[3 * kOneLanes + 16];
+    const uint32_t j = blockIdx.x, lane = threadIdx.x;
+    if (j >= (uint32_t)__builtin_amdgcn_readfirstlane(*njobs))
+        return;
+    const BlockJob J = jobs[j];
+    if (J.f == kNoJob)
+        return;
+    const FrameDesc d = desc[J.f];
+    const uint32_t ib = J.hpos + 4, iend = J.stop;
+    const Span sp = make_span(comp + d.c_off, d.c_size);
+    // the block [ib & ~3, iend + 64) staged: frame offset x at stage byte
+    // x - (ib & ~3) (chunk_block's staged reads take the frame offset)
+    const uint32_t a0 = ib & ~3u, np = (iend + 64 - a0 + 15) / 16;
+    const bool staged = np * 16 <= kOneStage;
+    if (staged) {
+        for (uint32_t i0 = 0; i0 < np; i0 += 4 * kOneLanes) {
+            u32x4 v[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t i = i0 + kOneLanes * q + lane;
+                v[q] = load16u(sp.r, i < np ? sp.s0 + a0 + 16 * i : 0x80000000u);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t i = i0 + kOneLanes * q + lane;
+                if (i < np)
+                    stw[i] = v[q];
+            }
+        }
+    }
+    __syncthreads();
+    Src S;
+    S.r = sp.r;
+    S.s0 = sp.s0;
+    S.staged = staged;
+    S.lds = (uint32_t)(uintptr_t)stw - a0;
+    Win W;
+    W.base = 0x80000000u;
+    W.lds = (uint32_t)(uintptr_t)(stw) + 64 * lane;
+    const uint32_t bsid = J.info & 0xFF, max_block = 1u << (8 + 2 * bsid);
+    const bool indep = (J.info >> 8) & 1;
+    const uint32_t bh = load16u(sp.r, sp.s0 + J.hpos).x, bsize = bh & 0x7FFFFFFFu;
+    uint64_t *it = items + rec_base[J.f] + J.slot_off;
+    const uint32_t cap = J.slot_cap;
+    uint32_t op = J.bop, k = 0;
+    int32_t st;
+    Blk B;
+    B.ib = ib;
+    B.iend = iend;
+    B.bop = op;
+    B.oend = op + max_block;
+    B.floor_ = indep ? op : 0;
+    B.dlen = d.d_size;
+    if (rec_base[J.f] + J.slot_off + cap > capacity || ib + bsize != iend) {
+        st = ST_NOT_RUN;
+    } else if (bh & 0x80000000u) {   // stored block: one literal run
+        const uint32_t nk = bsize > 255 ? 2 : 1;
+        st = op + bsize > d.d_size ? ST_DST_OVERFLOW : nk > cap ? ST_NOT_RUN : ST_OK;
+        if (st == ST_OK) {
+            if (lane == 0)
+                put_item(it, k, ib, bsize, 0, 0);
+            k = nk;
+            op += bsize;
+        }
+    } else if (bsize == 0) {
+        st = block_fail(B, bsid, max_block);
+    } else {
+        const int32_t bs = staged ? chunk_block<true, 1, OW>(S, W, B, lane, (uint32_t)(uintptr_t)maps, it, k, cap, op,
+                                                            (uint32_t)(uintptr_t)recs, (uint32_t)(uintptr_t)coll, lead)
+                                  : chunk_block<true, 0, OW>(S, W, B, lane, (uint32_t)(uintptr_t)maps, it, k, cap, op,
+                                                            (uint32_t)(uintptr_t)recs, (uint32_t)(uintptr_t)coll, lead);
+        st = bs < 0 ? ST_OK : bs == ST_BLOCK_ERR ? block_fail(B, bsid, max_block) : bs;
+    }
+    if (lane == 0)
+        jres[j] = BlockRes{k, op, st, 0};
+}
+
 }   // namespace
 
 // the one-frame parse's lead-in (bytes before each chunk): env ZSEEK_ONE_LEAD
@@ -952,6 +1067,16 @@ uint32_t one_lead()
     return v;
 }
 
+int launch_lz4_job_parse(const FrameDesc *d_desc, const uint8_t *d_comp, const uint64_t *rec_base, uint64_t capacity,
+                         uint64_t *items, const SplitScratch *s, uint32_t jobs, hipStream_t stream)
+{
+    if (jobs == 0)
+        return 0;
+    hipLaunchKernelGGL((lz4_job_parse_kernel<8>), dim3(jobs), dim3(64 * 8), 0, stream, d_desc, d_comp, rec_base,
+                       capacity, items, s->jobs, s->jres, s->njobs, one_lead());
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
@@ -960,16 +1085,19 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     if (nframes == 0)
         return 0;
     if (one) {
+        // (blk: the big frames' jobs, lz4_job_parse_kernel's results)
         if (one_waves() == 8)
             hipLaunchKernelGGL((lz4_chunk_kernel<true, 8>), dim3(nframes), dim3(64 * 8), 0, stream, d_desc, nframes,
-                               d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
-                               nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u,
-                               one_lead());
+                               d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize,
+                               blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr, blk ? blk->jobs : nullptr,
+                               blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr, min_jobs,
+                               nframes == 1 ? solo_total : nullptr, 1u, one_lead());
         else
             hipLaunchKernelGGL((lz4_chunk_kernel<true, 4>), dim3(nframes), dim3(64 * 4), 0, stream, d_desc, nframes,
-                               d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize, nullptr,
-                               nullptr, nullptr, nullptr, nullptr, 0u, nframes == 1 ? solo_total : nullptr, 1u,
-                               one_lead());
+                               d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize,
+                               blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr, blk ? blk->jobs : nullptr,
+                               blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr, min_jobs,
+                               nframes == 1 ? solo_total : nullptr, 1u, one_lead());
 #ifdef ZSK_TUNING
         if (getenv("ZSEEK_CHUNK_TIMERS")) {
             unsigned long long z[16];

@@ -156,7 +156,8 @@ __global__ __launch_bounds__(256) void lz4_block_plan_kernel(const FrameDesc *__
                                                               uint32_t *__restrict__ bfirst,
                                                               uint32_t *__restrict__ bcount,
                                                               uint32_t *__restrict__ njobs,
-                                                              BlockJob *__restrict__ jobs, uint32_t jobs_cap)
+                                                              BlockJob *__restrict__ jobs, uint32_t jobs_cap,
+                                                              uint32_t max_bsid)
 {
     const uint32_t f = blockIdx.x * 256 + threadIdx.x;
     if (f >= n)
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(256) void lz4_block_plan_kernel(const FrameDesc *__
     if (r32(0) != kLz4Magic)
         return;
     const uint32_t flg = c[4], bd = c[5];
-    if ((flg & 0xC0) != 0x40 || (flg & 0x16) || (bd & 0x8F) || ((bd >> 4) & 7) < 4)
+    if ((flg & 0xC0) != 0x40 || (flg & 0x16) || (bd & 0x8F) || ((bd >> 4) & 7) < 4 || ((bd >> 4) & 7) > max_bsid)
         return;
     const uint32_t csz = (flg >> 3) & 1, dictid = flg & 1;
     const uint32_t hdr = 7 + 8 * csz + 4 * dictid;
@@ -583,12 +584,23 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     BlockRoute br = one ? BlockRoute{false, 0, 0} : block_route(nframes, route, r);
     const uint64_t jw = (uint64_t)nframes * kMaxBlockJobs;
     const uint32_t jlanes = (uint32_t)(jw < kJobsCapMax ? jw : kJobsCapMax);
+    // the one-frame route's frames of > 64 KiB: their blocks
+    // of <= 64 KiB get block-plan jobs, parsed a workgroup each
+    // (launch_lz4_job_parse), and the windowed execute takes them
+    // (launch_seq_exec_big); env ZSEEK_ONE_BIG=0: as round 5
+    static const bool big_off = [] {
+        const char *v = getenv("ZSEEK_ONE_BIG");
+        return v && !strcmp(v, "0");
+    }();
+    bool big = one && max_dsize > 65536 && !big_off && ((tune >> 8) & 0xFFF) == 0;
+    if (big)
+        br = BlockRoute{true, 0, 1};
     if (br.on && block_scratch_reserve(s, nframes, jlanes, stream) != 0)
-        br.on = false;   // no room: the chunk parse takes the frames as before
+        br.on = big = false;   // no room: the chunk parse takes the frames as before
     SplitScratch *blk = br.on ? s : nullptr;
     stage_mark(0, stream);
     // one frame on the one-frame route: the chunk kernel does the plan's work
-    const bool solo = one && nframes == 1 && (stages & 3) == 3;
+    const bool solo = one && nframes == 1 && (stages & 3) == 3 && !big;
     if ((stages & 1) && !solo) {
         hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3(std::min<uint32_t>((nframes + 255) / 256, kPlanGroups)),
                            dim3(256), 0, stream, d_desc, nframes, s->rec_base, total_dev, s->redo, d_status,
@@ -596,7 +608,8 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         if (blk) {
             (void)hipMemsetAsync(s->njobs, 0, sizeof(uint32_t), stream);
             hipLaunchKernelGGL(lz4_block_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
-                               nframes, d_comp, br.min_csize, s->bfirst, s->bcount, s->njobs, s->jobs, jlanes);
+                               nframes, d_comp, br.min_csize, s->bfirst, s->bcount, s->njobs, s->jobs, jlanes,
+                               big ? 4u : 7u);
         }
     }
     stage_mark(1, stream);
@@ -605,7 +618,9 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     // route jobs before the chunk parse, which accepts or re-parses their
     // frames
     if (stages & 2) {
-        if (blk)
+        if (big)
+            launch_lz4_job_parse(d_desc, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items, s, jlanes, stream);
+        else if (blk)
             launch_lz4_lean_blocks(d_desc, d_comp, s->rec_base, (uint64_t)s->items_cap, s->items, s, jlanes,
                                    br.min_jobs, stream);
         if (r.chunk_min > r.lean_min)
@@ -632,12 +647,15 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
             // hand-offs of <= 64 KiB frames decoded inside (when the batch has
             // no bigger frame and the hand-off stage is asked for: no
             // hand-off launch below)
-            frame_handoff = (stages & 8) && max_dsize <= 65536;
+            frame_handoff = (stages & 8) && (max_dsize <= 65536 || big);
             launch_seq_exec_frames(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
                                    d_fail_at, stream, stop_last, frame_handoff);
-            if (max_dsize > 65536)
+            if (big)
+                launch_seq_exec_big(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
+                                    d_fail_at, stream, stop_last, frame_handoff, s);
+            else if (max_dsize > 65536)
                 launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status, stream,
-                                0, blk, stop_last, 65537);
+                                0, nullptr, stop_last, 65537);
         } else {
             launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status, stream,
                             (tune >> 8) & 0xFFF, blk, stop_last);

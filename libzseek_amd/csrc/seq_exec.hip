@@ -52,6 +52,54 @@ __device__ uint32_t g_fdiag;   // ZSEEK_FRAME_DIAG: 1 no literal copies, 2 no li
 #define ZSK_FT(i)
 #endif
 
+// 1..64 bytes between disjoint LDS ranges with whole-width writes only:
+// 16-byte pieces from the start plus one ending at n (overlapping pieces
+// rewrite equal bytes), two 8- or 4-byte ones below 16 bytes -- no per-piece
+// partial-store branches (reads may run past the source: the arrays have
+// slack)
+__device__ __forceinline__ void scopy(uint32_t dst, uint32_t src, uint32_t n)
+{
+    if (n >= 16) {
+        const u32x4 a = lds16(src), b = lds16(src + 16), c = lds16(src + 32), e = lds16(src + n - 16);
+        *lp<u32x4_l>(dst) = a;
+        if (n > 32)
+            *lp<u32x4_l>(dst + 16) = b;
+        if (n > 48)
+            *lp<u32x4_l>(dst + 32) = c;
+        *lp<u32x4_l>(dst + n - 16) = e;
+    } else if (n >= 8) {
+        const uint64_t a = *lp<u64_l>(src), e = *lp<u64_l>(src + n - 8);
+        *lp<u64_l>(dst) = a;
+        *lp<u64_l>(dst + n - 8) = e;
+    } else if (n >= 4) {
+        const uint32_t a = *lp<u32_l>(src), e = *lp<u32_l>(src + n - 4);
+        *lp<u32_l>(dst) = a;
+        *lp<u32_l>(dst + n - 4) = e;
+    } else {
+        for (uint32_t k = 0; k < n; k++)
+            *lp<uint8_t>(dst + k) = *lp<uint8_t>(src + k);
+    }
+}
+
+// n bytes from LDS src to LDS dst, dst - src >= step or the ranges apart: up
+// to four 16-byte pieces read before they are written (a piece's source was
+// written at least `step` bytes earlier)
+__device__ __forceinline__ void lcopy(uint32_t dst, uint32_t src, uint32_t n, uint32_t step)
+{
+    for (uint32_t k = 0; k < n; k += step) {
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)
+            if (16 * q < step)
+                v[q] = lds16(src + k + 16 * q);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)
+            if (16 * q < step && k + 16 * q < n)
+                lds_put(dst + k + 16 * q, v[q], min(16u, n - k - 16 * q));
+        wave_lds_sync();
+    }
+}
+
 __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
@@ -156,51 +204,6 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         return all;
     };
-    // 1..64 bytes between disjoint LDS ranges with whole-width writes only:
-    // 16-byte pieces from the start plus one ending at n (overlapping pieces
-    // rewrite equal bytes), two 8- or 4-byte ones below 16 bytes -- no
-    // per-piece partial-store branches (reads may run past the source: the
-    // arrays have slack)
-    auto scopy = [&](uint32_t dst, uint32_t src, uint32_t n) {
-        if (n >= 16) {
-            const u32x4 a = lds16(src), b = lds16(src + 16), c = lds16(src + 32), e = lds16(src + n - 16);
-            *lp<u32x4_l>(dst) = a;
-            if (n > 32)
-                *lp<u32x4_l>(dst + 16) = b;
-            if (n > 48)
-                *lp<u32x4_l>(dst + 32) = c;
-            *lp<u32x4_l>(dst + n - 16) = e;
-        } else if (n >= 8) {
-            const uint64_t a = *lp<u64_l>(src), e = *lp<u64_l>(src + n - 8);
-            *lp<u64_l>(dst) = a;
-            *lp<u64_l>(dst + n - 8) = e;
-        } else if (n >= 4) {
-            const uint32_t a = *lp<u32_l>(src), e = *lp<u32_l>(src + n - 4);
-            *lp<u32_l>(dst) = a;
-            *lp<u32_l>(dst + n - 4) = e;
-        } else {
-            for (uint32_t k = 0; k < n; k++)
-                *lp<uint8_t>(dst + k) = *lp<uint8_t>(src + k);
-        }
-    };
-    // n bytes from LDS src to LDS dst, dst - src >= step or the ranges apart:
-    // up to four 16-byte pieces read before they are written (a piece's
-    // source was written at least `step` bytes earlier)
-    auto lcopy = [&](uint32_t dst, uint32_t src, uint32_t n, uint32_t step) {
-        for (uint32_t k = 0; k < n; k += step) {
-            u32x4 v[4];
-#pragma unroll
-            for (uint32_t q = 0; q < 4; q++)
-                if (16 * q < step)
-                    v[q] = lds16(src + k + 16 * q);
-#pragma unroll
-            for (uint32_t q = 0; q < 4; q++)
-                if (16 * q < step && k + 16 * q < n)
-                    lds_put(dst + k + 16 * q, v[q], min(16u, n - k - 16 * q));
-            wave_lds_sync();
-        }
-    };
-
     uint32_t base_op = 0;
     for (uint32_t w0 = 0; w0 < nit && base_op < stop; w0 += 2 * kFT) {
         uint32_t lit[2], ml[2], off[2], src[2], op[2], tot[2];
@@ -368,6 +371,362 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
 }
 #undef ZSK_FT
 
+// ---- the one-frame route's execute for frames of more than 64 KiB ----
+// (round 6, verdict r05 item 7: a 1 MiB frame's execute on one wave took
+// ~890 us per miss).  One frame per 1,024-thread workgroup, as
+// seq_exec_frame_kernel, through a sliding window: LDS holds the 64 KiB of
+// output before the window (every byte final: LZ4's offsets reach 65,535
+// back) and the window itself, 64 KiB at frame offset H.  A batch of 2,048
+// items is placed by the same workgroup scan and cut before the first item
+// that would end past the window; literal runs are copied from HBM (the
+// compressed frame does not fit beside the window), matches resolve in the
+// per-wave passes over the window's done bits, a source byte before H
+// always ready.  Then the window's bytes go out and it slides to the first
+// byte not decoded (the 64 KiB before it moved down as the new history).
+// Items: contiguous (rec_base[f]), or -- a frame the block route accepted
+// (bfirst[f] != kNoJob, the job parse of lz4_chunk.hip) -- job by job, item
+// index i mapped onto its job's slots through a table of the jobs' first
+// indices.  A frame no window can take (an item longer than 64 KiB: blocks
+// over 64 KiB) and the batch's hand-offs (ST_NOT_RUN) are decoded by the
+// wave decoder on wave 0 instead.
+constexpr uint32_t kBWin = 65536;
+
+#ifdef ZSK_TUNING
+// tuning builds: seq_exec_big_kernel's phase cycles (thread 0): [0] init,
+// [1] items + scans, [2] cut + literal runs, [3] match passes, [4] slides,
+// [5] last output; [6] slides, [7] batches, [8] frames (ZSEEK_BIG_TIMERS)
+__device__ unsigned long long g_btime[9];
+#define ZSK_BT(i)                                                             \
+    {                                                                         \
+        const uint64_t tn_ = __builtin_readcyclecounter();                    \
+        if (t == 0)                                                           \
+            atomicAdd(&g_btime[i], (unsigned long long)(tn_ - tmark_));       \
+        tmark_ = tn_;                                                         \
+    }
+#define ZSK_BC(i)                                                             \
+    if (t == 0)                                                               \
+        atomicAdd(&g_btime[i], 1ull);
+#else
+#define ZSK_BT(i)
+#define ZSK_BC(i)
+#endif
+
+__global__ __launch_bounds__(kFT) void seq_exec_big_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
+    const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
+    int32_t *__restrict__ status, uint32_t *__restrict__ fail_at, uint32_t stop_last, uint32_t handoff,
+    const uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount, const BlockJob *__restrict__ jobs,
+    const BlockRes *__restrict__ jres)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t ob[2 * kBWin + 80];
+    __shared__ uint32_t done[kBWin / 32 + 2];
+    __shared__ uint32_t wsum[kFT / 64];
+    __shared__ uint32_t jtab[2 * kMaxBlockJobs];   // per job: its first item index, slot offset - that index
+    __shared__ uint32_t cut_i, cut_op, hi_end;
+    const uint32_t f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (f >= n)
+        return;
+    const FrameDesc d = desc[f];
+    if (d.d_size <= kFMax)
+        return;   // seq_exec_frame_kernel's frame
+    // the windowed execute; false: stuck (an item longer than the window)
+    auto window_frame = [&]() -> bool {
+    #ifdef ZSK_TUNING
+    uint64_t tmark_ = __builtin_readcyclecounter();
+#endif
+    const uint32_t j0 = bfirst ? __builtin_amdgcn_readfirstlane(bfirst[f]) : kNoJob;
+        const uint32_t nj = j0 != kNoJob ? __builtin_amdgcn_readfirstlane(bcount[f]) : 0u;
+        uint32_t nit;
+        if (nj) {
+            if (wv == 0) {
+                uint32_t so = 0, k = 0;
+                if (lane < nj) {
+                    so = jobs[j0 + lane].slot_off;
+                    k = jres[j0 + lane].n;
+                }
+                const uint32_t inc = wave_incl_add(k);
+                if (lane < nj) {
+                    jtab[2 * lane] = inc - k;
+                    jtab[2 * lane + 1] = so - (inc - k);
+                }
+                if (lane == 63)
+                    wsum[0] = inc;
+            }
+            __syncthreads();
+            nit = wsum[0];
+        } else {
+            nit = nitems[f];
+        }
+        // item index -> slot (relative to rec_base[f]): the last job starting at
+        // or before i (job starts ascend: an accepted job has items)
+        auto slot = [&](uint32_t i) -> uint32_t {
+            if (nj == 0)
+                return i;
+            uint32_t lo = 0, hi = nj;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (jtab[2 * mid] <= i)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            return i + jtab[2 * lo + 1];
+        };
+        const uint32_t stop = f + 1 == n ? min(stop_last, d.d_size) : d.d_size;
+        const uint64_t *it = items + rec_base[f];
+        const Span lsp = make_span(comp + d.c_off, d.c_size);
+        uint8_t *o = out + d.d_off;
+        const uint32_t ob0 = (uint32_t)(uintptr_t)ob, C = ob0 + kBWin;   // window byte x at C + x - H
+        for (uint32_t i = t; i < kBWin / 32 + 2; i += kFT)
+            done[i] = 0;
+        if (t == 0)
+            hi_end = 0;
+        __syncthreads();
+        ZSK_BT(0)
+        ZSK_BC(8)
+
+        auto scan = [&](uint32_t v, uint32_t &total) -> uint32_t {   // exclusive, in thread order
+            const uint32_t inc = wave_incl_add(v);
+            if (lane == 63)
+                wsum[wv] = inc;
+            __syncthreads();
+            uint32_t before = 0, tot = 0;
+            for (uint32_t k = 0; k < kFT / 64; k++) {
+                const uint32_t x = wsum[k];
+                before += k < wv ? x : 0;
+                tot += x;
+            }
+            __syncthreads();
+            total = tot;
+            return before + inc - v;
+        };
+        auto mark = [&](uint32_t a, uint32_t len) {   // window bytes [a, a + len) written
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            for (const uint32_t e = a + len; a < e;) {
+                const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
+                __hip_atomic_fetch_or(&done[a >> 5], nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                a += nb;
+            }
+        };
+        auto ready = [&](uint32_t a, uint32_t len) -> bool {   // window bytes
+            bool all = true;
+            for (const uint32_t e = a + len; a < e;) {
+                const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
+                const uint32_t m = nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0;
+                all &= (__hip_atomic_load(&done[a >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & m) == m;
+                a += nb;
+            }
+            if (all)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            return all;
+        };
+        // frame bytes [a, e) of the window out: a byte head to 16-byte
+        // alignment, whole 16-byte stores, a byte tail
+        auto put_out = [&](uint32_t H, uint32_t a, uint32_t e) {
+            if (e <= a)
+                return;
+            const uint32_t head = min(e - a, (uint32_t)((16 - ((uintptr_t)(o + a) & 15)) & 15));
+            const uint32_t w = kBWin + a - H;
+            if (t < head)
+                o[a + t] = ob[w + t];
+            const uint32_t nchunks = (e - a - head) / 16;
+            for (uint32_t c = t; c < nchunks; c += kFT)
+                *reinterpret_cast<u32x4 *>(o + a + head + 16 * c) = lds16(ob0 + w + head + 16 * c);
+            const uint32_t tail0 = head + 16 * nchunks;
+            if (tail0 + t < e - a)
+                o[a + tail0 + t] = ob[w + tail0 + t];
+        };
+
+        uint32_t H = 0, P = 0, w0 = 0;   // window start, bytes decoded, next item
+        bool stuck = false;
+        while (w0 < nit && P < stop) {
+            if (t == 0) {
+                cut_i = 0xFFFFFFFFu;
+                cut_op = 0xFFFFFFFFu;
+            }
+            uint32_t lit[2], ml[2], off[2], src[2], op[2], tot[2], idx[2];
+            for (int j = 0; j < 2; j++) {
+                const uint32_t i = w0 + j * kFT + t;
+                idx[j] = i;
+                lit[j] = ml[j] = off[j] = src[j] = 0;
+                if (i < nit) {
+                    const uint32_t si = slot(i);
+                    const uint64_t cur = it[si];
+                    const uint32_t c0 = (uint32_t)cur, c1 = (uint32_t)(cur >> 32);
+                    const bool second = i > 0 && ((uint32_t)it[slot(i - 1)] & kItemExt);   // an extended item's second half
+                    if (!second) {
+                        src[j] = c0 & kItemPos;
+                        if (c0 & kItemExt) {
+                            const uint64_t nx = it[si + 1];
+                            lit[j] = (uint32_t)nx;
+                            ml[j] = (uint32_t)(nx >> 32);
+                            off[j] = c1;
+                        } else {
+                            lit[j] = (c1 >> 16) & 0xFF;
+                            const uint32_t mc = c1 >> 24;
+                            ml[j] = mc ? mc + 3 : 0;
+                            off[j] = c1 & 0xFFFF;
+                        }
+                    }
+                }
+            }
+            const uint32_t x0 = scan(lit[0] + ml[0], tot[0]);
+            const uint32_t x1 = scan(lit[1] + ml[1], tot[1]);
+            ZSK_BT(1)
+            ZSK_BC(7)
+            op[0] = P + x0;
+            op[1] = P + tot[0] + x1;
+            // the cut: the first item ending past the window (ops ascend with the
+            // index, so the smallest index and op are the same item's)
+            for (int j = 0; j < 2; j++) {
+                const bool over = lit[j] + ml[j] != 0 && op[j] + lit[j] + ml[j] > H + kBWin;
+                const uint64_t ov = __ballot(over);
+                if (ov && lane == (uint32_t)__builtin_ctzll(ov)) {
+                    atomicMin(&cut_i, idx[j]);
+                    atomicMin(&cut_op, op[j]);
+                }
+            }
+            __syncthreads();
+            const uint32_t ci = cut_i, lim = min(cut_op, stop);
+            bool pend[2];
+            for (int j = 0; j < 2; j++) {
+                const bool on = op[j] < lim && lit[j] + ml[j] != 0;
+                const uint32_t L = on ? lit[j] : 0;
+                const uint32_t dst = C + op[j] - H;
+                const bool coop = L > kFLong;   // (as seq_exec_frame_kernel)
+                for (uint64_t lm = __ballot(coop); lm; lm &= lm - 1) {
+                    const int q = (int)__builtin_ctzll(lm);
+                    const uint32_t d0 = lane_val(dst, q), s = lane_val(src[j], q), nq = lane_val(L, q);
+                    for (uint32_t k = 16 * lane; k < nq; k += 1024)
+                        lds_put(d0 + k, load16u(lsp.r, lsp.s0 + s + k), min(16u, nq - k));
+                }
+                if (!coop && L) {
+                    // up to 64 bytes per step, four 16-byte loads in flight
+                    for (uint32_t k = 0; k < L; k += 64) {
+                        u32x4 v[4];
+    #pragma unroll
+                        for (uint32_t q = 0; q < 4; q++)
+                            v[q] = load16u(lsp.r, k + 16 * q < L ? lsp.s0 + src[j] + k + 16 * q : kBad);
+    #pragma unroll
+                        for (uint32_t q = 0; q < 4; q++)
+                            if (k + 16 * q < L)
+                                lds_put(dst + k + 16 * q, v[q], min(16u, L - k - 16 * q));
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                for (uint64_t lm = __ballot(coop); lm; lm &= lm - 1) {
+                    const int q = (int)__builtin_ctzll(lm);
+                    const uint32_t a = lane_val(op[j], q) - H, e = a + lane_val(L, q) - 1;
+                    for (uint32_t g = (a >> 5) + lane; g <= e >> 5; g += 64) {
+                        const uint32_t lo = g == a >> 5 ? a & 31 : 0, hi = g == e >> 5 ? e & 31 : 31;
+                        const uint32_t m = hi - lo == 31 ? 0xFFFFFFFFu : ((1u << (hi - lo + 1)) - 1) << lo;
+                        __hip_atomic_fetch_or(&done[g], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                if (!coop && L)
+                    mark(op[j] - H, L);
+                pend[j] = on && ml[j] != 0;
+            }
+            {
+                const bool on0 = op[0] < lim && lit[0] + ml[0] != 0, on1 = op[1] < lim && lit[1] + ml[1] != 0;
+                const uint32_t e = max(on0 ? op[0] + lit[0] + ml[0] : 0u, on1 ? op[1] + lit[1] + ml[1] : 0u);
+                const uint32_t we = wave_incl_max(e);
+                if (lane == 63 && we)
+                    atomicMax(&hi_end, we);
+            }
+            __syncthreads();
+            ZSK_BT(2)
+            for (uint32_t pass = 0;; pass++) {
+                bool moved = false;
+                for (int j = 0; j < 2; j++) {
+                    if (!pend[j])
+                        continue;
+                    const uint32_t mb = op[j] + lit[j], ov = off[j], m = ml[j];
+                    // the source's first min(off, ml) bytes: those before H are final
+                    const uint32_t s0 = mb - ov, s1 = s0 + (ov >= m ? m : ov);
+                    if (s1 > H && !ready(s0 > H ? s0 - H : 0u, s1 - (s0 > H ? s0 : H)))
+                        continue;
+                    const uint32_t db = C + mb - H, sb = db - ov;
+                    if (ov >= m && m <= 128) {
+                        scopy(db, sb, min(m, 64u));
+                        if (m > 64)
+                            scopy(db + 64, sb + 64, m - 64);
+                    } else if (ov >= m || ov >= 16) {
+                        lcopy(db, sb, m, ov >= m ? 64u : min(64u, ov & ~15u));
+                    } else {
+                        const uint32_t e = ov * ((16 + ov - 1) / ov);
+                        const uint32_t h = min(e, m);
+                        for (uint32_t k = 0; k < h; k++) {
+                            *lp<uint8_t>(db + k) = *lp<uint8_t>(sb + k);
+                            wave_lds_sync();
+                        }
+                        for (uint32_t k = h; k < m; k += 16) {
+                            lds_put(db + k, lds16(db + k - e), min(16u, m - k));
+                            wave_lds_sync();
+                        }
+                    }
+                    mark(mb - H, m);
+                    pend[j] = false;
+                    moved = true;
+                }
+                if (!__any(pend[0] || pend[1]) || pass > (1u << 22))
+                    break;
+                if (!__any(moved))
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            __syncthreads();
+            ZSK_BT(3)
+            const uint32_t P1 = ci != 0xFFFFFFFFu ? min(cut_op, P + tot[0] + tot[1]) : P + tot[0] + tot[1];
+            if (ci != 0xFFFFFFFFu && P1 == H) {   // one item longer than the window
+                stuck = true;
+                break;
+            }
+            P = P1;
+            w0 = ci != 0xFFFFFFFFu ? ci : w0 + 2 * kFT;
+            // slide once the window is cut or three quarters full (and there is
+            // more to decode): its bytes out, the 64 KiB before P down as history
+            if ((ci != 0xFFFFFFFFu || P - H >= kBWin - kBWin / 4) && w0 < nit && P < stop) {
+                put_out(H, H, P);
+                const uint32_t sh = P - H;
+                u32x4 v[4];
+    #pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    v[q] = lds16(ob0 + sh + 16 * (t + q * kFT));
+                __syncthreads();
+    #pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    *lp<u32x4>(ob0 + 16 * (t + q * kFT)) = v[q];
+                for (uint32_t i = t; i < kBWin / 32 + 2; i += kFT)
+                    done[i] = 0;
+                __syncthreads();
+                H = P;
+                ZSK_BT(4)
+                ZSK_BC(6)
+            }
+        }
+        if (stuck)
+            return false;
+        put_out(H, H, min(hi_end, d.d_size));
+#ifdef ZSK_TUNING
+        __syncthreads();
+        ZSK_BT(5)
+#endif
+        return true;
+    };
+    // the wave decoder's frame: a hand-off, or one no window can take (one
+    // call site: the decoder inlined twice spilled)
+    bool whole = __builtin_amdgcn_readfirstlane(status[f]) == ST_NOT_RUN;
+    if (whole && !handoff)
+        return;
+    if (!whole)
+        whole = !window_frame();
+    if (whole) {
+        if (wv == 0)
+            lz4w::wave_frame<4096>(desc, f, comp, out, status, fail_at, ob);
+    }
+}
+
 }   // namespace
 
 #ifdef ZSK_TUNING
@@ -430,6 +789,35 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
                 "frame execute cycles per frame: stage+init %.0f items+scan %.0f literals %.0f matches %.0f "
                 "output %.0f | windows %.2f wave passes %.1f (%llu frames)\n",
                 z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr, z[6] / fr / 16.0, z[7]);
+    }
+#endif
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_seq_exec_big(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                        const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
+                        int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
+                        bool handoff, const SplitScratch *blk)
+{
+    if (nframes == 0)
+        return 0;
+    hipLaunchKernelGGL(seq_exec_big_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
+                       rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff ? 1u : 0u,
+                       blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr, blk ? blk->jobs : nullptr,
+                       blk ? blk->jres : nullptr);
+#ifdef ZSK_TUNING
+    // ZSEEK_BIG_TIMERS: accumulate the phase cycles, print every 100 launches
+    static const bool timers = getenv("ZSEEK_BIG_TIMERS") != nullptr;
+    static int calls = 0;
+    if (timers && ++calls % 100 == 0) {
+        unsigned long long z[9] = {0};
+        (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_btime), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+        (void)hipStreamSynchronize(stream);
+        const double fr = z[8] ? (double)z[8] : 1.0;
+        fprintf(stderr,
+                "big execute cycles per frame: init %.0f items+scan %.0f cut+literals %.0f matches %.0f slides %.0f "
+                "output %.0f | slides %.2f batches %.2f (%llu frames)\n",
+                z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr, z[6] / fr, z[7] / fr, z[8]);
     }
 #endif
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -215,6 +215,13 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
                            const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                            int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
                            bool handoff, const uint8_t *lit = nullptr);
+// ... and its frames of more than 64 KiB (the one-frame route's big frames):
+// one per workgroup through a sliding 64 KiB window, items job by job for a
+// frame the block route accepted (blk, may be null); handoff as above.
+int launch_seq_exec_big(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                        const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
+                        int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
+                        bool handoff, const SplitScratch *blk);
 int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         const int32_t *d_status, hipStream_t stream, const SplitScratch *blk);
@@ -347,14 +354,22 @@ int launch_lz4_lean_blocks(const FrameDesc *d_desc, const uint8_t *d_comp, const
                            uint64_t capacity, uint64_t *items, const SplitScratch *s, uint32_t lanes,
                            uint32_t min_jobs, hipStream_t stream);
 
+// The one-frame route's big frames (lz4_chunk.hip): each of the first
+// *s->njobs block-plan jobs (a grid of `jobs` workgroups) parsed by a
+// workgroup, the one-frame route's chunk parse over the block staged in LDS,
+// results into s->jres as the block route's lean parse gives them.
+int launch_lz4_job_parse(const FrameDesc *d_desc, const uint8_t *d_comp, const uint64_t *rec_base, uint64_t capacity,
+                         uint64_t *items, const SplitScratch *s, uint32_t jobs, hipStream_t stream);
+
 // Parse phase, one wave per frame, chunk-parallel (lz4_chunk.hip): the same
 // outputs as launch_lz4_scan for the frames of min_csize compressed bytes and
 // more (other frames are left to lz4_scan_kernel), items without padding.
 // With `blk`: a frame with a job list is accepted from its jobs' results
 // (when at least min_jobs were planned and every job parsed cleanly at its
 // speculative offset) or parsed here, its job list dropped.
-// `one` (the one-frame route; no `blk`): one frame per workgroup, the frame
-// staged whole in LDS when it fits (lz4_chunk.hip, ONE).
+// `one` (the one-frame route): one frame per workgroup, the frame staged
+// whole in LDS when it fits (lz4_chunk.hip, ONE); its `blk` holds the big
+// frames' jobs (launch_lz4_job_parse).
 int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      const uint64_t *rec_base, uint64_t capacity, uint64_t *items, uint32_t *nitems,
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,

@@ -7,8 +7,11 @@ Frames built here by splicing LZ4F blocks — reordered independent blocks,
 short stored blocks before the last (the speculation fails and the chunk
 parse takes the frame), corrupt blocks mid-frame, trailing bytes, more blocks
 than the route takes, seek-table sizes that disagree — go through the forced
-route (ZSK_DECODER_BLOCK: any batch, any job count) and must give the CPU
-restatement's status and bytes (oracle/lz4_oracle.c decode_frame, liblz4
+route (ZSK_DECODER_BLOCK: any batch, any job count) -- and the one-frame
+route's big-frame path (ZSK_DECODER_ONE: its jobs of <= 64 KiB blocks parsed a
+workgroup each, lz4_job_parse_kernel, and executed through the sliding
+window, seq_exec_big_kernel) -- and must give the CPU restatement's status
+and bytes (oracle/lz4_oracle.c decode_frame, liblz4
 1.9.3 LZ4F_decompress semantics) and the wave kernel's status codes."""
 import numpy as np
 import pytest
@@ -82,9 +85,9 @@ def _decode(zs, gpu, frames, dsizes, engine):
     return [o[int(d[i]): int(d[i + 1])] for i in range(n)], status.cpu().tolist()
 
 
-def _check(zs, oracle, gpu, frames, dsizes):
+def _check(zs, oracle, gpu, frames, dsizes, engine="block"):
     """block route == oracle (status, bytes of OK frames) and == wave statuses"""
-    got, st = _decode(zs, gpu, frames, dsizes, "block")
+    got, st = _decode(zs, gpu, frames, dsizes, engine)
     _, st_w = _decode(zs, gpu, frames, dsizes, "wave")
     assert st == st_w
     for i, (f, ds) in enumerate(zip(frames, dsizes)):
@@ -106,7 +109,8 @@ def indep(zs):
     return [_split(f)[3] for f in frames]
 
 
-def test_block_route_reordered_independent_blocks(gpu, zs, oracle, indep):
+@pytest.mark.parametrize("engine", ["block", "one"])
+def test_block_route_reordered_independent_blocks(gpu, zs, oracle, indep, engine):
     """Independent blocks reordered and mixed across frames: accepted by the
     route (every block but the last full-size), bytes == oracle."""
     b = indep
@@ -114,11 +118,12 @@ def test_block_route_reordered_independent_blocks(gpu, zs, oracle, indep):
               _frame([b[1][5], b[0][0]], flg=0x60 | 0x20),
               _frame([b[2][i] for i in range(16)][::-1][1:] + [b[2][15]], flg=0x60 | 0x20)]
     dsizes = [len(oracle.decode_frame(f, 1 << 24)[1]) for f in frames]
-    st = _check(zs, oracle, gpu, frames, dsizes)
+    st = _check(zs, oracle, gpu, frames, dsizes, engine)
     assert st == [0, 0, 0]
 
 
-def test_block_route_short_blocks_reparsed(gpu, zs, oracle, indep):
+@pytest.mark.parametrize("engine", ["block", "one"])
+def test_block_route_short_blocks_reparsed(gpu, zs, oracle, indep, engine):
     """A stored block shorter than the maximum before the last: the
     speculative offsets are wrong for the blocks after it; the chunk parse
     re-parses the frame (bytes == oracle).  Also all-stored frames (accepted),
@@ -131,11 +136,12 @@ def test_block_route_short_blocks_reparsed(gpu, zs, oracle, indep):
               _frame([raw[1], raw[2], raw[4]]),
               _frame([b[2][0], b[2][1], raw[3]], flg=0x60 | 0x20)]
     dsizes = [len(oracle.decode_frame(f, 1 << 24)[1]) for f in frames]
-    st = _check(zs, oracle, gpu, frames, dsizes)
+    st = _check(zs, oracle, gpu, frames, dsizes, engine)
     assert st == [0, 0, 0, 0]
 
 
-def test_block_route_corrupt_and_odd_frames(gpu, zs, oracle, indep):
+@pytest.mark.parametrize("engine", ["block", "one"])
+def test_block_route_corrupt_and_odd_frames(gpu, zs, oracle, indep, engine):
     """Failures inside the route's frames give the exact statuses: a corrupt
     block mid-frame, a block size over the maximum, a zero-size compressed
     block, trailing bytes after the end mark, a truncated frame, a seek-table
@@ -161,12 +167,13 @@ def test_block_route_corrupt_and_odd_frames(gpu, zs, oracle, indep):
               _frame(blocks[:4], flg=0x60 | 0x20, content_size=4 * 65536, dict_id=77)]
     dsizes = [1 << 20, 3 * 65536, 4 * 65536, 4 * 65536, 1 << 20,
               (1 << 20) + 100, (1 << 20) - 100, 65 * 65536, 4 * 65536, 4 * 65536]
-    st = _check(zs, oracle, gpu, frames, dsizes)
+    st = _check(zs, oracle, gpu, frames, dsizes, engine)
     # (the corrupt block may still decode: _check holds it to the oracle)
     assert st[-1] == 0 and st[1] != 0 and st[7] == 0
 
 
-def test_block_route_linked_and_big_blocks(gpu, zs, oracle):
+@pytest.mark.parametrize("engine", ["block", "one"])
+def test_block_route_linked_and_big_blocks(gpu, zs, oracle, engine):
     """Linked 64 KiB blocks (the reference writer's frames), 256 KiB blocks,
     frames of 64 blocks (the route's maximum) and 65 (the chunk parse), and a
     frame one byte past a block boundary: bytes == the generator."""
@@ -175,13 +182,14 @@ def test_block_route_linked_and_big_blocks(gpu, zs, oracle):
                 zs.lz4_seekable(data, 4 << 20), zs.lz4_seekable(data, (4 << 20) + 65536),
                 zs.lz4_seekable(data, 65537)):
         frames, dsizes = _frames_of(zs, img)
-        got, st = _decode(zs, gpu, frames, dsizes, "block")
+        got, st = _decode(zs, gpu, frames, dsizes, engine)
         assert all(s == 0 for s in st)
         assert b"".join(got) == data.tobytes()
 
 
+@pytest.mark.parametrize("engine", ["block", "one"])
 @pytest.mark.parametrize("case", ["1m_block4_offset0", "1m_block4_size_huge"])
-def test_block_route_reference_corruptions(gpu, zs, golden, case):
+def test_block_route_reference_corruptions(gpu, zs, golden, case, engine):
     """The reference fixtures' corruptions in block 4 of a 1 MiB frame (a
     zero match offset, which liblz4 decodes and the route hands to the wave
     kernel; a block size over the maximum): the route's statuses == the wave
@@ -191,7 +199,7 @@ def test_block_route_reference_corruptions(gpu, zs, golden, case):
     for at, v in rec["mutations"]:
         img[at] = v
     frames, dsizes = _frames_of(zs, np.frombuffer(bytes(img), np.uint8))
-    got, st = _decode(zs, gpu, frames, dsizes, "block")
+    got, st = _decode(zs, gpu, frames, dsizes, engine)
     got_w, st_w = _decode(zs, gpu, frames, dsizes, "wave")
     assert st == st_w
     for i, s in enumerate(st):

@@ -9,6 +9,9 @@ error strings on the single-frame read cases of tests/env_switch_probe.py.
   ZSEEK_FRAME_HELP=0  zstd one-frame route: no helper wave in the frame kernel
   ZSEEK_ONE_WAVES=4   LZ4 one-frame parse over four waves (round 4's shape)
   ZSEEK_ONE_ROUTE=0   no one-frame route (the throughput kernels)
+  ZSEEK_ONE_BIG=0     one-frame route, frames over 64 KiB: one sequential
+                      parse and the wave execute (round 5) instead of the
+                      job parse and the windowed execute
 """
 from __future__ import annotations
 
@@ -22,7 +25,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SWITCHES = ["ZSEEK_HOST_DMA=1", "ZSEEK_ONE_FUSE=0", "ZSEEK_FRAME_HELP=0", "ZSEEK_ONE_WAVES=4",
-            "ZSEEK_ONE_ROUTE=0"]
+            "ZSEEK_ONE_ROUTE=0", "ZSEEK_ONE_BIG=0"]
 
 
 def _probe(env_kv=None):
