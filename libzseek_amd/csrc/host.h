@@ -135,6 +135,12 @@ struct Slot {
     size_t f0 = 0, f1 = 0;
     uint64_t h_from = 0, h_len = 0;   // batch-span bytes copied into h_out
     CopyTicket copies;                // h_out -> caller, still running
+    // completion flag (download_flagged): the pinned word past the status
+    // words (h_status's slack) that the batch's download sets to `seq`;
+    // flagged: this batch posts it
+    uint32_t seq = 0;
+    bool flagged = false;
+    volatile uint32_t *h_flag = nullptr;
 
     bool reserve(size_t comp, size_t out, size_t host_out, size_t nframes, bool ck, char *errbuf);
     void destroy();

@@ -83,7 +83,57 @@ __global__ __launch_bounds__(kUpT) void d2h_small_kernel(uint32_t *__restrict__ 
     hout[t] = v;
 }
 
+// The same download with the batch's completion posted to the host: one
+// 1,024-thread workgroup writes everything (<= kFlagMax bytes), each wave
+// waits for its stores and releases them at system scope, then, after the
+// barrier, thread 0 writes `seq` to the pinned flag -- the reader spins on
+// that word instead of waiting for the stream's completion signal (the
+// kernel's end, the end-of-pipe flush, the signal, the runtime's wake-up).
+constexpr uint32_t kFlagT = 1024;
+__global__ __launch_bounds__(kFlagT) void d2h_flag_kernel(uint32_t *__restrict__ hst, const uint32_t *__restrict__ dst_,
+                                                          uint32_t nst, u32x4 *__restrict__ hout,
+                                                          const uint8_t *__restrict__ src, uint32_t len,
+                                                          uint32_t *__restrict__ hflag, uint32_t seq)
+{
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < nst; i += kFlagT)
+        hst[i] = dst_[i];
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
+    for (uint32_t i = t; 16 * i < len; i += kFlagT) {
+        const uint32_t *a = reinterpret_cast<const uint32_t *>(src - sh) + 4 * i;
+        uint32_t d[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            d[k] = a[k];
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+        v.y = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+        v.z = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+        v.w = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+        hout[i] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // (system scope: this wave's stores complete)
+    __syncthreads();
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(hflag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 }   // namespace
+
+int download_flagged(uint32_t *h_status, void *hs, const uint32_t *d_status, uint32_t nst, uint8_t *h_out, void *ho,
+                     const uint8_t *d_src, size_t len, void *hflag_dev, uint32_t seq, hipStream_t stream)
+{
+    if (!hs || !hflag_dev || len > kFlagMax || nst > kFlagMaxStatus ||
+        (len && (!ho || (reinterpret_cast<uintptr_t>(ho) & 15))))
+        return 1;
+    hipLaunchKernelGGL(d2h_flag_kernel, dim3(1), dim3(kFlagT), 0, stream, static_cast<uint32_t *>(hs), d_status, nst,
+                       static_cast<u32x4 *>(ho), d_src, (uint32_t)len, static_cast<uint32_t *>(hflag_dev), seq);
+    (void)h_status;
+    (void)h_out;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int download_small(uint32_t *h_status, void *hs, const uint32_t *d_status, uint32_t nst, uint8_t *h_out, void *ho,
                    const uint8_t *d_src, size_t len, hipStream_t stream)

@@ -500,13 +500,13 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // decode's first kernel, host_io.hip; env ZSEEK_HOST_DMA=1: always DMA,
     // the download too)
     static const bool host_dma = getenv("ZSEEK_HOST_DMA") != nullptr;
+    // (the LZ4 two-phase decoder's plan kernel initializes both itself, the
+    // zstd sequence kernel writes both for every frame)
+    const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
     if (host_dma)
         e = hipMemcpyAsync(s.d_comp, s.h_comp, up, hipMemcpyHostToDevice, s.stream);
     else if (upload_small(s.d_comp, s.h_comp, s.h_comp_dev, up, s.stream) != 0)
         e = hipErrorLaunchFailure;
-    // (the LZ4 two-phase decoder's plan kernel initializes both itself, the
-    // zstd sequence kernel writes both for every frame)
-    const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
     const bool preset = r->type == ZSEEK_LZ4 && !lz4_split;
     if (e == hipSuccess && preset)
         e = hipMemsetD32Async((hipDeviceptr_t)s.d_status, ST_NOT_RUN, n, s.stream);
@@ -556,11 +556,33 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         e = hipMemcpyAsync(s.h_status, s.d_status, 2 * n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
         if (e == hipSuccess && s.h_len)
             e = hipMemcpyAsync(s.h_out, s.d_out + s.h_from, s.h_len, hipMemcpyDeviceToHost, s.stream);
-    } else if (e == hipSuccess &&
-               download_small(reinterpret_cast<uint32_t *>(s.h_status), s.h_status_dev,
-                              reinterpret_cast<const uint32_t *>(s.d_status), (uint32_t)(2 * n), s.h_out, s.h_out_dev,
-                              s.d_out + s.h_from, s.h_len, s.stream) != 0) {
-        e = hipErrorLaunchFailure;
+    } else if (e == hipSuccess) {
+        // a small batch posts its completion to a pinned word the host spins
+        // on (finish); env ZSEEK_DONE_FLAG=0: the stream's event only
+        static const bool no_flag = [] {
+            const char *v = getenv("ZSEEK_DONE_FLAG");
+            return v && !strcmp(v, "0");
+        }();
+        int rc = 1;
+        s.flagged = false;
+        if (!no_flag && s.h_status_dev) {
+            // the word past the 2n status words: in h_status's 256-byte slack
+            // (cleared first: the word may hold an older batch's fail_at)
+            s.h_flag = reinterpret_cast<volatile uint32_t *>(s.h_status + 2 * n);
+            *s.h_flag = 0;
+            s.seq = s.seq + 1 ? s.seq + 1 : 1;
+            rc = download_flagged(reinterpret_cast<uint32_t *>(s.h_status), s.h_status_dev,
+                                  reinterpret_cast<const uint32_t *>(s.d_status), (uint32_t)(2 * n), s.h_out,
+                                  s.h_out_dev, s.d_out + s.h_from, s.h_len,
+                                  reinterpret_cast<uint32_t *>(s.h_status_dev) + 2 * n, s.seq, s.stream);
+            s.flagged = rc == 0;
+        }
+        if (rc == 1)
+            rc = download_small(reinterpret_cast<uint32_t *>(s.h_status), s.h_status_dev,
+                                reinterpret_cast<const uint32_t *>(s.d_status), (uint32_t)(2 * n), s.h_out,
+                                s.h_out_dev, s.d_out + s.h_from, s.h_len, s.stream);
+        if (rc != 0)
+            e = hipErrorLaunchFailure;
     }
     if (e == hipSuccess)
         e = hipEventRecord(s.done, s.stream);
@@ -594,8 +616,24 @@ bool finish(LaneJob &J, Slot &s)
     const uint64_t ht2 = ht_now();
 #endif
     // (hipEventSynchronize: polling hipEventQuery instead for a small batch
-    // measured no better, LZ4 4 KiB p50 85.6-86.2 against 83.5-84.4 us)
-    hipError_t e = hipEventSynchronize(s.done);
+    // measured no better, LZ4 4 KiB p50 85.6-86.2 against 83.5-84.4 us.)
+    // A flagged batch: spin on its pinned completion word -- posted once its
+    // download is in host memory -- asking the event every 256 spins, so a
+    // batch that fails before the download (no flag ever) still ends
+    hipError_t e = hipErrorNotReady;
+    if (s.flagged) {
+        for (uint32_t k = 0;; k++) {
+            if (__atomic_load_n(s.h_flag, __ATOMIC_ACQUIRE) == s.seq) {
+                e = hipSuccess;
+                break;
+            }
+            if ((k & 255) == 255 && hipEventQuery(s.done) != hipErrorNotReady)
+                break;
+            __builtin_ia32_pause();
+        }
+    }
+    if (e != hipSuccess)
+        e = hipEventSynchronize(s.done);
 #ifdef ZSK_TUNING
     g_ht[2] += ht_now() - ht2;
     struct HtAfter {

@@ -303,6 +303,16 @@ int upload_small(void *d_dst, const void *h_src, const void *h_src_dev, size_t b
 constexpr size_t kDownloadSmallMax = 256u << 10;
 int download_small(uint32_t *h_status, void *h_status_dev, const uint32_t *d_status, uint32_t nst, uint8_t *h_out,
                    void *h_out_dev, const uint8_t *d_src, size_t len, hipStream_t stream);
+// ... or, for a request's small batch, as one workgroup that then writes
+// `seq` to a pinned word (hflag_dev: its device mapping) once every byte is
+// in host memory: the host may spin on it instead of synchronizing with the
+// stream.  0 (flag posted at the end), 1 (too big: nothing launched, use
+// download_small), -1.
+constexpr size_t kFlagMax = 64u << 10;
+constexpr uint32_t kFlagMaxStatus = 4096;
+int download_flagged(uint32_t *h_status, void *h_status_dev, const uint32_t *d_status, uint32_t nst, uint8_t *h_out,
+                     void *h_out_dev, const uint8_t *d_src, size_t len, void *hflag_dev, uint32_t seq,
+                     hipStream_t stream);
 // plan + synchronize + reserve + decode (stop_last as launch_zstd_decode)
 int zstd_decode_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                        uint8_t *d_out, int32_t *d_status, ZstdScratch *s, hipStream_t stream,

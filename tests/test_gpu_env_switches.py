@@ -12,6 +12,8 @@ error strings on the single-frame read cases of tests/env_switch_probe.py.
   ZSEEK_ONE_BIG=0     one-frame route, frames over 64 KiB: one sequential
                       parse and the wave execute (round 5) instead of the
                       job parse and the windowed execute
+  ZSEEK_DONE_FLAG=0   a small batch's completion by the stream's event only
+                      (no pinned completion word)
 """
 from __future__ import annotations
 
@@ -25,7 +27,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SWITCHES = ["ZSEEK_HOST_DMA=1", "ZSEEK_ONE_FUSE=0", "ZSEEK_FRAME_HELP=0", "ZSEEK_ONE_WAVES=4",
-            "ZSEEK_ONE_ROUTE=0", "ZSEEK_ONE_BIG=0"]
+            "ZSEEK_ONE_ROUTE=0", "ZSEEK_ONE_BIG=0", "ZSEEK_DONE_FLAG=0"]
 
 
 def _probe(env_kv=None):
