@@ -570,8 +570,10 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route)
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                      hipStream_t stream, SplitScratch *s, int route, int stages, int tune, uint32_t stop_last,
-                     uint32_t max_dsize)
+                     uint32_t max_dsize, const HostPost *post, bool *posted)
 {
+    if (posted)
+        *posted = false;
     if (nframes == 0)
         return 0;
     if (s->frames_cap < nframes || !s->rec_base || !s->redo)
@@ -648,8 +650,13 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
             // no bigger frame and the hand-off stage is asked for: no
             // hand-off launch below)
             frame_handoff = (stages & 8) && (max_dsize <= 65536 || big);
+            // a lone frame posts its results to the host itself (no download)
+            const bool post_here = post && frame_handoff && nframes == 1 && !big;
             launch_seq_exec_frames(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                                   d_fail_at, stream, stop_last, frame_handoff);
+                                   d_fail_at, stream, stop_last, frame_handoff, nullptr,
+                                   post_here ? post : nullptr);
+            if (post_here && posted)
+                *posted = true;
             if (big)
                 launch_seq_exec_big(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
                                     d_fail_at, stream, stop_last, frame_handoff, s);

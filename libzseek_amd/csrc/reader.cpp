@@ -500,6 +500,13 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
     // decode's first kernel, host_io.hip; env ZSEEK_HOST_DMA=1: always DMA,
     // the download too)
     static const bool host_dma = getenv("ZSEEK_HOST_DMA") != nullptr;
+    // env ZSEEK_DONE_FLAG=0: a batch's completion by the stream's event only
+    // (no pinned completion word, no results posted by the execute)
+    static const bool no_flag = [] {
+        const char *v = getenv("ZSEEK_DONE_FLAG");
+        return v && !strcmp(v, "0");
+    }();
+    s.flagged = false;
     // (the LZ4 two-phase decoder's plan kernel initializes both itself, the
     // zstd sequence kernel writes both for every frame)
     const bool lz4_split = r->type == ZSEEK_LZ4 && lz4_pick_engine((uint32_t)n) != ENGINE_WAVE;
@@ -528,9 +535,33 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         } else if (split_scratch_reserve(&s.split, (uint32_t)n, split_items_needed(h_desc, (uint32_t)n),
                                          s.stream) != 0) {
             e = hipErrorOutOfMemory;
-        } else if (launch_lz4_split(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, d_fail,
-                                    s.stream, &s.split, ROUTE_AUTO, 15, 0, stop_last, max_dsize) != 0) {
-            e = hipErrorLaunchFailure;
+        } else {
+            // a lone frame with a host destination (or none): its execute
+            // writes the status words, the bytes and the completion word
+            // itself when it takes the one-frame route (no download kernel)
+            HostPost post;
+            const bool want_post = n == 1 && !host_dma && !no_flag && !ck && br.route != COPY_DEVICE &&
+                                   br.route != COPY_PEER && s.h_status_dev &&
+                                   (!s.h_len || (s.h_out_dev && !(reinterpret_cast<uintptr_t>(s.h_out_dev) & 15)));
+            if (want_post) {
+                if (s.h_len)
+                    pool_wait(&s.copies);   // (the execute writes h_out)
+                s.h_flag = reinterpret_cast<volatile uint32_t *>(s.h_status + 2 * n);
+                *s.h_flag = 0;
+                s.seq = s.seq + 1 ? s.seq + 1 : 1;
+                post.h_status = reinterpret_cast<uint32_t *>(s.h_status_dev);
+                post.h_out = static_cast<uint8_t *>(s.h_out_dev);
+                post.h_from = (uint32_t)s.h_from;
+                post.h_len = (uint32_t)s.h_len;
+                post.h_flag = reinterpret_cast<uint32_t *>(s.h_status_dev) + 2 * n;
+                post.seq = s.seq;
+            }
+            bool posted = false;
+            if (launch_lz4_split(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, d_fail, s.stream, &s.split,
+                                 ROUTE_AUTO, 15, 0, stop_last, max_dsize, want_post ? &post : nullptr,
+                                 &posted) != 0)
+                e = hipErrorLaunchFailure;
+            s.flagged = posted;
         }
     }
     // seek-table checksums (descriptor bit 7) when asked for: XXH64 low 32
@@ -552,19 +583,16 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
         e = hipMemcpyPeerAsync(J.buf + br.dst_off, J.dst_dev, s.d_out + br.src_off, g.device, br.len, s.stream);
     if (e == hipSuccess && s.h_len)
         pool_wait(&s.copies);
-    if (e == hipSuccess && host_dma) {
+    if (e == hipSuccess && s.flagged) {
+        // (posted by the execute: nothing to download)
+    } else if (e == hipSuccess && host_dma) {
         e = hipMemcpyAsync(s.h_status, s.d_status, 2 * n * sizeof(int32_t), hipMemcpyDeviceToHost, s.stream);
         if (e == hipSuccess && s.h_len)
             e = hipMemcpyAsync(s.h_out, s.d_out + s.h_from, s.h_len, hipMemcpyDeviceToHost, s.stream);
     } else if (e == hipSuccess) {
         // a small batch posts its completion to a pinned word the host spins
-        // on (finish); env ZSEEK_DONE_FLAG=0: the stream's event only
-        static const bool no_flag = [] {
-            const char *v = getenv("ZSEEK_DONE_FLAG");
-            return v && !strcmp(v, "0");
-        }();
+        // on (finish)
         int rc = 1;
-        s.flagged = false;
         if (!no_flag && s.h_status_dev) {
             // the word past the 2n status words: in h_status's 256-byte slack
             // (cleared first: the word may hold an older batch's fail_at)

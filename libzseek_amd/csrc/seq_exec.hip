@@ -104,7 +104,7 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     int32_t *__restrict__ status, uint32_t *__restrict__ fail_at, uint32_t stop_last, uint32_t handoff,
-    const uint8_t *__restrict__ lit)
+    const uint8_t *__restrict__ lit, const HostPost post)
 {
     __shared__ __attribute__((aligned(16))) uint8_t ob[kFMax + 80];
     __shared__ __attribute__((aligned(16))) uint8_t cs[kFCStage + 80];
@@ -121,8 +121,35 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
         // the hand-off (handoff != 0): the wave decoder of lz4_wave_kernel on
         // wave 0, its ring in the stage -- the batch then launches no
         // hand-off kernel (5 us + a launch gap per one-frame miss)
-        if (handoff && wv == 0)
+        if (handoff && wv == 0) {
             lz4w::wave_frame<4096>(desc, f, comp, out, status, fail_at, ob);
+            if (post.h_flag) {
+                // (post: wave 0's decoded bytes, from HBM, then its status)
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+                const uint8_t *src = out + d.d_off + post.h_from;
+                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
+                for (uint32_t c = lane; 16 * c < post.h_len; c += 64) {
+                    const uint32_t *a = reinterpret_cast<const uint32_t *>(src - sh) + 4 * c;
+                    uint32_t w[5];
+#pragma unroll
+                    for (int k = 0; k < 5; k++)
+                        w[k] = a[k];
+                    u32x4 v;
+                    v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+                    v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+                    v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+                    v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+                    reinterpret_cast<u32x4 *>(post.h_out)[c] = v;
+                }
+                if (lane == 0) {
+                    post.h_status[0] = (uint32_t)status[f];
+                    post.h_status[1] = fail_at ? fail_at[f] : 0u;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                if (lane == 0)
+                    __hip_atomic_store(post.h_flag, post.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
         return;
     }
     const uint32_t nit = nitems[f];
@@ -364,6 +391,23 @@ __global__ __launch_bounds__(kFT) void seq_exec_frame_kernel(
     const uint32_t tail0 = head + 16 * nchunks;
     if (tail0 + t < E)
         o[tail0 + t] = ob[tail0 + t];
+    if (post.h_flag) {
+        // a lone frame's results to the host from the staged output (the
+        // request's bytes; past E they are whatever LDS holds, as HBM's would
+        // be), then the flag once every wave's stores are complete
+        for (uint32_t c = t; 16 * c < post.h_len; c += kFT)
+            reinterpret_cast<u32x4 *>(post.h_out)[c] = lds16(ob0 + post.h_from + 16 * c);
+        if (t == 0) {
+            post.h_status[0] = (uint32_t)status[f];
+            post.h_status[1] = fail_at ? fail_at[f] : 0u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __hip_atomic_store(post.h_flag, post.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 #ifdef ZSK_TUNING
     __syncthreads();
     ZSK_FT(4)
@@ -762,7 +806,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                            const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                            int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                           bool handoff, const uint8_t *lit)
+                           bool handoff, const uint8_t *lit, const HostPost *post)
 {
     if (nframes == 0)
         return 0;
@@ -777,8 +821,10 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fdiag), &fd, sizeof(fd), 0, hipMemcpyHostToDevice, stream);
     }
 #endif
+    // (post: one frame, host-checked; its hand-off decoded here)
+    const HostPost hp = post && nframes == 1 && handoff && !lit ? *post : HostPost{};
     hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
-                       rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff && !lit ? 1u : 0u, lit);
+                       rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff && !lit ? 1u : 0u, lit, hp);
 #ifdef ZSK_TUNING
     if (timers && ++calls % 100 == 0) {
         unsigned long long z[8] = {0};
@@ -832,7 +878,7 @@ int launch_seq_exec_lit(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
         return 0;
     if (one) {   // frames of <= 64 KiB a workgroup each, bigger ones a wave
         hipLaunchKernelGGL(seq_exec_frame_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, nullptr,
-                           d_out, rec_base, items, nitems, d_status, nullptr, stop_last, 0u, lit);
+                           d_out, rec_base, items, nitems, d_status, nullptr, stop_last, 0u, lit, HostPost{});
         if (max_dsize <= kFMax)
             return hipGetLastError() == hipSuccess ? 0 : -1;
     }

@@ -150,12 +150,27 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route = ROU
 // frames' item slots; frames that do not fit are decoded by the wave kernel).
 // stages: bitmask 1 plan, 2 parse, 4 execute, 8 hand-offs (tuning builds
 // time subsets).
+// A lone frame's results straight into the reader's pinned buffers from the
+// one-frame route's execute (no download kernel, no launch behind it): its
+// status and fail_at to h_status[0..1], decoded bytes [h_from, h_from +
+// h_len) to h_out (16-aligned, 15 bytes of slack), then `seq` to h_flag --
+// the device mappings of the slot's buffers (download_flagged's word).
+struct HostPost {
+    uint32_t *h_status = nullptr;
+    uint8_t *h_out = nullptr;
+    uint32_t h_from = 0, h_len = 0;
+    uint32_t *h_flag = nullptr;
+    uint32_t seq = 0;
+};
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                      hipStream_t stream, SplitScratch *s, int route = ROUTE_AUTO, int stages = 15,
-                     int tune = 0, uint32_t stop_last = 0xFFFFFFFFu, uint32_t max_dsize = 0xFFFFFFFFu);
+                     int tune = 0, uint32_t stop_last = 0xFFFFFFFFu, uint32_t max_dsize = 0xFFFFFFFFu,
+                     const HostPost *post = nullptr, bool *posted = nullptr);
 // (max_dsize: the batch's largest decoded frame when the caller knows it --
-// the one-frame route then skips the wave execute for frames of <= 64 KiB)
+// the one-frame route then skips the wave execute for frames of <= 64 KiB.
+// post: a one-frame batch's results to the host from its execute, when the
+// batch takes that route (*posted = true; else the caller downloads))
 
 // Item slots of a frame in the split decoder's scratch.  An item is 8 bytes;
 // a sequence takes one (two when extended), a stored block two.  LZ4 data
@@ -214,7 +229,7 @@ int launch_seq_exec(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_
 int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                            const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                            int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                           bool handoff, const uint8_t *lit = nullptr);
+                           bool handoff, const uint8_t *lit = nullptr, const HostPost *post = nullptr);
 // ... and its frames of more than 64 KiB (the one-frame route's big frames):
 // one per workgroup through a sliding 64 KiB window, items job by job for a
 // frame the block route accepted (blk, may be null); handoff as above.

@@ -13,7 +13,8 @@ error strings on the single-frame read cases of tests/env_switch_probe.py.
                       parse and the wave execute (round 5) instead of the
                       job parse and the windowed execute
   ZSEEK_DONE_FLAG=0   a small batch's completion by the stream's event only
-                      (no pinned completion word)
+                      (no pinned completion word, no results posted by the
+                      one-frame execute)
 """
 from __future__ import annotations
 
