@@ -745,17 +745,21 @@ __global__ __launch_bounds__(64 * (ONE ? OW : kCW)) void lz4_chunk_kernel(
                         nitems[f] = total;
                         if (fail_at)
                             fail_at[f] = 0;
-                    } else {
+                    } else if (!ONE) {
                         bfirst[f] = kNoJob;
                     }
                 }
             }
             if constexpr (ONE) {
+                // (the job list dropped only once every wave has read it: a
+                // wave reading kNoJob would skip these barriers)
                 if (threadIdx.x == 0)
                     coll[3 * kOneLanes + 15] = take ? 1u : 0u;
                 __syncthreads();
                 take = coll[3 * kOneLanes + 15] != 0;
                 __syncthreads();
+                if (!take && threadIdx.x == 0)
+                    bfirst[f] = kNoJob;
             }
             if (take)
                 return;
