@@ -21,6 +21,10 @@ namespace zsk {
 
 namespace {
 
+// traffic split (tuning only): round 0's literal pieces / HBM match pieces
+// not loaded (zeros staged instead: the output is not checked)
+constexpr int kDiagNoLit = 1 << 23, kDiagNoMatch = 1 << 24;
+
 __device__ unsigned long long g_xstats[12];   // DIAG 16: cycles per section, counts
 
 // Copy, for every lane, a literal run (lit bytes of the literal source at src
@@ -280,7 +284,10 @@ __device__ __forceinline__ void copy_desc4(const Stage &S, const uint8_t *lbase,
             dw[j] = on ? (uint32_t)(D >> 32) : 0;
             const uint32_t kind = dw[j] >> 24;
             const uint8_t *p = kind == K_HBM ? obase + sx[j] : lbase + (kind == K_LIT ? sx[j] : 0);
-            v[j] = (DIAG & 1) ? (u32x4){0, 0, 0, 0} : *reinterpret_cast<const u32x4_l *>(p);
+            // (traffic split: kDiagNoLit / kDiagNoMatch leave one kind's pieces unloaded)
+            const bool skip = (DIAG & 1) || ((DIAG & kDiagNoLit) && kind == K_LIT) ||
+                              ((DIAG & kDiagNoMatch) && kind == K_HBM);
+            v[j] = skip ? (u32x4){0, 0, 0, 0} : *reinterpret_cast<const u32x4_l *>(p);
             if (t0 + 64 * j + 64 >= TT)
                 break;
         }
@@ -1081,6 +1088,8 @@ int launch_seq_exec_variant(int version, const FrameDesc *d_desc, uint32_t nfram
     case 0x360: ZSK_X(24576); break;  // both
     case 0x380: ZSK_X(32768); break;  // round 0: long runs' descriptors by the whole wave (-0.8 % at 6 waves, +0.5 % at 7)
     case 0x400: ZSK_X(65536); break;  // round 0 direct (copy_direct)
+    case 0x810: ZSK_X(kDiagNoLit); break;     // traffic split: no literal piece loads
+    case 0x811: ZSK_X(kDiagNoMatch); break;   // traffic split: no HBM match piece loads
     case 0x700: ZSK_X(kDiagEntries); break;   // round 0 and rounds in 64-byte entries
     case 0x703: ZSK_X(kDiagE0); break;        // round 0 only
     case 0x704: ZSK_X(kDiagER); break;        // the rounds only

@@ -121,6 +121,8 @@ int launch_lz4_frames_variant(int variant, const FrameDesc *d_desc, uint32_t nfr
         return staged(15, ROUTE_AUTO, 0, d_desc, nframes, d_comp, d_out, d_status, stream);
     if ((variant & 0xF00) == 0x700)   // execute alone, round-6 candidates (seq_exec.hip 0x7xx)
         return staged(4, ROUTE_AUTO, (variant & 0xFFF) << 8, d_desc, nframes, d_comp, d_out, d_status, stream);
+    if ((variant & 0xF00) == 0x800)   // execute alone, traffic split (seq_exec_tune.hip 0x81x)
+        return staged(4, ROUTE_AUTO, (variant & 0xFFF) << 8, d_desc, nframes, d_comp, d_out, d_status, stream);
     if ((variant & 0xF00) == 0x600)   // execute alone at W = variant & 0xF waves per SIMD (LDS padding)
         return staged(4, ROUTE_AUTO, (variant & 0xFFF) << 8, d_desc, nframes, d_comp, d_out, d_status, stream);
     if ((variant & 0xF00) == 0x500)   // plan, then K = variant & 0xFF chunks: parse beside the execute

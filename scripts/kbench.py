@@ -72,7 +72,7 @@ def main():
         assert rc == 0, f"variant {v} launch failed"
 
     # stage subsets and diagnostic builds: timing only, output not complete
-    diag = set(range(10, 16)) | {20} | set(range(0x100, 0x400))
+    diag = set(range(10, 16)) | {20} | set(range(0x100, 0x400)) | set(range(0x800, 0x900))
 
     for v in variants:   # correctness once per variant
         out.zero_()
