@@ -38,7 +38,9 @@
 //
 // One-frame route (ONE, batches of <= 64 frames): one frame per workgroup,
 // staged whole in LDS, and pass 1 records each lane's first tokens with the
-// counts before them so the count pass is skipped (below).
+// counts before them so the count pass is skipped (below).  Its frames of
+// more than 64 KiB: each 64 KiB block a workgroup of lz4_job_parse_kernel
+// (below), accepted or re-parsed by the one-frame kernel.
 //
 // Output: the items of lz4_scan.hip (8 bytes per sequence, two when a run is
 // longer than the small form holds) at rec_base[f], without the padding item

@@ -1,5 +1,7 @@
 // seq_exec.hip — the execute phase's launchers and the one-frame route's
-// execute (gfx950).  The throughput kernel seq_exec_kernel<OUTB, SEG> and its
+// executes (gfx950): seq_exec_frame_kernel (a frame of <= 64 KiB staged whole
+// in LDS per workgroup) and seq_exec_big_kernel (bigger frames through a
+// sliding 64 KiB window).  The throughput kernel seq_exec_kernel<OUTB, SEG> and its
 // helpers live in seq_exec_dev.h (shared with seq_exec_seg.hip and the
 // tuning build's seq_exec_tune.hip, which holds the diagnostic variants).
 #include <hip/hip_runtime.h>
