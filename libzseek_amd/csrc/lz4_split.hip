@@ -657,9 +657,18 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                                    post_here ? post : nullptr);
             if (post_here && posted)
                 *posted = true;
+            // (the accepted frames block-parallel, the others through the
+            // window; env ZSEEK_ONE_BLOCKS=0: all through the window)
+            static const bool blocks_off = [] {
+                const char *v = getenv("ZSEEK_ONE_BLOCKS");
+                return v && !strcmp(v, "0");
+            }();
+            if (big && !blocks_off)
+                launch_seq_exec_blocks(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, stream, stop_last, s,
+                                       jlanes);
             if (big)
                 launch_seq_exec_big(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                                    d_fail_at, stream, stop_last, frame_handoff, s);
+                                    d_fail_at, stream, stop_last, frame_handoff, s, !blocks_off);
             else if (max_dsize > 65536)
                 launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status, stream,
                                 0, nullptr, stop_last, 65537);

@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kFT) void seq_exec_big_kernel(
     const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items, const uint32_t *__restrict__ nitems,
     int32_t *__restrict__ status, uint32_t *__restrict__ fail_at, uint32_t stop_last, uint32_t handoff,
     const uint32_t *__restrict__ bfirst, const uint32_t *__restrict__ bcount, const BlockJob *__restrict__ jobs,
-    const BlockRes *__restrict__ jres)
+    const BlockRes *__restrict__ jres, uint32_t skip_jobs)
 {
     __shared__ __attribute__((aligned(16))) uint8_t ob[2 * kBWin + 80];
     __shared__ uint32_t done[kBWin / 32 + 2];
@@ -475,12 +475,15 @@ __global__ __launch_bounds__(kFT) void seq_exec_big_kernel(
     const FrameDesc d = desc[f];
     if (d.d_size <= kFMax)
         return;   // seq_exec_frame_kernel's frame
+    // (skip_jobs: a frame the block route accepted is seq_exec_blocks_kernel's)
+    if (skip_jobs && bfirst && (uint32_t)__builtin_amdgcn_readfirstlane(bfirst[f]) != kNoJob)
+        return;
     // the windowed execute; false: stuck (an item longer than the window)
     auto window_frame = [&]() -> bool {
-    #ifdef ZSK_TUNING
-    uint64_t tmark_ = __builtin_readcyclecounter();
+#ifdef ZSK_TUNING
+        uint64_t tmark_ = __builtin_readcyclecounter();
 #endif
-    const uint32_t j0 = bfirst ? __builtin_amdgcn_readfirstlane(bfirst[f]) : kNoJob;
+        const uint32_t j0 = bfirst ? __builtin_amdgcn_readfirstlane(bfirst[f]) : kNoJob;
         const uint32_t nj = j0 != kNoJob ? __builtin_amdgcn_readfirstlane(bcount[f]) : 0u;
         uint32_t nit;
         if (nj) {
@@ -773,6 +776,372 @@ __global__ __launch_bounds__(kFT) void seq_exec_big_kernel(
     }
 }
 
+// ---- the one-frame route's big frames, block-parallel (round 6) ----
+// A frame the block route accepted (64 KiB linked blocks, each block's items
+// in its job's slots) is executed a block per 1,024-thread workgroup, all
+// blocks at once.  A block's matches may read up to 64 KiB back, i.e. the
+// previous block's output, which its own workgroup is still producing; so:
+//   A. every workgroup executes its block at once with the previous block's
+//      bytes unknown: the frame kernel's literal copies and match passes over
+//      the block staged in LDS (block bytes [0, 64 KiB) at B; below B the
+//      history, garbage for now), a source byte before the block taken as
+//      ready and as *tainted*, and every match reading a tainted byte
+//      tainting its own (one bit per byte, set before the done bit, so a
+//      match that sees its source done sees its taint too) and going on a
+//      list in LDS;
+//   B. a block without tainted matches is final already; one with them waits
+//      for the previous block's workgroup to publish its final bytes
+//      (jres[j - 1].pad, release / acquire at agent scope), loads them as its
+//      history and re-runs just the listed matches, every untainted byte
+//      ready.  (A list past its capacity: the whole block again, after the
+//      wait.)
+// Workgroups wait only on lower-numbered ones, dispatched first, so the
+// chain always drains; the wait is bounded (~1 s) so a broken chain cannot
+// hang the GPU.  Tainted matches sit in a block's first bytes (its matches
+// reaching back) and whatever copies them, so the chain's serial part is
+// short.  The last frame stops at stop_last (later blocks skip).
+constexpr uint32_t kTaintList = 1024;   // tainted matches a block keeps (8 bytes each)
+
+#ifdef ZSK_TUNING
+// tuning builds: seq_exec_blocks_kernel's timeline (ZSEEK_BLK_TIMERS), per
+// job < 64: realtime at start, after phase A, after the wait, at the end;
+// the tainted matches and bytes
+__device__ unsigned long long g_ktime[64][6];
+#define ZSK_KT(i)                                                             \
+    if (t == 0 && j < 64)                                                     \
+        g_ktime[j][i] = __builtin_amdgcn_s_memrealtime();
+#else
+#define ZSK_KT(i)
+#endif
+static_assert(kTaintList == kFT, "phase B takes one listed match per thread");
+
+__global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
+    const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
+    const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items,
+    const uint32_t *__restrict__ bfirst, const BlockJob *__restrict__ jobs, BlockRes *__restrict__ jres,
+    const uint32_t *__restrict__ njobs, uint32_t stop_last)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t ob[2 * kBWin + 80];   // history, then the block
+    __shared__ uint32_t done[kBWin / 32 + 2];
+    __shared__ uint32_t taint[kBWin / 32 + 2];
+    __shared__ uint64_t tl[kTaintList];
+    __shared__ uint32_t wsum[kFT / 64];
+    __shared__ uint32_t ntl, hi_end;
+    const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (j >= (uint32_t)__builtin_amdgcn_readfirstlane(*njobs))
+        return;
+    const BlockJob J = jobs[j];
+    if (J.f == kNoJob || J.f >= n)
+        return;
+    const uint32_t f = J.f;
+    const uint32_t j0 = __builtin_amdgcn_readfirstlane(bfirst[f]);
+    if (j0 == kNoJob)
+        return;   // re-parsed: seq_exec_big_kernel's frame
+    const FrameDesc d = desc[f];
+    const uint32_t stop = f + 1 == n ? min(stop_last, d.d_size) : d.d_size;
+    const uint32_t bop = J.bop;
+    auto publish = [&]() {   // this block's bytes are final
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (t == 0)
+            __hip_atomic_store(&jres[j].pad, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (bop >= stop) {
+        publish();
+        return;
+    }
+    ZSK_KT(0)
+    const uint32_t lim = min(stop - bop, kBWin);   // block bytes the request needs
+    const uint32_t nit = jres[j].n;
+    const uint64_t *it = items + rec_base[f] + J.slot_off;
+    const Span lsp = make_span(comp + d.c_off, d.c_size);
+    const uint32_t ob0 = (uint32_t)(uintptr_t)ob, B = ob0 + kBWin;   // block byte x at B + x
+    for (uint32_t i = t; i < kBWin / 32 + 2; i += kFT)
+        done[i] = taint[i] = 0;
+    if (t == 0) {
+        hi_end = 0;
+        ntl = 0;
+    }
+    __syncthreads();
+
+    auto scan = [&](uint32_t v, uint32_t &total) -> uint32_t {   // exclusive, in thread order
+        const uint32_t inc = wave_incl_add(v);
+        if (lane == 63)
+            wsum[wv] = inc;
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+        for (uint32_t k = 0; k < kFT / 64; k++) {
+            const uint32_t x = wsum[k];
+            before += k < wv ? x : 0;
+            tot += x;
+        }
+        __syncthreads();
+        total = tot;
+        return before + inc - v;
+    };
+    auto bits_or = [&](uint32_t *w, uint32_t a, uint32_t len) {
+        for (const uint32_t e = a + len; a < e;) {
+            const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
+            __hip_atomic_fetch_or(&w[a >> 5], nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            a += nb;
+        }
+    };
+    auto all_set = [&](uint32_t *w, uint32_t a, uint32_t len) -> bool {
+        bool all = true;
+        for (const uint32_t e = a + len; a < e;) {
+            const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
+            const uint32_t m = nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0;
+            all &= (__hip_atomic_load(&w[a >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & m) == m;
+            a += nb;
+        }
+        return all;
+    };
+    auto any_set = [&](uint32_t *w, uint32_t a, uint32_t len) -> bool {
+        bool any = false;
+        for (const uint32_t e = a + len; a < e;) {
+            const uint32_t b0 = a & 31, nb = min(32 - b0, e - a);
+            const uint32_t m = nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1) << b0;
+            any |= (__hip_atomic_load(&w[a >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & m) != 0;
+            a += nb;
+        }
+        return any;
+    };
+    auto mark = [&](uint32_t a, uint32_t len) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        bits_or(done, a, len);
+    };
+    // a match's copy inside the staged block (its source may reach into the
+    // history below B)
+    auto copy_match = [&](uint32_t mb, uint32_t ov, uint32_t m) {
+        const uint32_t db = B + mb, sb = db - ov;
+        if (ov >= m && m <= 128) {
+            scopy(db, sb, min(m, 64u));
+            if (m > 64)
+                scopy(db + 64, sb + 64, m - 64);
+        } else if (ov >= m || ov >= 16) {
+            lcopy(db, sb, m, ov >= m ? 64u : min(64u, ov & ~15u));
+        } else {
+            const uint32_t e = ov * ((16 + ov - 1) / ov);
+            const uint32_t h = min(e, m);
+            for (uint32_t k = 0; k < h; k++) {
+                *lp<uint8_t>(db + k) = *lp<uint8_t>(sb + k);
+                wave_lds_sync();
+            }
+            for (uint32_t k = h; k < m; k += 16) {
+                lds_put(db + k, lds16(db + k - e), min(16u, m - k));
+                wave_lds_sync();
+            }
+        }
+    };
+    // the readiness range of a match at mb: its source's first min(off, ml)
+    // bytes, clipped to the block (bytes before it: the history)
+    auto src_range = [&](uint32_t mb, uint32_t ov, uint32_t m, uint32_t &a, uint32_t &len) -> bool {
+        const int32_t s0 = (int32_t)mb - (int32_t)ov, s1 = s0 + (int32_t)(ov >= m ? m : ov);
+        a = s0 > 0 ? (uint32_t)s0 : 0u;
+        len = s1 > (int32_t)a ? (uint32_t)s1 - a : 0u;
+        return s0 < 0;   // reaches before the block
+    };
+
+    // ---- the block's items, batches of 2,048 (phase A, or the whole block
+    // again with the history in place: full) ----
+    auto run_items = [&](bool full) {
+        uint32_t P = 0;
+        for (uint32_t w0 = 0; w0 < nit && P < lim; w0 += 2 * kFT) {
+            uint32_t lit[2], ml[2], off[2], src[2], op[2], tot[2];
+            for (int q = 0; q < 2; q++) {
+                const uint32_t i = w0 + q * kFT + t;
+                lit[q] = ml[q] = off[q] = src[q] = 0;
+                if (i < nit) {
+                    const uint64_t cur = it[i];
+                    const uint32_t c0 = (uint32_t)cur, c1 = (uint32_t)(cur >> 32);
+                    const bool second = i > 0 && ((uint32_t)it[i - 1] & kItemExt);
+                    if (!second) {
+                        src[q] = c0 & kItemPos;
+                        if (c0 & kItemExt) {
+                            const uint64_t nx = it[i + 1];
+                            lit[q] = (uint32_t)nx;
+                            ml[q] = (uint32_t)(nx >> 32);
+                            off[q] = c1;
+                        } else {
+                            lit[q] = (c1 >> 16) & 0xFF;
+                            const uint32_t mc = c1 >> 24;
+                            ml[q] = mc ? mc + 3 : 0;
+                            off[q] = c1 & 0xFFFF;
+                        }
+                    }
+                }
+            }
+            const uint32_t x0 = scan(lit[0] + ml[0], tot[0]);
+            const uint32_t x1 = scan(lit[1] + ml[1], tot[1]);
+            op[0] = P + x0;
+            op[1] = P + tot[0] + x1;
+            bool pend[2];
+            for (int q = 0; q < 2; q++) {
+                const bool on = op[q] < lim && lit[q] + ml[q] != 0 && op[q] + lit[q] + ml[q] <= kBWin;
+                const uint32_t L = on ? lit[q] : 0;
+                const uint32_t dst = B + op[q];
+                const bool coop = L > kFLong;
+                for (uint64_t lm = __ballot(coop); lm; lm &= lm - 1) {
+                    const int qq = (int)__builtin_ctzll(lm);
+                    const uint32_t d0 = lane_val(dst, qq), sx = lane_val(src[q], qq), nq = lane_val(L, qq);
+                    for (uint32_t k = 16 * lane; k < nq; k += 1024)
+                        lds_put(d0 + k, load16u(lsp.r, lsp.s0 + sx + k), min(16u, nq - k));
+                }
+                if (!coop && L) {
+                    for (uint32_t k = 0; k < L; k += 64) {
+                        u32x4 v[4];
+#pragma unroll
+                        for (uint32_t qq = 0; qq < 4; qq++)
+                            v[qq] = load16u(lsp.r, k + 16 * qq < L ? lsp.s0 + src[q] + k + 16 * qq : kBad);
+#pragma unroll
+                        for (uint32_t qq = 0; qq < 4; qq++)
+                            if (k + 16 * qq < L)
+                                lds_put(dst + k + 16 * qq, v[qq], min(16u, L - k - 16 * qq));
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                for (uint64_t lm = __ballot(coop); lm; lm &= lm - 1) {
+                    const int qq = (int)__builtin_ctzll(lm);
+                    const uint32_t a = lane_val(op[q], qq), e = a + lane_val(L, qq) - 1;
+                    for (uint32_t g = (a >> 5) + lane; g <= e >> 5; g += 64) {
+                        const uint32_t lo = g == a >> 5 ? a & 31 : 0, hi = g == e >> 5 ? e & 31 : 31;
+                        const uint32_t m = hi - lo == 31 ? 0xFFFFFFFFu : ((1u << (hi - lo + 1)) - 1) << lo;
+                        __hip_atomic_fetch_or(&done[g], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                if (!coop && L)
+                    mark(op[q], L);
+                pend[q] = on && ml[q] != 0;
+            }
+            {
+                const bool on0 = op[0] < lim && lit[0] + ml[0] != 0, on1 = op[1] < lim && lit[1] + ml[1] != 0;
+                const uint32_t e = max(on0 ? op[0] + lit[0] + ml[0] : 0u, on1 ? op[1] + lit[1] + ml[1] : 0u);
+                const uint32_t we = wave_incl_max(e);
+                if (lane == 63 && we)
+                    atomicMax(&hi_end, we);
+            }
+            __syncthreads();
+            for (uint32_t pass = 0;; pass++) {
+                bool moved = false;
+                for (int q = 0; q < 2; q++) {
+                    if (!pend[q])
+                        continue;
+                    const uint32_t mb = op[q] + lit[q], ov = off[q], m = ml[q];
+                    uint32_t a, len;
+                    const bool before = src_range(mb, ov, m, a, len);
+                    if (len && !all_set(done, a, len))
+                        continue;
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    // phase A: bytes before the block, or tainted ones, taint it
+                    if (!full && (before || (len && any_set(taint, a, len)))) {
+                        bits_or(taint, mb, m);
+                        const uint32_t x = atomicAdd(&ntl, 1u);
+                        if (x < kTaintList)
+                            tl[x] = (uint64_t)mb | (uint64_t)m << 20 | (uint64_t)ov << 40;
+                    }
+                    copy_match(mb, ov, m);
+                    mark(mb, m);
+                    pend[q] = false;
+                    moved = true;
+                }
+                if (!__any(pend[0] || pend[1]) || pass > (1u << 22))
+                    break;
+                if (!__any(moved))
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            __syncthreads();
+            P += tot[0] + tot[1];
+        }
+    };
+    run_items(false);
+    __syncthreads();
+    const uint32_t nt = ntl;
+    ZSK_KT(1)
+    if (!nt)
+        ZSK_KT(2)
+#ifdef ZSK_TUNING
+    if (t == 0 && j < 64) {
+        uint32_t pc = 0;
+        for (uint32_t i = 0; i < kBWin / 32; i++)
+            pc += __builtin_popcount(taint[i]);
+        g_ktime[j][4] = nt;
+        g_ktime[j][5] = pc;
+    }
+#endif
+    if (nt) {
+        // phase B: the previous block's final bytes as the history (a block
+        // with tainted matches is never the frame's first: nothing reaches
+        // before byte 0)
+        if (t == 0 && j > j0) {
+            uint32_t k = 0;
+            while (__hip_atomic_load(&jres[j - 1].pad, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+                   k++ < (1u << 24))
+                __builtin_amdgcn_s_sleep(2);
+        }
+        __syncthreads();
+        ZSK_KT(2)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint8_t *prev = out + d.d_off + (bop - kBWin);
+        for (uint32_t c = t; c < kBWin / 16; c += kFT)
+            *lp<u32x4>(ob0 + 16 * c) = *reinterpret_cast<const u32x4_l *>(prev + 16 * c);
+        if (nt > kTaintList) {
+            // the list overflowed: the block again, the history in place
+            for (uint32_t i = t; i < kBWin / 32 + 2; i += kFT)
+                done[i] = 0;
+            if (t == 0)
+                hi_end = 0;
+            __syncthreads();
+            run_items(true);
+        } else {
+            // untainted bytes final, tainted ones pending: the listed matches
+            // again, in passes over the done bits
+            for (uint32_t i = t; i < kBWin / 32 + 2; i += kFT)
+                done[i] = ~taint[i];
+            __syncthreads();
+            // (kTaintList = kFT entries: one per thread)
+            bool pend = t < nt;
+            const uint64_t e = pend ? tl[t] : 0;
+            const uint32_t mb = (uint32_t)e & 0xFFFFF, m = (uint32_t)(e >> 20) & 0xFFFFF,
+                           ov = (uint32_t)(e >> 40) & 0xFFFFF;
+            for (uint32_t pass = 0;; pass++) {
+                bool moved = false;
+                if (pend) {
+                    uint32_t a, len;
+                    (void)src_range(mb, ov, m, a, len);
+                    if (!len || all_set(done, a, len)) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                        copy_match(mb, ov, m);
+                        mark(mb, m);
+                        pend = false;
+                        moved = true;
+                    }
+                }
+                if (!__any(pend) || pass > (1u << 22))
+                    break;
+                if (!__any(moved))
+                    __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+    }
+    // the block's decoded bytes out: a byte head to 16-byte alignment, whole
+    // 16-byte stores, a byte tail
+    const uint32_t E = min(hi_end, lim);
+    uint8_t *o = out + d.d_off + bop;
+    const uint32_t head = min(E, (uint32_t)((16 - ((uintptr_t)o & 15)) & 15));
+    if (t < head)
+        o[t] = ob[kBWin + t];
+    const uint32_t nchunks = (E - head) / 16;
+    for (uint32_t c = t; c < nchunks; c += kFT)
+        *reinterpret_cast<u32x4 *>(o + head + 16 * c) = lds16(B + head + 16 * c);
+    const uint32_t tail0 = head + 16 * nchunks;
+    if (tail0 + t < E)
+        o[tail0 + t] = ob[kBWin + tail0 + t];
+    publish();
+    ZSK_KT(3)
+}
+
 }   // namespace
 
 #ifdef ZSK_TUNING
@@ -845,14 +1214,14 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
 int launch_seq_exec_big(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                        bool handoff, const SplitScratch *blk)
+                        bool handoff, const SplitScratch *blk, bool skip_jobs)
 {
     if (nframes == 0)
         return 0;
     hipLaunchKernelGGL(seq_exec_big_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
                        rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff ? 1u : 0u,
                        blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr, blk ? blk->jobs : nullptr,
-                       blk ? blk->jres : nullptr);
+                       blk ? blk->jres : nullptr, skip_jobs ? 1u : 0u);
 #ifdef ZSK_TUNING
     // ZSEEK_BIG_TIMERS: accumulate the phase cycles, print every 100 launches
     static const bool timers = getenv("ZSEEK_BIG_TIMERS") != nullptr;
@@ -866,6 +1235,33 @@ int launch_seq_exec_big(const FrameDesc *d_desc, uint32_t nframes, const uint8_t
                 "big execute cycles per frame: init %.0f items+scan %.0f cut+literals %.0f matches %.0f slides %.0f "
                 "output %.0f | slides %.2f batches %.2f (%llu frames)\n",
                 z[0] / fr, z[1] / fr, z[2] / fr, z[3] / fr, z[4] / fr, z[5] / fr, z[6] / fr, z[7] / fr, z[8]);
+    }
+#endif
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_seq_exec_blocks(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                           const uint64_t *rec_base, const uint64_t *items, hipStream_t stream, uint32_t stop_last,
+                           const SplitScratch *blk, uint32_t jobs)
+{
+    if (nframes == 0 || jobs == 0)
+        return 0;
+    hipLaunchKernelGGL(seq_exec_blocks_kernel, dim3(jobs), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
+                       rec_base, items, blk->bfirst, blk->jobs, blk->jres, blk->njobs, stop_last);
+#ifdef ZSK_TUNING
+    // ZSEEK_BLK_TIMERS: every 100th launch, each job's timeline in µs from the
+    // first job's start
+    static const bool timers = getenv("ZSEEK_BLK_TIMERS") != nullptr;
+    static int calls = 0;
+    if (timers && ++calls % 100 == 0) {
+        static unsigned long long z[64][6];
+        (void)hipStreamSynchronize(stream);
+        (void)hipMemcpyFromSymbol(z, HIP_SYMBOL(g_ktime), sizeof(z), 0, hipMemcpyDeviceToHost);
+        const unsigned long long t0 = z[0][0];
+        for (uint32_t k = 0; k < jobs && k < 64; k++)
+            fprintf(stderr, "blk %2u: start %6.2f A %6.2f wait %6.2f end %6.2f us | tainted matches %llu bytes %llu\n",
+                    k, (z[k][0] - t0) / 100.0, (z[k][1] - t0) / 100.0, (z[k][2] - t0) / 100.0,
+                    (z[k][3] - t0) / 100.0, z[k][4], z[k][5]);
     }
 #endif
     return hipGetLastError() == hipSuccess ? 0 : -1;

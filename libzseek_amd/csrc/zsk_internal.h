@@ -236,7 +236,13 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
 int launch_seq_exec_big(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                        bool handoff, const SplitScratch *blk);
+                        bool handoff, const SplitScratch *blk, bool skip_jobs = false);
+// ... the frames the block route accepted, block-parallel: a workgroup per
+// job of blk (a grid of `jobs`), then launch_seq_exec_big(..., skip_jobs)
+// for the rest (seq_exec.hip, seq_exec_blocks_kernel).
+int launch_seq_exec_blocks(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
+                           const uint64_t *rec_base, const uint64_t *items, hipStream_t stream, uint32_t stop_last,
+                           const SplitScratch *blk, uint32_t jobs);
 int launch_seq_exec_seg(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         const int32_t *d_status, hipStream_t stream, const SplitScratch *blk);
