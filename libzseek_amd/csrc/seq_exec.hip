@@ -783,37 +783,35 @@ __global__ __launch_bounds__(kFT) void seq_exec_big_kernel(
 // previous block's output, which its own workgroup is still producing; so:
 //   A. every workgroup executes its block at once with the previous block's
 //      bytes unknown: the frame kernel's literal copies and match passes over
-//      the block staged in LDS (block bytes [0, 64 KiB) at B; below B the
-//      history, garbage for now), a source byte before the block taken as
-//      ready and as *tainted*, and every match reading a tainted byte
-//      tainting its own (one bit per byte, set before the done bit, so a
-//      match that sees its source done sees its taint too) and going on a
-//      list in LDS;
-//   B. a block without tainted matches is final already; one with them waits
-//      for the previous block's workgroup to publish its final bytes
-//      (jres[j - 1].pad, release / acquire at agent scope), loads them as its
-//      history and re-runs just the listed matches, every untainted byte
-//      ready.  (A list past its capacity: the whole block again, after the
-//      wait.)
-// Workgroups wait only on lower-numbered ones, dispatched first, so the
-// chain always drains; the wait is bounded (~1 s) so a broken chain cannot
-// hang the GPU.  Tainted matches sit in a block's first bytes (its matches
-// reaching back) and whatever copies them, so the chain's serial part is
-// short.  The last frame stops at stop_last (later blocks skip).
-constexpr uint32_t kTaintList = 1024;   // tainted matches a block keeps (8 bytes each)
-
+//      the block staged in LDS (block byte x at B + x).  A byte copied from
+//      before the block, or from a byte so copied, is *tainted* (a bit per
+//      byte): it holds not its value but its *origin*, the previous block's
+//      byte it is a copy of, low byte at B + x and high byte at B - 64 KiB + x
+//      (the LDS below B, free in this kernel).  A match reading no tainted
+//      byte copies as usual; one that does goes byte by byte, carrying
+//      values and origins (taint bits set before the done bits, so a match
+//      that sees its source done sees its taint too);
+//   B. the untainted bytes are final and go out at once.  A block with tainted
+//      bytes then waits for the previous block's workgroup to publish its
+//      final bytes (jres[j - 1].pad, release / acquire at agent scope),
+//      gathers each tainted byte from its origin there, and writes those.
+// After the wait, phase B is one round of gathers (16 a thread), so the
+// chain of waits costs a few microseconds a block.  Workgroups wait only on
+// lower-numbered ones, dispatched first, so the chain always drains; the wait
+// is bounded (~1 s) so a broken chain cannot hang the GPU.  The last frame
+// stops at stop_last (later blocks skip).
 #ifdef ZSK_TUNING
 // tuning builds: seq_exec_blocks_kernel's timeline (ZSEEK_BLK_TIMERS), per
-// job < 64: realtime at start, after phase A, after the wait, at the end;
-// the tainted matches and bytes
-__device__ unsigned long long g_ktime[64][6];
+// job < 64: realtime at start, after phase A, after the untainted bytes went
+// out, after the wait, after the gather, at the end; the tainted matches and
+// bytes
+__device__ unsigned long long g_ktime[64][10];
 #define ZSK_KT(i)                                                             \
     if (t == 0 && j < 64)                                                     \
         g_ktime[j][i] = __builtin_amdgcn_s_memrealtime();
 #else
 #define ZSK_KT(i)
 #endif
-static_assert(kTaintList == kFT, "phase B takes one listed match per thread");
 
 __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
@@ -821,12 +819,11 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
     const uint32_t *__restrict__ bfirst, const BlockJob *__restrict__ jobs, BlockRes *__restrict__ jres,
     const uint32_t *__restrict__ njobs, uint32_t stop_last)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t ob[2 * kBWin + 80];   // history, then the block
+    __shared__ __attribute__((aligned(16))) uint8_t ob[2 * kBWin + 80];   // origins' high bytes, then the block
     __shared__ uint32_t done[kBWin / 32 + 2];
     __shared__ uint32_t taint[kBWin / 32 + 2];
-    __shared__ uint64_t tl[kTaintList];
     __shared__ uint32_t wsum[kFT / 64];
-    __shared__ uint32_t ntl, hi_end;
+    __shared__ uint32_t ntm, hi_end;
     const uint32_t j = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (j >= (uint32_t)__builtin_amdgcn_readfirstlane(*njobs))
         return;
@@ -860,7 +857,7 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         done[i] = taint[i] = 0;
     if (t == 0) {
         hi_end = 0;
-        ntl = 0;
+        ntm = 0;
     }
     __syncthreads();
 
@@ -911,8 +908,7 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         bits_or(done, a, len);
     };
-    // a match's copy inside the staged block (its source may reach into the
-    // history below B)
+    // a match reading no tainted byte: a plain copy inside the staged block
     auto copy_match = [&](uint32_t mb, uint32_t ov, uint32_t m) {
         const uint32_t db = B + mb, sb = db - ov;
         if (ov >= m && m <= 128) {
@@ -934,8 +930,52 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
             }
         }
     };
+    // one that does: the wave's 64 lanes a byte each, byte k's source
+    // s = mb - ov + k mod ov (before the match, so the bytes are independent;
+    // an overlapping match repeats its first ov source bytes), a byte before
+    // the block becoming the origin s + 64 KiB, a tainted one passing its
+    // origin on, an untainted one its value; the taint bits of 64 bytes at a
+    // time from a ballot
+    auto taint_wide = [&](uint32_t mb, uint32_t ov, uint32_t m) {
+        const int32_t s0 = (int32_t)mb - (int32_t)ov;
+        for (uint32_t k0 = 0; k0 < m; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const bool in = k < m;
+            bool tb = false;
+            if (in) {
+                const int32_t s = s0 + (int32_t)(ov >= m ? k : k % ov);
+                const uint32_t x = mb + k;
+                if (s < 0) {
+                    const uint32_t h = (uint32_t)(s + (int32_t)kBWin);
+                    *lp<uint8_t>(B + x) = (uint8_t)h;
+                    *lp<uint8_t>(ob0 + x) = (uint8_t)(h >> 8);
+                    tb = true;
+                } else {
+                    const uint32_t sx = (uint32_t)s;
+                    tb = (__hip_atomic_load(&taint[sx >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+                          (sx & 31)) & 1;
+                    *lp<uint8_t>(B + x) = *lp<uint8_t>(B + sx);
+                    if (tb)
+                        *lp<uint8_t>(ob0 + x) = *lp<uint8_t>(ob0 + sx);
+                }
+            }
+            const uint64_t bm = __ballot(tb);
+            if (lane == 0 && bm) {
+                const uint32_t x0 = mb + k0, w = x0 >> 5, sh = x0 & 31;
+                const uint64_t lo = bm << sh;
+                const uint32_t w2 = sh ? (uint32_t)(bm >> (64 - sh)) : 0u;
+                if ((uint32_t)lo)
+                    __hip_atomic_fetch_or(&taint[w], (uint32_t)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if ((uint32_t)(lo >> 32))
+                    __hip_atomic_fetch_or(&taint[w + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (w2)
+                    __hip_atomic_fetch_or(&taint[w + 2], w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    };
     // the readiness range of a match at mb: its source's first min(off, ml)
-    // bytes, clipped to the block (bytes before it: the history)
+    // bytes, clipped to the block (bytes before it: always "ready")
     auto src_range = [&](uint32_t mb, uint32_t ov, uint32_t m, uint32_t &a, uint32_t &len) -> bool {
         const int32_t s0 = (int32_t)mb - (int32_t)ov, s1 = s0 + (int32_t)(ov >= m ? m : ov);
         a = s0 > 0 ? (uint32_t)s0 : 0u;
@@ -943,9 +983,8 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         return s0 < 0;   // reaches before the block
     };
 
-    // ---- the block's items, batches of 2,048 (phase A, or the whole block
-    // again with the history in place: full) ----
-    auto run_items = [&](bool full) {
+    // ---- phase A: the block's items, batches of 2,048 ----
+    {
         uint32_t P = 0;
         for (uint32_t w0 = 0; w0 < nit && P < lim; w0 += 2 * kFT) {
             uint32_t lit[2], ml[2], off[2], src[2], op[2], tot[2];
@@ -1025,25 +1064,31 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
             for (uint32_t pass = 0;; pass++) {
                 bool moved = false;
                 for (int q = 0; q < 2; q++) {
-                    if (!pend[q])
-                        continue;
                     const uint32_t mb = op[q] + lit[q], ov = off[q], m = ml[q];
-                    uint32_t a, len;
-                    const bool before = src_range(mb, ov, m, a, len);
-                    if (len && !all_set(done, a, len))
-                        continue;
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    // phase A: bytes before the block, or tainted ones, taint it
-                    if (!full && (before || (len && any_set(taint, a, len)))) {
-                        bits_or(taint, mb, m);
-                        const uint32_t x = atomicAdd(&ntl, 1u);
-                        if (x < kTaintList)
-                            tl[x] = (uint64_t)mb | (uint64_t)m << 20 | (uint64_t)ov << 40;
+                    bool rdy = false, tnt = false;
+                    if (pend[q]) {
+                        uint32_t a, len;
+                        const bool before = src_range(mb, ov, m, a, len);
+                        rdy = !len || all_set(done, a, len);
+                        if (rdy) {
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                            tnt = before || (len && any_set(taint, a, len));
+                        }
                     }
-                    copy_match(mb, ov, m);
-                    mark(mb, m);
-                    pend[q] = false;
-                    moved = true;
+                    // tainted: the wave's lanes a byte each
+                    for (uint64_t lm = __ballot(rdy && tnt); lm; lm &= lm - 1) {
+                        const int qq = (int)__builtin_ctzll(lm);
+                        taint_wide(lane_val(mb, qq), lane_val(ov, qq), lane_val(m, qq));
+                    }
+                    if (rdy && !tnt)
+                        copy_match(mb, ov, m);
+                    if (rdy) {
+                        if (tnt)
+                            atomicAdd(&ntm, 1u);
+                        mark(mb, m);
+                        pend[q] = false;
+                        moved = true;
+                    }
                 }
                 if (!__any(pend[0] || pend[1]) || pass > (1u << 22))
                     break;
@@ -1053,26 +1098,52 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
             __syncthreads();
             P += tot[0] + tot[1];
         }
-    };
-    run_items(false);
-    __syncthreads();
-    const uint32_t nt = ntl;
-    ZSK_KT(1)
-    if (!nt)
-        ZSK_KT(2)
-#ifdef ZSK_TUNING
-    if (t == 0 && j < 64) {
-        uint32_t pc = 0;
-        for (uint32_t i = 0; i < kBWin / 32; i++)
-            pc += __builtin_popcount(taint[i]);
-        g_ktime[j][4] = nt;
-        g_ktime[j][5] = pc;
     }
-#endif
+    __syncthreads();
+    const uint32_t nt = ntm;
+    ZSK_KT(1)
+
+    // ---- phase B: the block's bytes [0, E) out at once (the tainted ones
+    // holding origins yet): a byte head to 16-byte alignment, whole 16-byte
+    // stores, a byte tail ----
+    const uint32_t E = min(hi_end, lim);
+    uint8_t *o = out + d.d_off + bop;
+    const uint32_t head = min(E, (uint32_t)((16 - ((uintptr_t)o & 15)) & 15));
+    const uint32_t nchunks = (E - head) / 16, tail0 = head + 16 * nchunks;
+    if (t < head)
+        o[t] = ob[kBWin + t];
+    for (uint32_t c = t; c < nchunks; c += kFT)
+        *reinterpret_cast<u32x4 *>(o + head + 16 * c) = lds16(B + head + 16 * c);
+    if (tail0 + t < E)
+        o[tail0 + t] = ob[kBWin + tail0 + t];
+    ZSK_KT(2)
     if (nt) {
-        // phase B: the previous block's final bytes as the history (a block
-        // with tainted matches is never the frame's first: nothing reaches
-        // before byte 0)
+        // the tainted bytes split evenly: ranks [r0, r1) a thread, found by a
+        // binary search over the taint words' prefix counts (in done[], dead
+        // now), before the wait
+        const uint32_t c0 = __builtin_popcount(taint[2 * t]), c1 = __builtin_popcount(taint[2 * t + 1]);
+        uint32_t T;
+        const uint32_t pre = scan(c0 + c1, T);
+        done[2 * t] = pre;
+        done[2 * t + 1] = pre + c0;
+        __syncthreads();
+        const uint32_t r0 = (uint32_t)((uint64_t)T * t / kFT), r1 = (uint32_t)((uint64_t)T * (t + 1) / kFT);
+        uint32_t w = 0, bits = 0;
+        if (r0 < r1) {
+            uint32_t hi = kBWin / 32;   // the last word w with done[w] <= r0 holds rank r0
+            while (hi - w > 1) {
+                const uint32_t mid = (w + hi) / 2;
+                if (done[mid] <= r0)
+                    w = mid;
+                else
+                    hi = mid;
+            }
+            bits = taint[w];
+            for (uint32_t k = r0 - done[w]; k; k--)
+                bits &= bits - 1;
+        }
+        // the previous block's final bytes (a block with tainted bytes is
+        // never the frame's first: nothing reaches before byte 0)
         if (t == 0 && j > j0) {
             uint32_t k = 0;
             while (__hip_atomic_load(&jres[j - 1].pad, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
@@ -1080,66 +1151,53 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
                 __builtin_amdgcn_s_sleep(2);
         }
         __syncthreads();
-        ZSK_KT(2)
+        ZSK_KT(3)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // each tainted byte from its origin, 16 gathers in flight a thread,
+        // stored over the origin the first write left
         const uint8_t *prev = out + d.d_off + (bop - kBWin);
-        for (uint32_t c = t; c < kBWin / 16; c += kFT)
-            *lp<u32x4>(ob0 + 16 * c) = *reinterpret_cast<const u32x4_l *>(prev + 16 * c);
-        if (nt > kTaintList) {
-            // the list overflowed: the block again, the history in place
-            for (uint32_t i = t; i < kBWin / 32 + 2; i += kFT)
-                done[i] = 0;
-            if (t == 0)
-                hi_end = 0;
-            __syncthreads();
-            run_items(true);
-        } else {
-            // untainted bytes final, tainted ones pending: the listed matches
-            // again, in passes over the done bits
-            for (uint32_t i = t; i < kBWin / 32 + 2; i += kFT)
-                done[i] = ~taint[i];
-            __syncthreads();
-            // (kTaintList = kFT entries: one per thread)
-            bool pend = t < nt;
-            const uint64_t e = pend ? tl[t] : 0;
-            const uint32_t mb = (uint32_t)e & 0xFFFFF, m = (uint32_t)(e >> 20) & 0xFFFFF,
-                           ov = (uint32_t)(e >> 40) & 0xFFFFF;
-            for (uint32_t pass = 0;; pass++) {
-                bool moved = false;
-                if (pend) {
-                    uint32_t a, len;
-                    (void)src_range(mb, ov, m, a, len);
-                    if (!len || all_set(done, a, len)) {
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                        copy_match(mb, ov, m);
-                        mark(mb, m);
-                        pend = false;
-                        moved = true;
-                    }
+        for (uint32_t r = r0; r < r1; r += 16) {
+            uint32_t v[16], xs[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++) {
+                xs[k] = ~0u;
+                v[k] = 0;
+                if (r + k < r1) {
+                    while (!bits)
+                        bits = taint[++w];
+                    const uint32_t x = 32 * w + __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    xs[k] = x;
+                    v[k] = prev[*lp<uint8_t>(B + x) | (uint32_t)*lp<uint8_t>(ob0 + x) << 8];
                 }
-                if (!__any(pend) || pass > (1u << 22))
-                    break;
-                if (!__any(moved))
-                    __builtin_amdgcn_s_sleep(1);
             }
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++)
+                if (xs[k] < E)
+                    o[xs[k]] = (uint8_t)v[k];
         }
+#ifdef ZSK_TUNING
         __syncthreads();
+#endif
+        ZSK_KT(4)
     }
-    // the block's decoded bytes out: a byte head to 16-byte alignment, whole
-    // 16-byte stores, a byte tail
-    const uint32_t E = min(hi_end, lim);
-    uint8_t *o = out + d.d_off + bop;
-    const uint32_t head = min(E, (uint32_t)((16 - ((uintptr_t)o & 15)) & 15));
-    if (t < head)
-        o[t] = ob[kBWin + t];
-    const uint32_t nchunks = (E - head) / 16;
-    for (uint32_t c = t; c < nchunks; c += kFT)
-        *reinterpret_cast<u32x4 *>(o + head + 16 * c) = lds16(B + head + 16 * c);
-    const uint32_t tail0 = head + 16 * nchunks;
-    if (tail0 + t < E)
-        o[tail0 + t] = ob[kBWin + tail0 + t];
+#ifdef ZSK_TUNING
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    ZSK_KT(6)
+    __syncthreads();
+    ZSK_KT(7)
+#endif
     publish();
-    ZSK_KT(3)
+    ZSK_KT(5)
+#ifdef ZSK_TUNING
+    if (t == 0 && j < 64) {
+        uint32_t pc = 0;
+        for (uint32_t i = 0; i < kBWin / 32; i++)
+            pc += __builtin_popcount(taint[i]);
+        g_ktime[j][8] = nt;
+        g_ktime[j][9] = pc;
+    }
+#endif
 }
 
 }   // namespace
@@ -1254,14 +1312,21 @@ int launch_seq_exec_blocks(const FrameDesc *d_desc, uint32_t nframes, const uint
     static const bool timers = getenv("ZSEEK_BLK_TIMERS") != nullptr;
     static int calls = 0;
     if (timers && ++calls % 100 == 0) {
-        static unsigned long long z[64][6];
+        static unsigned long long z[64][10];
         (void)hipStreamSynchronize(stream);
         (void)hipMemcpyFromSymbol(z, HIP_SYMBOL(g_ktime), sizeof(z), 0, hipMemcpyDeviceToHost);
         const unsigned long long t0 = z[0][0];
         for (uint32_t k = 0; k < jobs && k < 64; k++)
-            fprintf(stderr, "blk %2u: start %6.2f A %6.2f wait %6.2f end %6.2f us | tainted matches %llu bytes %llu\n",
-                    k, (z[k][0] - t0) / 100.0, (z[k][1] - t0) / 100.0, (z[k][2] - t0) / 100.0,
-                    (z[k][3] - t0) / 100.0, z[k][4], z[k][5]);
+            fprintf(stderr,
+                    "blk %2u: start %6.2f A %6.2f out %6.2f wait %6.2f gather %6.2f end %6.2f us | tainted matches "
+                    "%llu bytes %llu\n",
+                    k, (double)(long long)(z[k][0] - t0) / 100.0, (double)(long long)(z[k][1] - t0) / 100.0,
+                    (double)(long long)(z[k][2] - t0) / 100.0, (double)(long long)(z[k][3] - t0) / 100.0,
+                    (double)(long long)(z[k][4] - t0) / 100.0, (double)(long long)(z[k][5] - t0) / 100.0, z[k][8],
+                    z[k][9]);
+        for (uint32_t k = 0; k < jobs && k < 64; k++)
+            fprintf(stderr, "blk %2u: fence %6.2f barrier %6.2f\n", k, (double)(long long)(z[k][6] - t0) / 100.0,
+                    (double)(long long)(z[k][7] - t0) / 100.0);
     }
 #endif
     return hipGetLastError() == hipSuccess ? 0 : -1;

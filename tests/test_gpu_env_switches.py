@@ -11,7 +11,9 @@ error strings on the single-frame read cases of tests/env_switch_probe.py.
   ZSEEK_ONE_ROUTE=0   no one-frame route (the throughput kernels)
   ZSEEK_ONE_BIG=0     one-frame route, frames over 64 KiB: one sequential
                       parse and the wave execute (round 5) instead of the
-                      job parse and the windowed execute
+                      job parse and the block-parallel execute
+  ZSEEK_ONE_BLOCKS=0  ... the job parse, but the windowed execute
+                      (seq_exec_big_kernel) instead of the block-parallel one
   ZSEEK_DONE_FLAG=0   a small batch's completion by the stream's event only
                       (no pinned completion word, no results posted by the
                       one-frame execute)
@@ -28,7 +30,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SWITCHES = ["ZSEEK_HOST_DMA=1", "ZSEEK_ONE_FUSE=0", "ZSEEK_FRAME_HELP=0", "ZSEEK_ONE_WAVES=4",
-            "ZSEEK_ONE_ROUTE=0", "ZSEEK_ONE_BIG=0", "ZSEEK_DONE_FLAG=0"]
+            "ZSEEK_ONE_ROUTE=0", "ZSEEK_ONE_BIG=0", "ZSEEK_ONE_BLOCKS=0", "ZSEEK_DONE_FLAG=0"]
 
 
 def _probe(env_kv=None):
