@@ -58,10 +58,13 @@ __global__ __launch_bounds__(256) void lz4_plan_direct_kernel(const FrameDesc *_
                                                                uint64_t *__restrict__ total,
                                                                uint32_t *__restrict__ redo,
                                                                int32_t *__restrict__ status,
-                                                               uint32_t *__restrict__ fail_at)
+                                                               uint32_t *__restrict__ fail_at,
+                                                               uint32_t *__restrict__ zero)
 {
     __shared__ uint64_t part[256];
     __shared__ uint32_t last;
+    if (zero && blockIdx.x == 0 && threadIdx.x == 0)
+        *zero = 0;   // the block plan's job count (the block plan runs next)
     // at most kPlanGroups workgroups (the finish counter is one atomic per
     // workgroup: 4,096 of them cost 0.11 ms at 1,048,576 frames), each thread
     // striding over its frames
@@ -606,9 +609,8 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     if ((stages & 1) && !solo) {
         hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3(std::min<uint32_t>((nframes + 255) / 256, kPlanGroups)),
                            dim3(256), 0, stream, d_desc, nframes, s->rec_base, total_dev, s->redo, d_status,
-                           d_fail_at);
+                           d_fail_at, blk ? s->njobs : nullptr);
         if (blk) {
-            (void)hipMemsetAsync(s->njobs, 0, sizeof(uint32_t), stream);
             hipLaunchKernelGGL(lz4_block_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
                                nframes, d_comp, br.min_csize, s->bfirst, s->bcount, s->njobs, s->jobs, jlanes,
                                big ? 4u : 7u);
@@ -652,9 +654,10 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
             frame_handoff = (stages & 8) && (max_dsize <= 65536 || big);
             // a lone frame posts its results to the host itself (no download)
             const bool post_here = post && frame_handoff && nframes == 1 && !big;
-            launch_seq_exec_frames(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                                   d_fail_at, stream, stop_last, frame_handoff, nullptr,
-                                   post_here ? post : nullptr);
+            if (!(big && nframes == 1))   // (a lone big frame: nothing for it)
+                launch_seq_exec_frames(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
+                                       d_fail_at, stream, stop_last, frame_handoff, nullptr,
+                                       post_here ? post : nullptr);
             if (post_here && posted)
                 *posted = true;
             // (the accepted frames block-parallel, the others through the

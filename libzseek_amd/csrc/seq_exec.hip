@@ -1118,9 +1118,8 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         o[tail0 + t] = ob[kBWin + tail0 + t];
     ZSK_KT(2)
     if (nt) {
-        // the tainted bytes split evenly: ranks [r0, r1) a thread, found by a
-        // binary search over the taint words' prefix counts (in done[], dead
-        // now), before the wait
+        // the tainted bytes split evenly: ranks [r0, r1) a thread, over the
+        // taint words' prefix counts (in done[], dead now)
         const uint32_t c0 = __builtin_popcount(taint[2 * t]), c1 = __builtin_popcount(taint[2 * t + 1]);
         uint32_t T;
         const uint32_t pre = scan(c0 + c1, T);
@@ -1128,20 +1127,42 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         done[2 * t + 1] = pre + c0;
         __syncthreads();
         const uint32_t r0 = (uint32_t)((uint64_t)T * t / kFT), r1 = (uint32_t)((uint64_t)T * (t + 1) / kFT);
-        uint32_t w = 0, bits = 0;
-        if (r0 < r1) {
-            uint32_t hi = kBWin / 32;   // the last word w with done[w] <= r0 holds rank r0
-            while (hi - w > 1) {
-                const uint32_t mid = (w + hi) / 2;
-                if (done[mid] <= r0)
-                    w = mid;
-                else
-                    hi = mid;
+        // the next 16 ranks' bytes and origins, the first 16 before the wait:
+        // rank r's word the last w with done[w] <= r (16 interleaved binary
+        // searches), its bit the (r - done[w])-th set one (a select by halves)
+        uint32_t xs[16], og[16];
+        auto collect = [&](uint32_t r) {
+            uint32_t wk[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++)
+                wk[k] = 0;
+            for (uint32_t st = kBWin / 64; st; st >>= 1) {
+#pragma unroll
+                for (uint32_t k = 0; k < 16; k++)
+                    if (r + k < r1 && done[wk[k] + st] <= r + k)
+                        wk[k] += st;
             }
-            bits = taint[w];
-            for (uint32_t k = r0 - done[w]; k; k--)
-                bits &= bits - 1;
-        }
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++) {
+                xs[k] = ~0u;
+                og[k] = 0;
+                if (r + k < r1) {
+                    const uint32_t m = taint[wk[k]];
+                    uint32_t nb = r + k - done[wk[k]], pos = 0;
+                    for (uint32_t h = 16; h; h >>= 1) {
+                        const uint32_t c = __builtin_popcount((m >> pos) & ((1u << h) - 1));
+                        if (c <= nb) {
+                            nb -= c;
+                            pos += h;
+                        }
+                    }
+                    const uint32_t x = 32 * wk[k] + pos;
+                    xs[k] = x;
+                    og[k] = *lp<uint8_t>(B + x) | (uint32_t)*lp<uint8_t>(ob0 + x) << 8;
+                }
+            }
+        };
+        collect(r0);
         // the previous block's final bytes (a block with tainted bytes is
         // never the frame's first: nothing reaches before byte 0)
         if (t == 0 && j > j0) {
@@ -1156,25 +1177,18 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         // each tainted byte from its origin, 16 gathers in flight a thread,
         // stored over the origin the first write left
         const uint8_t *prev = out + d.d_off + (bop - kBWin);
-        for (uint32_t r = r0; r < r1; r += 16) {
-            uint32_t v[16], xs[16];
+        for (uint32_t r = r0; r < r1;) {
+            uint32_t v[16];
 #pragma unroll
-            for (uint32_t k = 0; k < 16; k++) {
-                xs[k] = ~0u;
-                v[k] = 0;
-                if (r + k < r1) {
-                    while (!bits)
-                        bits = taint[++w];
-                    const uint32_t x = 32 * w + __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    xs[k] = x;
-                    v[k] = prev[*lp<uint8_t>(B + x) | (uint32_t)*lp<uint8_t>(ob0 + x) << 8];
-                }
-            }
+            for (uint32_t k = 0; k < 16; k++)
+                v[k] = xs[k] != ~0u ? prev[og[k]] : 0u;
 #pragma unroll
             for (uint32_t k = 0; k < 16; k++)
                 if (xs[k] < E)
                     o[xs[k]] = (uint8_t)v[k];
+            r += 16;
+            if (r < r1)
+                collect(r);
         }
 #ifdef ZSK_TUNING
         __syncthreads();
