@@ -264,6 +264,10 @@ void split_scratch_free(SplitScratch *s)
         (void)hipFree(s->jobs);
     if (s->jres)
         (void)hipFree(s->jres);
+    if (s->borg)
+        (void)hipFree(s->borg);
+    if (s->btaint)
+        (void)hipFree(s->btaint);
     *s = SplitScratch();
 }
 
@@ -301,6 +305,28 @@ int block_scratch_reserve(SplitScratch *s, uint32_t frames, uint32_t jobs, hipSt
             return -1;
         s->jobs_cap = jobs;
     }
+    return 0;
+}
+
+// the block-parallel execute's scratch for `jobs` jobs (136 KiB each)
+constexpr uint32_t kOriginJobsMax = 1024;
+int origin_scratch_reserve(SplitScratch *s, uint32_t jobs, hipStream_t stream)
+{
+    if (jobs <= s->borg_cap)
+        return 0;
+    (void)hipStreamSynchronize(stream);
+    if (s->borg)
+        (void)hipFree(s->borg);
+    if (s->btaint)
+        (void)hipFree(s->btaint);
+    s->borg = nullptr;
+    s->btaint = nullptr;
+    s->borg_cap = 0;
+    const uint32_t cap = jobs < 16 ? 16 : jobs;
+    if (hipMalloc((void **)&s->borg, (size_t)cap * 65536 * sizeof(uint16_t)) != hipSuccess ||
+        hipMalloc((void **)&s->btaint, (size_t)cap * 2048 * sizeof(uint32_t)) != hipSuccess)
+        return -1;
+    s->borg_cap = cap;
     return 0;
 }
 
@@ -602,6 +628,21 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
         br = BlockRoute{true, 0, 1};
     if (br.on && block_scratch_reserve(s, nframes, jlanes, stream) != 0)
         br.on = big = false;   // no room: the chunk parse takes the frames as before
+    // the accepted big frames block-parallel (their jobs: at most
+    // ceil(max_dsize / 64 KiB) a frame; the device API's unknown sizes: the
+    // job lanes, at most kOriginJobsMax -- a frame with a job past the scratch
+    // goes through the window), the others through the window; env
+    // ZSEEK_ONE_BLOCKS=0 (or no room for the origins): all through the window
+    static const bool blocks_off = [] {
+        const char *v = getenv("ZSEEK_ONE_BLOCKS");
+        return v && !strcmp(v, "0");
+    }();
+    bool blocks = big && !blocks_off;
+    if (blocks) {
+        const uint64_t need = std::min<uint64_t>((uint64_t)nframes * (((uint64_t)max_dsize + 65535) / 65536),
+                                                 std::min<uint64_t>(jlanes, kOriginJobsMax));
+        blocks = origin_scratch_reserve(s, (uint32_t)need, stream) == 0;
+    }
     SplitScratch *blk = br.on ? s : nullptr;
     stage_mark(0, stream);
     // one frame on the one-frame route: the chunk kernel does the plan's work
@@ -660,18 +701,12 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                                        post_here ? post : nullptr);
             if (post_here && posted)
                 *posted = true;
-            // (the accepted frames block-parallel, the others through the
-            // window; env ZSEEK_ONE_BLOCKS=0: all through the window)
-            static const bool blocks_off = [] {
-                const char *v = getenv("ZSEEK_ONE_BLOCKS");
-                return v && !strcmp(v, "0");
-            }();
-            if (big && !blocks_off)
+            if (blocks)
                 launch_seq_exec_blocks(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, stream, stop_last, s,
                                        jlanes);
             if (big)
                 launch_seq_exec_big(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status,
-                                    d_fail_at, stream, stop_last, frame_handoff, s, !blocks_off);
+                                    d_fail_at, stream, stop_last, frame_handoff, s, blocks ? s->borg_cap : 0u);
             else if (max_dsize > 65536)
                 launch_seq_exec(d_desc, nframes, d_comp, d_out, s->rec_base, s->items, s->nitems, d_status, stream,
                                 0, nullptr, stop_last, 65537);

@@ -475,9 +475,13 @@ __global__ __launch_bounds__(kFT) void seq_exec_big_kernel(
     const FrameDesc d = desc[f];
     if (d.d_size <= kFMax)
         return;   // seq_exec_frame_kernel's frame
-    // (skip_jobs: a frame the block route accepted is seq_exec_blocks_kernel's)
-    if (skip_jobs && bfirst && (uint32_t)__builtin_amdgcn_readfirstlane(bfirst[f]) != kNoJob)
-        return;
+    // (a frame the block route accepted whose jobs are all below skip_jobs
+    // is seq_exec_blocks_kernel's)
+    if (skip_jobs && bfirst) {
+        const uint32_t bf = __builtin_amdgcn_readfirstlane(bfirst[f]);
+        if (bf != kNoJob && bf + (uint32_t)__builtin_amdgcn_readfirstlane(bcount[f]) <= skip_jobs)
+            return;
+    }
     // the windowed execute; false: stuck (an item longer than the window)
     auto window_frame = [&]() -> bool {
 #ifdef ZSK_TUNING
@@ -788,18 +792,26 @@ __global__ __launch_bounds__(kFT) void seq_exec_big_kernel(
 //      byte): it holds not its value but its *origin*, the previous block's
 //      byte it is a copy of, low byte at B + x and high byte at B - 64 KiB + x
 //      (the LDS below B, free in this kernel).  A match reading no tainted
-//      byte copies as usual; one that does goes byte by byte, carrying
-//      values and origins (taint bits set before the done bits, so a match
-//      that sees its source done sees its taint too);
-//   B. the untainted bytes are final and go out at once.  A block with tainted
-//      bytes then waits for the previous block's workgroup to publish its
-//      final bytes (jres[j - 1].pad, release / acquire at agent scope),
-//      gathers each tainted byte from its origin there, and writes those.
-// After the wait, phase B is one round of gathers (16 a thread), so the
-// chain of waits costs a few microseconds a block.  Workgroups wait only on
-// lower-numbered ones, dispatched first, so the chain always drains; the wait
-// is bounded (~1 s) so a broken chain cannot hang the GPU.  The last frame
-// stops at stop_last (later blocks skip).
+//      byte copies as usual; one that does carries values, origins and taint
+//      bits -- in 16-byte pieces on its lane, or (offsets < 16, matches over
+//      256 bytes) with the wave's 64 lanes a byte each (taint bits set before
+//      the done bits, so a match that sees its source done sees its taint
+//      too);
+//   B. the block goes out at once, its untainted bytes final, and its taint
+//      bits and origins go to the job's scratch (borg, btaint); then it
+//      publishes (jres[j].pad, release at agent scope).  A block with tainted
+//      bytes splits them evenly over its threads (binary searches over the
+//      taint words' prefix counts), waits for every earlier block of its frame
+//      to publish (acquire), and follows each tainted byte back block by block
+//      -- an untainted byte at (block, position) is the value, a tainted one
+//      names its origin one block further back -- then stores the values
+//      over the origins.
+// No block waits for another's final bytes: the wait is for phase A (all
+// blocks finish it about together) and a chain of h hops costs h load round
+// trips.  The waits are on lower-numbered workgroups, dispatched first, and
+// bounded (~1 s), so a broken chain cannot hang the GPU.  The last frame
+// stops at stop_last (later blocks skip).  A frame with a job at or past
+// borg_cap (the scratch's jobs) is left to seq_exec_big_kernel.
 #ifdef ZSK_TUNING
 // tuning builds: seq_exec_blocks_kernel's timeline (ZSEEK_BLK_TIMERS), per
 // job < 64: realtime at start, after phase A, after the untainted bytes went
@@ -817,7 +829,8 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp, uint8_t *__restrict__ out,
     const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ items,
     const uint32_t *__restrict__ bfirst, const BlockJob *__restrict__ jobs, BlockRes *__restrict__ jres,
-    const uint32_t *__restrict__ njobs, uint32_t stop_last)
+    const uint32_t *__restrict__ njobs, uint32_t stop_last, uint16_t *__restrict__ borg,
+    uint32_t *__restrict__ btaint, const uint32_t *__restrict__ bcount, uint32_t borg_cap)
 {
     __shared__ __attribute__((aligned(16))) uint8_t ob[2 * kBWin + 80];   // origins' high bytes, then the block
     __shared__ uint32_t done[kBWin / 32 + 2];
@@ -832,12 +845,12 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         return;
     const uint32_t f = J.f;
     const uint32_t j0 = __builtin_amdgcn_readfirstlane(bfirst[f]);
-    if (j0 == kNoJob)
-        return;   // re-parsed: seq_exec_big_kernel's frame
+    if (j0 == kNoJob || j0 + (uint32_t)__builtin_amdgcn_readfirstlane(bcount[f]) > borg_cap)
+        return;   // re-parsed, or jobs past the scratch: seq_exec_big_kernel's frame
     const FrameDesc d = desc[f];
     const uint32_t stop = f + 1 == n ? min(stop_last, d.d_size) : d.d_size;
     const uint32_t bop = J.bop;
-    auto publish = [&]() {   // this block's bytes are final
+    auto publish = [&]() {   // this block's phase A is out
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __syncthreads();
         if (t == 0)
@@ -974,6 +987,52 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
             }
         }
     };
+    // ... or, offset >= 16, by one lane in pieces of <= 16 bytes: a piece
+    // from before the block its 16 origins built in registers, one from the
+    // block its value and origin bytes and its 16 taint bits copied over
+    auto taint_copy = [&](uint32_t mb, uint32_t ov, uint32_t m) {
+        for (uint32_t k = 0; k < m;) {
+            const uint32_t x = mb + k;
+            const int32_t s = (int32_t)x - (int32_t)ov;
+            uint32_t n = min(16u, m - k), bits;
+            if (s < 0) {
+                n = min(n, (uint32_t)-s);
+                const uint32_t h0 = (uint32_t)(s + (int32_t)kBWin);
+                uint32_t lo[4], hi[4];
+#pragma unroll
+                for (uint32_t i = 0; i < 4; i++) {
+                    lo[i] = hi[i] = 0;
+#pragma unroll
+                    for (uint32_t b = 0; b < 4; b++) {
+                        const uint32_t h = h0 + 4 * i + b;
+                        lo[i] |= (h & 0xFF) << (8 * b);
+                        hi[i] |= (h >> 8) << (8 * b);
+                    }
+                }
+                lds_put(B + x, u32x4{lo[0], lo[1], lo[2], lo[3]}, n);
+                lds_put(ob0 + x, u32x4{hi[0], hi[1], hi[2], hi[3]}, n);
+                bits = (1u << n) - 1;
+            } else {
+                const uint32_t sx = (uint32_t)s;
+                const uint64_t w = (uint64_t)__hip_atomic_load(&taint[sx >> 5], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP) |
+                                   (uint64_t)__hip_atomic_load(&taint[(sx >> 5) + 1], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP) << 32;
+                bits = (uint32_t)(w >> (sx & 31)) & ((1u << n) - 1);
+                lds_put(B + x, lds16(B + sx), n);
+                if (bits)
+                    lds_put(ob0 + x, lds16(ob0 + sx), n);
+            }
+            if (bits) {
+                const uint64_t sh = (uint64_t)bits << (x & 31);
+                __hip_atomic_fetch_or(&taint[x >> 5], (uint32_t)sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if ((uint32_t)(sh >> 32))
+                    __hip_atomic_fetch_or(&taint[(x >> 5) + 1], (uint32_t)(sh >> 32), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            k += n;
+        }
+    };
     // the readiness range of a match at mb: its source's first min(off, ml)
     // bytes, clipped to the block (bytes before it: always "ready")
     auto src_range = [&](uint32_t mb, uint32_t ov, uint32_t m, uint32_t &a, uint32_t &len) -> bool {
@@ -1075,11 +1134,15 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
                             tnt = before || (len && any_set(taint, a, len));
                         }
                     }
-                    // tainted: the wave's lanes a byte each
-                    for (uint64_t lm = __ballot(rdy && tnt); lm; lm &= lm - 1) {
+                    // tainted: short offsets and long matches with the
+                    // wave's lanes a byte each, the others by their lane
+                    const bool wide = rdy && tnt && (ov < 16 || m > 256);
+                    for (uint64_t lm = __ballot(wide); lm; lm &= lm - 1) {
                         const int qq = (int)__builtin_ctzll(lm);
                         taint_wide(lane_val(mb, qq), lane_val(ov, qq), lane_val(m, qq));
                     }
+                    if (rdy && tnt && !wide)
+                        taint_copy(mb, ov, m);
                     if (rdy && !tnt)
                         copy_match(mb, ov, m);
                     if (rdy) {
@@ -1105,7 +1168,8 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
 
     // ---- phase B: the block's bytes [0, E) out at once (the tainted ones
     // holding origins yet): a byte head to 16-byte alignment, whole 16-byte
-    // stores, a byte tail ----
+    // stores, a byte tail; its taint bits and (with tainted bytes) its
+    // origins to the job's scratch; then published ----
     const uint32_t E = min(hi_end, lim);
     uint8_t *o = out + d.d_off + bop;
     const uint32_t head = min(E, (uint32_t)((16 - ((uintptr_t)o & 15)) & 15));
@@ -1116,6 +1180,29 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         *reinterpret_cast<u32x4 *>(o + head + 16 * c) = lds16(B + head + 16 * c);
     if (tail0 + t < E)
         o[tail0 + t] = ob[kBWin + tail0 + t];
+    for (uint32_t i = t; i < kBWin / 32; i += kFT)
+        btaint[(size_t)j * (kBWin / 32) + i] = taint[i];
+    if (nt) {
+        // origin of byte x as one u16 (low byte from the block plane, high
+        // from the plane below it), 16 bytes a thread a step
+        u32x4 *og = reinterpret_cast<u32x4 *>(borg + (size_t)j * kBWin);
+        for (uint32_t c = t; c < kBWin / 16; c += kFT) {
+            if (!((taint[c >> 1] >> (16 * (c & 1))) & 0xFFFF))
+                continue;   // (no tainted byte: no origin read)
+            const u32x4 lo = lds16(B + 16 * c), hi = lds16(ob0 + 16 * c);
+            const uint32_t l[4] = {lo.x, lo.y, lo.z, lo.w}, h[4] = {hi.x, hi.y, hi.z, hi.w};
+            uint32_t w[8];
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                w[2 * i] = (l[i] & 0xFF) | (h[i] & 0xFF) << 8 | (l[i] & 0xFF00) << 8 | (h[i] & 0xFF00) << 16;
+                w[2 * i + 1] = (l[i] >> 16 & 0xFF) | (h[i] >> 16 & 0xFF) << 8 | (l[i] >> 24) << 16 |
+                               (h[i] >> 24) << 24;
+            }
+            og[2 * c] = u32x4{w[0], w[1], w[2], w[3]};
+            og[2 * c + 1] = u32x4{w[4], w[5], w[6], w[7]};
+        }
+    }
+    publish();
     ZSK_KT(2)
     if (nt) {
         // the tainted bytes split evenly: ranks [r0, r1) a thread, over the
@@ -1127,23 +1214,24 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
         done[2 * t + 1] = pre + c0;
         __syncthreads();
         const uint32_t r0 = (uint32_t)((uint64_t)T * t / kFT), r1 = (uint32_t)((uint64_t)T * (t + 1) / kFT);
-        // the next 16 ranks' bytes and origins, the first 16 before the wait:
-        // rank r's word the last w with done[w] <= r (16 interleaved binary
-        // searches), its bit the (r - done[w])-th set one (a select by halves)
-        uint32_t xs[16], og[16];
+        // the next kG ranks' bytes and origins: rank r's word the last w
+        // with done[w] <= r (kG interleaved binary searches), its bit the
+        // (r - done[w])-th set one (a select by halves)
+        constexpr uint32_t kG = 8;
+        uint32_t xs[kG], og[kG];
         auto collect = [&](uint32_t r) {
-            uint32_t wk[16];
+            uint32_t wk[kG];
 #pragma unroll
-            for (uint32_t k = 0; k < 16; k++)
+            for (uint32_t k = 0; k < kG; k++)
                 wk[k] = 0;
             for (uint32_t st = kBWin / 64; st; st >>= 1) {
 #pragma unroll
-                for (uint32_t k = 0; k < 16; k++)
+                for (uint32_t k = 0; k < kG; k++)
                     if (r + k < r1 && done[wk[k] + st] <= r + k)
                         wk[k] += st;
             }
 #pragma unroll
-            for (uint32_t k = 0; k < 16; k++) {
+            for (uint32_t k = 0; k < kG; k++) {
                 xs[k] = ~0u;
                 og[k] = 0;
                 if (r + k < r1) {
@@ -1163,45 +1251,71 @@ __global__ __launch_bounds__(kFT) void seq_exec_blocks_kernel(
             }
         };
         collect(r0);
-        // the previous block's final bytes (a block with tainted bytes is
-        // never the frame's first: nothing reaches before byte 0)
-        if (t == 0 && j > j0) {
+        // every earlier block of the frame published (they finish phase A
+        // about together): a thread a block
+        if (t < j - j0) {
             uint32_t k = 0;
-            while (__hip_atomic_load(&jres[j - 1].pad, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+            while (__hip_atomic_load(&jres[j0 + t].pad, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
                    k++ < (1u << 24))
                 __builtin_amdgcn_s_sleep(2);
         }
         __syncthreads();
         ZSK_KT(3)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        // each tainted byte from its origin, 16 gathers in flight a thread,
-        // stored over the origin the first write left
-        const uint8_t *prev = out + d.d_off + (bop - kBWin);
+        // each tainted byte followed back block by block: at (block cb,
+        // position p) an untainted byte is the value, a tainted one sends it
+        // on to its origin in block cb - 1 (the taint word, the origin and the
+        // byte loaded together: one round trip a hop)
+        const uint8_t *fo = out + d.d_off;
         for (uint32_t r = r0; r < r1;) {
-            uint32_t v[16];
+            uint32_t cb[kG], val[kG];
+            bool pend[kG];
 #pragma unroll
-            for (uint32_t k = 0; k < 16; k++)
-                v[k] = xs[k] != ~0u ? prev[og[k]] : 0u;
+            for (uint32_t k = 0; k < kG; k++) {
+                cb[k] = j - 1;
+                val[k] = 0;
+                pend[k] = xs[k] != ~0u;
+            }
+            for (uint32_t hop = 0; hop <= j - j0; hop++) {
+                bool any = false;
+                uint32_t tw[kG], o2[kG], v[kG];
 #pragma unroll
-            for (uint32_t k = 0; k < 16; k++)
+                for (uint32_t k = 0; k < kG; k++) {
+                    if (pend[k]) {
+                        const uint32_t p = og[k], b = cb[k];
+                        tw[k] = btaint[(size_t)b * (kBWin / 32) + (p >> 5)];
+                        o2[k] = borg[(size_t)b * kBWin + p];
+                        v[k] = fo[(size_t)bop - (size_t)(j - b) * kBWin + p];
+                    }
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < kG; k++) {
+                    if (pend[k]) {
+                        if (!((tw[k] >> (og[k] & 31)) & 1)) {
+                            val[k] = v[k];
+                            pend[k] = false;
+                        } else if (cb[k] == j0) {
+                            pend[k] = false;   // (cannot happen: nothing reaches before a frame)
+                        } else {
+                            og[k] = o2[k];
+                            cb[k]--;
+                            any = true;
+                        }
+                    }
+                }
+                if (!any)
+                    break;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kG; k++)
                 if (xs[k] < E)
-                    o[xs[k]] = (uint8_t)v[k];
-            r += 16;
+                    o[xs[k]] = (uint8_t)val[k];
+            r += kG;
             if (r < r1)
                 collect(r);
         }
-#ifdef ZSK_TUNING
-        __syncthreads();
-#endif
         ZSK_KT(4)
     }
-#ifdef ZSK_TUNING
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    ZSK_KT(6)
-    __syncthreads();
-    ZSK_KT(7)
-#endif
-    publish();
     ZSK_KT(5)
 #ifdef ZSK_TUNING
     if (t == 0 && j < 64) {
@@ -1286,14 +1400,14 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
 int launch_seq_exec_big(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                        bool handoff, const SplitScratch *blk, bool skip_jobs)
+                        bool handoff, const SplitScratch *blk, uint32_t skip_jobs)
 {
     if (nframes == 0)
         return 0;
     hipLaunchKernelGGL(seq_exec_big_kernel, dim3(nframes), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
                        rec_base, items, nitems, d_status, d_fail_at, stop_last, handoff ? 1u : 0u,
                        blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr, blk ? blk->jobs : nullptr,
-                       blk ? blk->jres : nullptr, skip_jobs ? 1u : 0u);
+                       blk ? blk->jres : nullptr, skip_jobs);
 #ifdef ZSK_TUNING
     // ZSEEK_BIG_TIMERS: accumulate the phase cycles, print every 100 launches
     static const bool timers = getenv("ZSEEK_BIG_TIMERS") != nullptr;
@@ -1319,7 +1433,8 @@ int launch_seq_exec_blocks(const FrameDesc *d_desc, uint32_t nframes, const uint
     if (nframes == 0 || jobs == 0)
         return 0;
     hipLaunchKernelGGL(seq_exec_blocks_kernel, dim3(jobs), dim3(kFT), 0, stream, d_desc, nframes, d_comp, d_out,
-                       rec_base, items, blk->bfirst, blk->jobs, blk->jres, blk->njobs, stop_last);
+                       rec_base, items, blk->bfirst, blk->jobs, blk->jres, blk->njobs, stop_last, blk->borg,
+                       blk->btaint, blk->bcount, blk->borg_cap);
 #ifdef ZSK_TUNING
     // ZSEEK_BLK_TIMERS: every 100th launch, each job's timeline in µs from the
     // first job's start
@@ -1332,15 +1447,12 @@ int launch_seq_exec_blocks(const FrameDesc *d_desc, uint32_t nframes, const uint
         const unsigned long long t0 = z[0][0];
         for (uint32_t k = 0; k < jobs && k < 64; k++)
             fprintf(stderr,
-                    "blk %2u: start %6.2f A %6.2f out %6.2f wait %6.2f gather %6.2f end %6.2f us | tainted matches "
+                    "blk %2u: start %6.2f A %6.2f published %6.2f wait %6.2f resolved %6.2f end %6.2f us | tainted matches "
                     "%llu bytes %llu\n",
                     k, (double)(long long)(z[k][0] - t0) / 100.0, (double)(long long)(z[k][1] - t0) / 100.0,
                     (double)(long long)(z[k][2] - t0) / 100.0, (double)(long long)(z[k][3] - t0) / 100.0,
                     (double)(long long)(z[k][4] - t0) / 100.0, (double)(long long)(z[k][5] - t0) / 100.0, z[k][8],
                     z[k][9]);
-        for (uint32_t k = 0; k < jobs && k < 64; k++)
-            fprintf(stderr, "blk %2u: fence %6.2f barrier %6.2f\n", k, (double)(long long)(z[k][6] - t0) / 100.0,
-                    (double)(long long)(z[k][7] - t0) / 100.0);
     }
 #endif
     return hipGetLastError() == hipSuccess ? 0 : -1;

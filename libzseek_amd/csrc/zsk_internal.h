@@ -124,6 +124,11 @@ struct SplitScratch {
     BlockJob *jobs = nullptr;       // [jobs_cap]
     BlockRes *jres = nullptr;       // [jobs_cap]
     uint32_t bframes_cap = 0, jobs_cap = 0;
+    // the one-frame route's block-parallel execute: each job's phase-A
+    // origins (64 Ki u16) and taint bits (2 Ki words), allocated on first use
+    uint16_t *borg = nullptr;       // [borg_cap][65536]
+    uint32_t *btaint = nullptr;     // [borg_cap][2048]
+    uint32_t borg_cap = 0;
 };
 
 // Item slots frame descriptors need (host-side mirror of the plan kernel).
@@ -236,10 +241,11 @@ int launch_seq_exec_frames(const FrameDesc *d_desc, uint32_t nframes, const uint
 int launch_seq_exec_big(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                         const uint64_t *rec_base, const uint64_t *items, const uint32_t *nitems,
                         int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t stop_last,
-                        bool handoff, const SplitScratch *blk, bool skip_jobs = false);
-// ... the frames the block route accepted, block-parallel: a workgroup per
-// job of blk (a grid of `jobs`), then launch_seq_exec_big(..., skip_jobs)
-// for the rest (seq_exec.hip, seq_exec_blocks_kernel).
+                        bool handoff, const SplitScratch *blk, uint32_t skip_jobs = 0);
+// ... the frames the block route accepted whose jobs are all below
+// blk->borg_cap (the origin scratch), block-parallel: a workgroup per job of
+// blk (a grid of `jobs`), then launch_seq_exec_big(..., blk->borg_cap) for
+// the rest (seq_exec.hip, seq_exec_blocks_kernel).
 int launch_seq_exec_blocks(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp, uint8_t *d_out,
                            const uint64_t *rec_base, const uint64_t *items, hipStream_t stream, uint32_t stop_last,
                            const SplitScratch *blk, uint32_t jobs);
