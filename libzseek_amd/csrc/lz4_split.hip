@@ -42,6 +42,116 @@ namespace {
 
 using namespace lz4d;
 
+// ---- block route plan ---------------------------------------------------------
+// Lane per frame: a frame of > 64 KiB decoded and >= min_csize compressed
+// bytes whose header passes every check lz4_lean_kernel's hdr_status makes
+// (no checksum flags; content size, when present, equal to the seek table's
+// dSize) and whose block headers chain to an end mark at exactly c_size, with
+// at most kMaxBlockJobs blocks and a dSize those blocks can hold, gets one job
+// per block (reserved with one atomic, written in block order).  Every other
+// frame keeps kNoJob and the chunk parse decodes it as before; a reservation
+// past the job slots marks the slots it got as no job.
+__device__ __forceinline__ uint32_t xxh32_short(const uint8_t *c, uint32_t p, uint32_t n)
+{
+    uint32_t acc = 0x165667B1u + n, i = 0;
+    for (; i + 4 <= n; i += 4) {
+        const uint32_t w = c[p + i] | c[p + i + 1] << 8 | c[p + i + 2] << 16 | (uint32_t)c[p + i + 3] << 24;
+        acc += w * 0xC2B2AE3Du;
+        acc = ((acc << 17) | (acc >> 15)) * 0x27D4EB2Fu;
+    }
+    for (; i < n; i++) {
+        acc += c[p + i] * 0x165667B1u;
+        acc = ((acc << 11) | (acc >> 21)) * 0x9E3779B1u;
+    }
+    acc ^= acc >> 15;
+    acc *= 0x85EBCA77u;
+    acc ^= acc >> 13;
+    acc *= 0xC2B2AE3Du;
+    acc ^= acc >> 16;
+    return acc;
+}
+
+struct BlockPlanArgs {
+    const uint8_t *comp;
+    uint32_t min_csize;
+    uint32_t *bfirst, *bcount, *njobs;
+    BlockJob *jobs;
+    uint32_t jobs_cap, max_bsid;
+};
+
+__device__ void block_plan_frame(uint32_t f, const FrameDesc *__restrict__ desc, const BlockPlanArgs &A)
+{
+    const uint8_t *__restrict__ comp = A.comp;
+    uint32_t *__restrict__ bfirst = A.bfirst, *__restrict__ bcount = A.bcount, *__restrict__ njobs = A.njobs;
+    BlockJob *__restrict__ jobs = A.jobs;
+    const uint32_t min_csize = A.min_csize, jobs_cap = A.jobs_cap, max_bsid = A.max_bsid;
+    const FrameDesc d = desc[f];
+    bfirst[f] = kNoJob;
+    bcount[f] = 0;
+    const uint32_t clen = d.c_size;
+    if (d.d_size <= 65536 || clen < min_csize || clen < 15 || clen > 0x3FFFFFFFu)   // item positions: 30 bits
+        return;
+    const uint8_t *c = comp + d.c_off;
+    auto r32 = [&](uint32_t p) -> uint32_t {
+        return c[p] | c[p + 1] << 8 | c[p + 2] << 16 | (uint32_t)c[p + 3] << 24;
+    };
+    if (r32(0) != kLz4Magic)
+        return;
+    const uint32_t flg = c[4], bd = c[5];
+    if ((flg & 0xC0) != 0x40 || (flg & 0x16) || (bd & 0x8F) || ((bd >> 4) & 7) < 4 || ((bd >> 4) & 7) > max_bsid)
+        return;
+    const uint32_t csz = (flg >> 3) & 1, dictid = flg & 1;
+    const uint32_t hdr = 7 + 8 * csz + 4 * dictid;
+    if (clen < hdr + 4 || ((xxh32_short(c, 4, hdr - 5) >> 8) & 0xFF) != c[hdr - 1])
+        return;
+    if (csz && (r32(6) != d.d_size || r32(10) != 0))
+        return;
+    const uint32_t bsid = (bd >> 4) & 7, max_block = 1u << (8 + 2 * bsid);
+    uint32_t p = hdr, nb = 0;
+    for (;;) {
+        if (clen - p < 4)
+            return;
+        const uint32_t h = r32(p);
+        if (h == 0) {
+            if (clen - p != 4)
+                return;
+            break;
+        }
+        const uint32_t sz = h & 0x7FFFFFFFu;
+        if (sz == 0 || sz > max_block || sz > clen - p - 8 || ++nb > kMaxBlockJobs)
+            return;
+        p += 4 + sz;
+    }
+    if ((uint64_t)(nb - 1) * max_block >= d.d_size || (uint64_t)nb * max_block < d.d_size)
+        return;
+    const uint32_t base = atomicAdd(njobs, nb);
+    if (base >= jobs_cap || nb > jobs_cap - base) {
+        for (uint32_t i = base; i < jobs_cap && i - base < nb; i++)
+            jobs[i].f = kNoJob;
+        return;
+    }
+    const uint32_t info = bsid | ((flg >> 5) & 1) << 8;
+    p = hdr;
+    for (uint32_t j = 0; j < nb; j++) {
+        const uint32_t q = p + 4 + (r32(p) & 0x7FFFFFFFu);
+        const uint32_t so = j ? (p >> 3) & ~3u : 0;
+        const uint32_t se = j + 1 < nb ? (q >> 3) & ~3u : slots_of(clen);
+        jobs[base + j] = BlockJob{f, p, q, so, se - so, info, j * max_block, 0};
+        p = q;
+    }
+    bfirst[f] = base;
+    bcount[f] = nb;
+}
+
+__global__ __launch_bounds__(256) void lz4_block_plan_kernel(const FrameDesc *__restrict__ desc, uint32_t n,
+                                                              BlockPlanArgs A)
+{
+    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+    if (f < n)
+        block_plan_frame(f, desc, A);
+}
+
+
 // ---- plan: per-frame item slot offsets ------------------------------------
 constexpr uint32_t kPlanGroups = 256;
 // Slot offsets without a scan (the usual case): when the frames lie in order
@@ -59,12 +169,21 @@ __global__ __launch_bounds__(256) void lz4_plan_direct_kernel(const FrameDesc *_
                                                                uint32_t *__restrict__ redo,
                                                                int32_t *__restrict__ status,
                                                                uint32_t *__restrict__ fail_at,
-                                                               uint32_t *__restrict__ zero)
+                                                               BlockPlanArgs bp)
 {
     __shared__ uint64_t part[256];
     __shared__ uint32_t last;
-    if (zero && blockIdx.x == 0 && threadIdx.x == 0)
-        *zero = 0;   // the block plan's job count (the block plan runs next)
+    // the block plan's job count zeroed (bp.njobs): the block plan runs next,
+    // or -- one workgroup and bp.bfirst set -- here, a lane per frame, behind
+    // a barrier (one launch less: a small batch's block plan is one lane's
+    // walk over a frame's block headers)
+    if (bp.njobs && blockIdx.x == 0 && threadIdx.x == 0)
+        *bp.njobs = 0;
+    if (bp.bfirst && gridDim.x == 1) {
+        __syncthreads();
+        for (uint32_t f = threadIdx.x; f < n; f += 256)
+            block_plan_frame(f, desc, bp);
+    }
     // at most kPlanGroups workgroups (the finish counter is one atomic per
     // workgroup: 4,096 of them cost 0.11 ms at 1,048,576 frames), each thread
     // striding over its frames
@@ -125,103 +244,6 @@ __global__ __launch_bounds__(256) void lz4_plan_direct_kernel(const FrameDesc *_
     }
 }
 
-// ---- block route plan ---------------------------------------------------------
-// Lane per frame: a frame of > 64 KiB decoded and >= min_csize compressed
-// bytes whose header passes every check lz4_lean_kernel's hdr_status makes
-// (no checksum flags; content size, when present, equal to the seek table's
-// dSize) and whose block headers chain to an end mark at exactly c_size, with
-// at most kMaxBlockJobs blocks and a dSize those blocks can hold, gets one job
-// per block (reserved with one atomic, written in block order).  Every other
-// frame keeps kNoJob and the chunk parse decodes it as before; a reservation
-// past the job slots marks the slots it got as no job.
-__device__ __forceinline__ uint32_t xxh32_short(const uint8_t *c, uint32_t p, uint32_t n)
-{
-    uint32_t acc = 0x165667B1u + n, i = 0;
-    for (; i + 4 <= n; i += 4) {
-        const uint32_t w = c[p + i] | c[p + i + 1] << 8 | c[p + i + 2] << 16 | (uint32_t)c[p + i + 3] << 24;
-        acc += w * 0xC2B2AE3Du;
-        acc = ((acc << 17) | (acc >> 15)) * 0x27D4EB2Fu;
-    }
-    for (; i < n; i++) {
-        acc += c[p + i] * 0x165667B1u;
-        acc = ((acc << 11) | (acc >> 21)) * 0x9E3779B1u;
-    }
-    acc ^= acc >> 15;
-    acc *= 0x85EBCA77u;
-    acc ^= acc >> 13;
-    acc *= 0xC2B2AE3Du;
-    acc ^= acc >> 16;
-    return acc;
-}
-
-__global__ __launch_bounds__(256) void lz4_block_plan_kernel(const FrameDesc *__restrict__ desc, uint32_t n,
-                                                              const uint8_t *__restrict__ comp, uint32_t min_csize,
-                                                              uint32_t *__restrict__ bfirst,
-                                                              uint32_t *__restrict__ bcount,
-                                                              uint32_t *__restrict__ njobs,
-                                                              BlockJob *__restrict__ jobs, uint32_t jobs_cap,
-                                                              uint32_t max_bsid)
-{
-    const uint32_t f = blockIdx.x * 256 + threadIdx.x;
-    if (f >= n)
-        return;
-    const FrameDesc d = desc[f];
-    bfirst[f] = kNoJob;
-    bcount[f] = 0;
-    const uint32_t clen = d.c_size;
-    if (d.d_size <= 65536 || clen < min_csize || clen < 15 || clen > 0x3FFFFFFFu)   // item positions: 30 bits
-        return;
-    const uint8_t *c = comp + d.c_off;
-    auto r32 = [&](uint32_t p) -> uint32_t {
-        return c[p] | c[p + 1] << 8 | c[p + 2] << 16 | (uint32_t)c[p + 3] << 24;
-    };
-    if (r32(0) != kLz4Magic)
-        return;
-    const uint32_t flg = c[4], bd = c[5];
-    if ((flg & 0xC0) != 0x40 || (flg & 0x16) || (bd & 0x8F) || ((bd >> 4) & 7) < 4 || ((bd >> 4) & 7) > max_bsid)
-        return;
-    const uint32_t csz = (flg >> 3) & 1, dictid = flg & 1;
-    const uint32_t hdr = 7 + 8 * csz + 4 * dictid;
-    if (clen < hdr + 4 || ((xxh32_short(c, 4, hdr - 5) >> 8) & 0xFF) != c[hdr - 1])
-        return;
-    if (csz && (r32(6) != d.d_size || r32(10) != 0))
-        return;
-    const uint32_t bsid = (bd >> 4) & 7, max_block = 1u << (8 + 2 * bsid);
-    uint32_t p = hdr, nb = 0;
-    for (;;) {
-        if (clen - p < 4)
-            return;
-        const uint32_t h = r32(p);
-        if (h == 0) {
-            if (clen - p != 4)
-                return;
-            break;
-        }
-        const uint32_t sz = h & 0x7FFFFFFFu;
-        if (sz == 0 || sz > max_block || sz > clen - p - 8 || ++nb > kMaxBlockJobs)
-            return;
-        p += 4 + sz;
-    }
-    if ((uint64_t)(nb - 1) * max_block >= d.d_size || (uint64_t)nb * max_block < d.d_size)
-        return;
-    const uint32_t base = atomicAdd(njobs, nb);
-    if (base >= jobs_cap || nb > jobs_cap - base) {
-        for (uint32_t i = base; i < jobs_cap && i - base < nb; i++)
-            jobs[i].f = kNoJob;
-        return;
-    }
-    const uint32_t info = bsid | ((flg >> 5) & 1) << 8;
-    p = hdr;
-    for (uint32_t j = 0; j < nb; j++) {
-        const uint32_t q = p + 4 + (r32(p) & 0x7FFFFFFFu);
-        const uint32_t so = j ? (p >> 3) & ~3u : 0;
-        const uint32_t se = j + 1 < nb ? (q >> 3) & ~3u : slots_of(clen);
-        jobs[base + j] = BlockJob{f, p, q, so, se - so, info, j * max_block, 0};
-        p = q;
-    }
-    bfirst[f] = base;
-    bcount[f] = nb;
-}
 
 }   // namespace
 
@@ -648,14 +670,23 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     // one frame on the one-frame route: the chunk kernel does the plan's work
     const bool solo = one && nframes == 1 && (stages & 3) == 3 && !big;
     if ((stages & 1) && !solo) {
-        hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3(std::min<uint32_t>((nframes + 255) / 256, kPlanGroups)),
-                           dim3(256), 0, stream, d_desc, nframes, s->rec_base, total_dev, s->redo, d_status,
-                           d_fail_at, blk ? s->njobs : nullptr);
+        const uint32_t pgroups = std::min<uint32_t>((nframes + 255) / 256, kPlanGroups);
+        BlockPlanArgs bp{d_comp, br.min_csize, nullptr, nullptr, nullptr, nullptr, jlanes, big ? 4u : 7u};
         if (blk) {
-            hipLaunchKernelGGL(lz4_block_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
-                               nframes, d_comp, br.min_csize, s->bfirst, s->bcount, s->njobs, s->jobs, jlanes,
-                               big ? 4u : 7u);
+            bp.bfirst = s->bfirst;
+            bp.bcount = s->bcount;
+            bp.njobs = s->njobs;
+            bp.jobs = s->jobs;
         }
+        // (one plan workgroup: the block plan inside it)
+        BlockPlanArgs pbp = bp;
+        if (pgroups != 1)
+            pbp.bfirst = nullptr;
+        hipLaunchKernelGGL(lz4_plan_direct_kernel, dim3(pgroups), dim3(256), 0, stream, d_desc, nframes, s->rec_base,
+                           total_dev, s->redo, d_status, d_fail_at, pbp);
+        if (blk && pgroups != 1)
+            hipLaunchKernelGGL(lz4_block_plan_kernel, dim3((nframes + 255) / 256), dim3(256), 0, stream, d_desc,
+                               nframes, bp);
     }
     stage_mark(1, stream);
     // parse: each kernel takes the frames of its compressed-size range and
