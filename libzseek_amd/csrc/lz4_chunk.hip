@@ -652,6 +652,13 @@ __device__ __forceinline__ uint32_t hdr_xxh32(const Src &S, Win &W, uint32_t n)
 constexpr uint32_t kOneStage = 65536 + 1024;   // bytes: frames of <= kOneStage - 64 compressed
 constexpr uint32_t kWinQ = 4;                  // window: 16-byte pieces per lane
 
+// frame f's first item slot when the batch's frames lie in order (the plan's
+// direct layout)
+__device__ __forceinline__ uint64_t solo_slots(const FrameDesc *__restrict__ desc, uint32_t f)
+{
+    return (((desc[f].c_off - desc[0].c_off) >> 3) + 40ull * f + 3) & ~3ull;
+}
+
 template <bool ONE, uint32_t OW = 4>
 __global__ __launch_bounds__(64 * (ONE ? OW : kCW)) void lz4_chunk_kernel(
     const FrameDesc *__restrict__ desc, uint32_t n, const uint8_t *__restrict__ comp,
@@ -703,12 +710,16 @@ __global__ __launch_bounds__(64 * (ONE ? OW : kCW)) void lz4_chunk_kernel(
             }
         }
         __syncthreads();
-        // a batch of one frame launches no plan kernel (solo_total != null):
-        // its slots start at 0 and the total the plan would report is this
-        // frame's; status and fail_at are written below whatever happens
+        // a batch whose frames the caller laid out in order launches no plan
+        // kernel (solo_total != null): each workgroup writes its frame's slot
+        // offset by the plan's in-order formula (lz4_plan_direct_kernel), the
+        // last frame's the total the plan would report; status and fail_at
+        // are written below whatever happens
         if (solo_total && lane == 0) {
-            const_cast<uint64_t *>(rec_base)[0] = 0;
-            *solo_total = slots_of(d.c_size);
+            const uint64_t r = solo_slots(desc, f);
+            const_cast<uint64_t *>(rec_base)[f] = r;
+            if (f + 1 == n)
+                *solo_total = r + slots_of(d.c_size);
         }
         ZSK_CT(0)
     }
@@ -767,7 +778,7 @@ __global__ __launch_bounds__(64 * (ONE ? OW : kCW)) void lz4_chunk_kernel(
                 return;
         }
     }
-    const uint64_t rb0 = (ONE && solo_total) ? 0 : rec_base[f];
+    const uint64_t rb0 = (ONE && solo_total) ? solo_slots(desc, f) : rec_base[f];
     const uint32_t cap = slots_of(d.c_size);
     const uint32_t clen = d.c_size, dlen = d.d_size;
     const uint32_t mapbase = (uint32_t)(uintptr_t)(maps) + w * (64 * kMapW * 4);
@@ -1097,13 +1108,13 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                                d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize,
                                blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr, blk ? blk->jobs : nullptr,
                                blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr, min_jobs,
-                               nframes == 1 ? solo_total : nullptr, 1u, one_lead());
+                               solo_total, 1u, one_lead());
         else
             hipLaunchKernelGGL((lz4_chunk_kernel<true, 4>), dim3(nframes), dim3(64 * 4), 0, stream, d_desc, nframes,
                                d_comp, rec_base, capacity, items, nitems, d_status, d_fail_at, min_csize,
                                blk ? blk->bfirst : nullptr, blk ? blk->bcount : nullptr, blk ? blk->jobs : nullptr,
                                blk ? blk->jres : nullptr, blk ? blk->njobs : nullptr, min_jobs,
-                               nframes == 1 ? solo_total : nullptr, 1u, one_lead());
+                               solo_total, 1u, one_lead());
 #ifdef ZSK_TUNING
         if (getenv("ZSEEK_CHUNK_TIMERS")) {
             unsigned long long z[16];

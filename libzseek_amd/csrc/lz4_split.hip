@@ -621,7 +621,7 @@ const char *parse_kernel_name(uint32_t nframes, uint32_t c_size, int route)
 int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d_comp,
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                      hipStream_t stream, SplitScratch *s, int route, int stages, int tune, uint32_t stop_last,
-                     uint32_t max_dsize, const HostPost *post, bool *posted)
+                     uint32_t max_dsize, const HostPost *post, bool *posted, bool in_order)
 {
     if (posted)
         *posted = false;
@@ -668,7 +668,9 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
     SplitScratch *blk = br.on ? s : nullptr;
     stage_mark(0, stream);
     // one frame on the one-frame route: the chunk kernel does the plan's work
-    const bool solo = one && nframes == 1 && (stages & 3) == 3 && !big;
+    // (frames in order: a lone frame, or the caller says so -- the reader's
+    // batches are file order)
+    const bool solo = one && (nframes == 1 || in_order) && (stages & 3) == 3 && !big;
     if ((stages & 1) && !solo) {
         const uint32_t pgroups = std::min<uint32_t>((nframes + 255) / 256, kPlanGroups);
         BlockPlanArgs bp{d_comp, br.min_csize, nullptr, nullptr, nullptr, nullptr, jlanes, big ? 4u : 7u};

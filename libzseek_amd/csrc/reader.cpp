@@ -559,7 +559,7 @@ bool submit(LaneJob &J, Slot &s, size_t f0, size_t f1)
             bool posted = false;
             if (launch_lz4_split(d_desc, (uint32_t)n, s.d_comp, s.d_out, s.d_status, d_fail, s.stream, &s.split,
                                  ROUTE_AUTO, 15, 0, stop_last, max_dsize, want_post ? &post : nullptr,
-                                 &posted) != 0)
+                                 &posted, true) != 0)
                 e = hipErrorLaunchFailure;
             s.flagged = posted;
         }

@@ -171,8 +171,10 @@ int launch_lz4_split(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                      uint8_t *d_out, int32_t *d_status, uint32_t *d_fail_at,
                      hipStream_t stream, SplitScratch *s, int route = ROUTE_AUTO, int stages = 15,
                      int tune = 0, uint32_t stop_last = 0xFFFFFFFFu, uint32_t max_dsize = 0xFFFFFFFFu,
-                     const HostPost *post = nullptr, bool *posted = nullptr);
-// (max_dsize: the batch's largest decoded frame when the caller knows it --
+                     const HostPost *post = nullptr, bool *posted = nullptr, bool in_order = false);
+// (in_order: the caller laid the frames out in order in d_comp -- the
+// one-frame route's chunk parse then does the plan's work, no plan launch.
+// max_dsize: the batch's largest decoded frame when the caller knows it --
 // the one-frame route then skips the wave execute for frames of <= 64 KiB.
 // post: a one-frame batch's results to the host from its execute, when the
 // batch takes that route (*posted = true; else the caller downloads))
@@ -412,8 +414,9 @@ int launch_lz4_chunk(const FrameDesc *d_desc, uint32_t nframes, const uint8_t *d
                      int32_t *d_status, uint32_t *d_fail_at, hipStream_t stream, uint32_t min_csize,
                      SplitScratch *blk = nullptr, uint32_t min_jobs = 0, bool one = false,
                      uint64_t *solo_total = nullptr);
-// (one && nframes == 1 && solo_total: the batch has no plan launch; the
-// kernel lays the frame's slots out itself and reports their total there)
+// (one && solo_total: the batch has no plan launch -- one frame, or frames
+// the caller laid out in order; each workgroup lays its frame's slots out by
+// the plan's in-order formula and the last reports their total there)
 // Frames of at least chunk_parse_min(nframes) compressed bytes go to the
 // chunk parse: with >= 32768 frames the lane-per-frame scan has a lane for
 // every frame it needs and wins on 64 KiB frames (2.07 vs 4.18 ms parse at
